@@ -1,0 +1,185 @@
+"""ctypes binding of the C-ABI in include/abnn/abnn.h (libabnn_hip.so).
+
+The library is built in-tree by ``abnn_amd.build.build_hip()`` (hipcc,
+--offload-arch=gfx950).  There is no fallback: if the shared object is missing
+or does not export the ABI, importing the product fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libabnn_hip.so")
+
+SUMMARY_WORDS = 4
+
+
+class Dims(C.Structure):
+    """abnn_dims -- Brain(nInput, nOutput, nHidden, nSynapses, eventsPerPass), brain.h:27-31."""
+
+    _fields_ = [
+        ("n_input", C.c_uint32),
+        ("n_output", C.c_uint32),
+        ("n_hidden", C.c_uint64),
+        ("n_syn", C.c_uint64),
+        ("events_per_pass", C.c_uint64),
+        ("syn_offset", C.c_uint64),
+        ("global_events", C.c_uint64),
+    ]
+
+
+class Params(C.Structure):
+    """abnn_params -- every knob of brain.metal:22-31, constants.h:16-19, brain.h:17-19."""
+
+    _fields_ = [
+        ("base_scale", C.c_float),
+        ("refractory", C.c_uint32),
+        ("window_pre", C.c_uint32),
+        ("clock_inc", C.c_uint32),
+        ("target_rate_hz", C.c_float),
+        ("eta_home", C.c_float),
+        ("eta_reward", C.c_float),
+        ("alpha_rbar", C.c_float),
+        ("a_ltp", C.c_float),
+        ("a_ltd", C.c_float),
+        ("w_min", C.c_float),
+        ("w_max", C.c_float),
+        ("max_spikes", C.c_uint32),
+        ("tick_ns", C.c_uint32),
+        ("tau_vis", C.c_uint32),
+        ("tau_pre", C.c_uint32),
+        ("renorm_thresh", C.c_uint64),
+        ("track_visits", C.c_uint32),
+        ("reserved0", C.c_uint32),
+        ("seed", C.c_uint64),
+    ]
+
+
+class Scalars(C.Structure):
+    _fields_ = [("clock", C.c_uint64), ("reward", C.c_float), ("rbar", C.c_float)]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("passes", C.c_uint64),
+        ("events", C.c_uint64),
+        ("pre_gated", C.c_uint64),
+        ("post_gated", C.c_uint64),
+        ("updated", C.c_uint64),
+        ("fired", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class State(C.Structure):
+    _fields_ = [
+        ("synapses", C.c_void_p),
+        ("last_fired", C.c_void_p),
+        ("last_visited", C.c_void_p),
+        ("clock", C.c_void_p),
+        ("reward", C.c_void_p),
+        ("rbar", C.c_void_p),
+    ]
+
+
+class AbnnError(RuntimeError):
+    def __init__(self, fn: str, status: int, msg: str):
+        super().__init__(f"{fn} failed: status {status} ({msg})")
+        self.status = status
+
+
+# Every symbol include/abnn/abnn.h declares: (name, restype, argtypes).
+_VP, _U32, _U64, _I32, _F = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_float
+_PU64, _PU32 = C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)
+SIGNATURES = [
+    ("abnn_abi_version", C.c_int, []),
+    ("abnn_status_string", C.c_char_p, [C.c_int]),
+    ("abnn_last_error", C.c_char_p, []),
+    ("abnn_default_params", None, [C.POINTER(Params)]),
+    ("abnn_device_count", C.c_int, []),
+    ("abnn_brain_create", C.c_int, [C.POINTER(Dims), C.POINTER(Params), C.c_int, C.POINTER(_VP)]),
+    ("abnn_brain_destroy", C.c_int, [_VP]),
+    ("abnn_get_dims", C.c_int, [_VP, C.POINTER(Dims)]),
+    ("abnn_get_params", C.c_int, [_VP, C.POINTER(Params)]),
+    ("abnn_state_ptrs", C.c_int, [_VP, C.POINTER(State)]),
+    ("abnn_n_neuron", C.c_uint64, [_VP]),
+    ("abnn_upload_synapses", C.c_int, [_VP, _U64, _VP, _U64]),
+    ("abnn_download_synapses", C.c_int, [_VP, _U64, _VP, _U64]),
+    ("abnn_generate_synapses", C.c_int, [_VP, _U64]),
+    ("abnn_checksum_synapses", C.c_int, [_VP, _PU64]),
+    ("abnn_get_last_fired", C.c_int, [_VP, _U64, _VP, _U64]),
+    ("abnn_set_last_fired", C.c_int, [_VP, _U64, _VP, _U64]),
+    ("abnn_get_last_visited", C.c_int, [_VP, _U64, _VP, _U64]),
+    ("abnn_set_last_visited", C.c_int, [_VP, _U64, _VP, _U64]),
+    ("abnn_set_timestamps", C.c_int, [_VP, _VP, _U64, _U64]),
+    ("abnn_get_scalars", C.c_int, [_VP, C.POINTER(Scalars)]),
+    ("abnn_set_scalars", C.c_int, [_VP, C.POINTER(Scalars)]),
+    ("abnn_set_reward", C.c_int, [_VP, _F]),
+    ("abnn_inject_inputs", C.c_int, [_VP, _VP, _U32, _F]),
+    ("abnn_read_outputs", C.c_int, [_VP, _VP, _U32]),
+    ("abnn_set_auto_stimulus", C.c_int, [_VP, _U64, _U64]),
+    ("abnn_traverse", C.c_int, [_VP, _U32, _VP]),
+    ("abnn_synchronize", C.c_int, [_VP, _VP]),
+    ("abnn_shard_gate", C.c_int, [_VP, _VP, _VP]),
+    ("abnn_shard_apply", C.c_int, [_VP, _VP, _U32, _U32, _VP, _VP]),
+    ("abnn_shard_commit", C.c_int, [_VP, _VP, _U32, _VP, _VP]),
+    ("abnn_get_stats", C.c_int, [_VP, C.POINTER(Stats)]),
+    ("abnn_reset_stats", C.c_int, [_VP]),
+    ("abnn_enable_timing", C.c_int, [_VP, C.c_int]),
+    ("abnn_get_kernel_time", C.c_int, [_VP, C.POINTER(C.c_double), _PU64]),
+    ("abnn_save_bnn", C.c_int, [_VP, C.c_char_p]),
+    ("abnn_load_bnn", C.c_int, [_VP, C.c_char_p]),
+    ("abnn_save_flat", C.c_int, [_VP, C.c_char_p]),
+    ("abnn_load_flat", C.c_int, [_VP, C.c_char_p]),
+]
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libabnn_hip.so (built in-tree); raise if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback for the traversal engine)")
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)  # AttributeError = the ABI is not exported
+        fn.restype = res
+        fn.argtypes = args
+    if lib.abnn_abi_version() != 1:
+        raise ImportError("libabnn_hip.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(fn_name: str, status: int) -> None:
+    if status != 0:
+        lib = load()
+        msg = lib.abnn_last_error().decode(errors="replace")
+        raise AbnnError(fn_name, status, msg)
+
+
+def call(fn_name: str, *args) -> None:
+    lib = load()
+    check(fn_name, getattr(lib, fn_name)(*args))
+
+
+def default_params(**overrides) -> Params:
+    p = Params()
+    load().abnn_default_params(C.byref(p))
+    for k, v in overrides.items():
+        if not hasattr(p, k):
+            raise KeyError(k)
+        setattr(p, k, v)
+    return p
+
+
+def device_count() -> int:
+    return int(load().abnn_device_count())

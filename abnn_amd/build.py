@@ -1,0 +1,84 @@
+"""In-tree build of the HIP library (and, for the test harness, the oracle).
+
+* ``build_hip()``    : hipcc --offload-arch=gfx950 -> abnn_amd/libabnn_hip.so
+* ``build_oracle()`` : gcc -> oracle/liboracle.so (test infrastructure)
+* ``build_cpp_example()`` : g++ -> tests/cpp/brain_cpp_test (C++ Brain API over the C-ABI)
+
+All fp32 code is compiled with -ffp-contract=off so that the GPU and the CPU
+oracle round every operation identically (bit-exact weights).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "abnn_amd")
+CSRC = os.path.join(PKG, "csrc")
+HIP_SOURCES = [os.path.join(CSRC, "kernels.hip"), os.path.join(CSRC, "capi.hip")]
+HIP_DEPS = HIP_SOURCES + [os.path.join(CSRC, "engine.h"),
+                          os.path.join(ROOT, "include", "abnn", "abnn.h")]
+LIB = os.path.join(PKG, "libabnn_hip.so")
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+CPP_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "brain_cpp_test.cpp")
+CPP_TEST_BIN = os.path.join(ROOT, "tests", "cpp", "brain_cpp_test")
+
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+             "-ffp-contract=off", "-Wall", "-Werror=return-type"]
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build_hip(force: bool = False) -> str:
+    if force or _stale(LIB, HIP_DEPS):
+        tmp = LIB + ".tmp"
+        _run([HIPCC, *HIP_FLAGS, "-o", tmp, *HIP_SOURCES])
+        os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False) -> str:
+    src = os.path.join(ORACLE_DIR, "c1_oracle.c")
+    deps = [src, os.path.join(ORACLE_DIR, "c1_oracle.h"), os.path.join(ROOT, "include", "abnn", "abnn.h")]
+    if force or _stale(ORACLE_LIB, deps):
+        tmp = ORACLE_LIB + ".tmp"
+        _run(["gcc", "-O2", "-std=c11", "-Wall", "-ffp-contract=off", "-fPIC", "-shared",
+              "-pthread", "-o", tmp, src])
+        os.replace(tmp, ORACLE_LIB)
+    return ORACLE_LIB
+
+
+def build_cpp_example(force: bool = False) -> str | None:
+    if not os.path.exists(CPP_TEST_SRC):
+        return None
+    deps = [CPP_TEST_SRC, LIB, os.path.join(ROOT, "include", "abnn", "brain.hpp")]
+    if force or _stale(CPP_TEST_BIN, deps):
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
+              "-o", CPP_TEST_BIN, CPP_TEST_SRC, "-L", PKG, "-labnn_hip",
+              f"-Wl,-rpath,{PKG}", "-Wl,-rpath,$ORIGIN/../../abnn_amd"])
+    return CPP_TEST_BIN
+
+
+def build_all(force: bool = False) -> None:
+    build_hip(force)
+    build_oracle(force)
+    build_cpp_example(force)
+
+
+if __name__ == "__main__":
+    build_all(force=True)
+    print("built", LIB, ORACLE_LIB)

@@ -1,0 +1,843 @@
+// capi.hip -- implementation of the C-ABI (include/abnn/abnn.h) over the HIP
+// kernels of kernels.hip.  Replaces the Metal host class Brain
+// (abnn/src/core/brain/brain.{h,cpp}); each function cites what it replaces.
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+
+using namespace abnn;
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const std::string& m) { g_err = m; }
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess) {                                                        \
+            set_err(std::string(#expr) + ": " + hipGetErrorString(_e));                \
+            return ABNN_ERR_HIP;                                                       \
+        }                                                                              \
+    } while (0)
+
+#define REQUIRE(cond, msg)                                                             \
+    do {                                                                               \
+        if (!(cond)) {                                                                 \
+            set_err(msg);                                                              \
+            return ABNN_ERR_INVALID;                                                   \
+        }                                                                              \
+    } while (0)
+
+uint64_t visited_events(const abnn_dims& d)
+{
+    uint64_t grid = (d.events_per_pass + 255u) / 256u * 256u;  // brain.cpp:116-118
+    return grid < d.n_syn ? grid : d.n_syn;                     // brain.metal:61
+}
+
+struct EventPair {
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct abnn_brain {
+    abnn_dims dims{};
+    abnn_params params{};
+    KernelParams kp{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t last_stream = nullptr;
+    uint64_t n_nrn = 0;
+    DeviceState d{};
+    void* scalar_block = nullptr;  // clock | reward | rbar
+    uint64_t clock_host = 0;       // mirror, for the renormalisation decision (brain.cpp:127)
+    uint64_t rng = 0;              // host RNG of inject_inputs
+    uint64_t stim_first = 0, stim_count = 0;
+    bool pending_renorm = false;   // shard protocol: decided at gate time
+    bool timing = false;
+    std::vector<EventPair> events;
+    size_t events_used = 0;
+    uint32_t* idx_scratch = nullptr;
+    uint64_t idx_cap = 0;
+    uint64_t* u64_scratch = nullptr;
+};
+
+namespace {
+
+hipStream_t pick(abnn_brain* b, void* s)
+{
+    hipStream_t st = s ? static_cast<hipStream_t>(s) : b->stream;
+    b->last_stream = st;
+    return st;
+}
+
+// State accessors run on the handle's stream after everything enqueued on it
+// and on the stream of the last pass has completed.
+abnn_status sync_all(abnn_brain* b)
+{
+    HIP_TRY(hipSetDevice(b->device));
+    if (b->last_stream && b->last_stream != b->stream) HIP_TRY(hipStreamSynchronize(b->last_stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return ABNN_OK;
+}
+
+void free_all(abnn_brain* b)
+{
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    void* ptrs[] = {b->d.syn,        b->d.last_fired, b->d.last_visited, b->scalar_block,
+                    b->d.bitmap,     b->d.chunk_cnt,  b->d.chunk_pre,    b->d.active,
+                    b->d.g2buf,      b->d.apply_partial, b->d.fired,     b->d.summary,
+                    b->d.work,       b->idx_scratch,  b->u64_scratch};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (auto& e : b->events) {
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+}
+
+template <typename T>
+abnn_status dalloc(T** p, uint64_t count)
+{
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        set_err(std::string("hipMalloc(") + std::to_string(count * sizeof(T)) + " B): " +
+                hipGetErrorString(e));
+        return ABNN_ERR_OOM;
+    }
+    e = hipMemset(*p, 0, count * sizeof(T));
+    if (e != hipSuccess) {
+        set_err(std::string("hipMemset: ") + hipGetErrorString(e));
+        return ABNN_ERR_HIP;
+    }
+    return ABNN_OK;
+}
+
+#define ST_TRY(expr)                        \
+    do {                                    \
+        abnn_status _s = (expr);            \
+        if (_s != ABNN_OK) return _s;       \
+    } while (0)
+
+abnn_status ensure_idx_scratch(abnn_brain* b, uint64_t n)
+{
+    if (n <= b->idx_cap) return ABNN_OK;
+    if (b->idx_scratch) (void)hipFree(b->idx_scratch);
+    b->idx_scratch = nullptr;
+    b->idx_cap = 0;
+    ST_TRY(dalloc(&b->idx_scratch, n));
+    b->idx_cap = n;
+    return ABNN_OK;
+}
+
+abnn_status validate_records(const abnn_brain* b, const abnn_synapse* s, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i)
+        if (s[i].src >= b->n_nrn || s[i].dst >= b->n_nrn) {
+            set_err("synapse " + std::to_string(i) + " has src/dst >= N_NRN (" +
+                    std::to_string(b->n_nrn) + ")");
+            return ABNN_ERR_INVALID;
+        }
+    return ABNN_OK;
+}
+
+uint64_t tick_events(const abnn_brain* b)
+{
+    return b->dims.global_events ? b->dims.global_events : b->d.events;
+}
+
+void host_tick(abnn_brain* b)
+{
+    if (tick_events(b) > 0) b->clock_host += b->params.clock_inc;  // brain.metal:129
+}
+
+abnn_status time_begin(abnn_brain* b, hipStream_t s, EventPair** out)
+{
+    *out = nullptr;
+    if (!b->timing) return ABNN_OK;
+    if (b->events_used == b->events.size()) {
+        EventPair p;
+        HIP_TRY(hipEventCreate(&p.a));
+        HIP_TRY(hipEventCreate(&p.b));
+        b->events.push_back(p);
+    }
+    *out = &b->events[b->events_used++];
+    HIP_TRY(hipEventRecord((*out)->a, s));
+    return ABNN_OK;
+}
+
+// bitmap + streaming gate + chunk scan: the first half of every pass.
+abnn_status run_gate(abnn_brain* b, int64_t* summary_out, hipStream_t s)
+{
+    HIP_TRY(launch_bitmap(b->d, b->kp, b->stim_first, b->stim_count, s));
+    EventPair* ev = nullptr;
+    ST_TRY(time_begin(b, s, &ev));
+    HIP_TRY(launch_gate(b->d, b->kp, s));
+    if (ev) HIP_TRY(hipEventRecord(ev->b, s));
+    HIP_TRY(launch_scan(b->d, b->kp, summary_out, s));
+    return ABNN_OK;
+}
+
+abnn_status run_commit(abnn_brain* b, const int64_t* summaries, uint32_t world,
+                       const int32_t* fired, bool renorm, hipStream_t s)
+{
+    HIP_TRY(launch_finalize(b->d, b->kp, summaries, world, fired, s));
+    host_tick(b);
+    if (renorm) {  // renormalise_if_needed, brain.cpp:125-141; kernel brain.metal:135-145
+        HIP_TRY(launch_renorm(b->d, b->clock_host, s));
+        b->clock_host = 0;
+    }
+    return ABNN_OK;
+}
+
+// Chunked host<->device copies for the file formats.
+constexpr uint64_t kIoRecs = 1u << 22;  // 4M records (64 MiB) per piece
+
+}  // namespace
+
+extern "C" {
+
+int abnn_abi_version(void) { return ABNN_ABI_VERSION; }
+
+const char* abnn_status_string(abnn_status s)
+{
+    switch (s) {
+        case ABNN_OK: return "ok";
+        case ABNN_ERR_INVALID: return "invalid argument";
+        case ABNN_ERR_HIP: return "HIP runtime error";
+        case ABNN_ERR_OOM: return "out of memory";
+        case ABNN_ERR_SIZE_MISMATCH: return "size mismatch";
+        case ABNN_ERR_IO: return "I/O error";
+        case ABNN_ERR_NO_DEVICE: return "no HIP device";
+    }
+    return "unknown status";
+}
+
+const char* abnn_last_error(void) { return g_err.c_str(); }
+
+void abnn_default_params(abnn_params* p)
+{
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->base_scale = 0.8f;         // brain.metal:22
+    p->refractory = 2u;           // brain.metal:23
+    p->window_pre = 5u;           // brain.metal:24
+    p->clock_inc = 1u;            // brain.metal:26
+    p->target_rate_hz = 1000.0f;  // brain.metal:28
+    p->eta_home = 1.0e-6f;        // brain.metal:29
+    p->eta_reward = 1.0e-3f;      // brain.metal:30
+    p->alpha_rbar = 0.001f;       // brain.metal:31
+    p->a_ltp = 0.04f;             // constants.h:16
+    p->a_ltd = 0.02f;             // constants.h:17
+    p->w_min = 0.001f;            // constants.h:18
+    p->w_max = 1.0f;              // constants.h:19
+    p->max_spikes = 2560u;        // brain.h:18
+    p->tick_ns = 1000u;           // brain.h:17
+    p->tau_vis = 50000u;          // brain.cpp:102
+    p->tau_pre = 50000u;          // brain.cpp:102
+    p->renorm_thresh = 4000000u;  // brain.h:19
+    p->track_visits = 0u;
+    p->seed = 1u;
+}
+
+int abnn_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, int device,
+                              abnn_brain** out)
+{
+    REQUIRE(dims && out, "null argument");
+    *out = nullptr;
+    REQUIRE(dims->n_input > 0 || dims->n_output > 0 || dims->n_hidden > 0, "no neurons");
+    const uint64_t n_nrn = (uint64_t)dims->n_input + dims->n_output + dims->n_hidden;
+    REQUIRE(n_nrn <= 0xFFFFFFFFull, "N_NRN must fit u32 (SynapsePacked src/dst are u32)");
+    abnn_params p;
+    if (params) p = *params;
+    else abnn_default_params(&p);
+    REQUIRE(p.max_spikes < (1u << 30), "max_spikes too large");
+    const uint64_t E = visited_events(*dims);
+    REQUIRE(E / kChunk < 0xFFFFFFFFull, "too many events for one handle");
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_err("no HIP device visible");
+        return ABNN_ERR_NO_DEVICE;
+    }
+    REQUIRE(device >= 0 && device < ndev, "device ordinal out of range");
+
+    abnn_brain* b = new (std::nothrow) abnn_brain();
+    if (!b) return ABNN_ERR_OOM;
+    b->dims = *dims;
+    b->params = p;
+    b->kp = to_kernel_params(p);
+    b->device = device;
+    b->n_nrn = n_nrn;
+    b->rng = p.seed;
+    auto fail = [&](abnn_status s) {
+        free_all(b);
+        delete b;
+        return s;
+    };
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_err("hipSetDevice/hipStreamCreate failed");
+        return fail(ABNN_ERR_HIP);
+    }
+    DeviceState& d = b->d;
+    d.n_syn = dims->n_syn;
+    d.n_nrn = n_nrn;
+    d.events = E;
+    d.syn_offset = dims->syn_offset;
+    d.n_chunks = (uint32_t)((E + kChunk - 1) / kChunk);
+    abnn_status s;
+    // build_buffers, brain.cpp:52-69: allocate and zero every buffer.
+    if ((s = dalloc(&d.syn, dims->n_syn)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.last_fired, n_nrn)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.last_visited, n_nrn)) != ABNN_OK) return fail(s);
+    uint64_t* sb = nullptr;
+    if ((s = dalloc(&sb, 2)) != ABNN_OK) return fail(s);
+    b->scalar_block = sb;
+    d.clock = sb;
+    d.reward = reinterpret_cast<float*>(sb + 1);
+    d.rbar = d.reward + 1;
+    if ((s = dalloc(&d.bitmap, (n_nrn + 63) / 64 + 1)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.chunk_cnt, d.n_chunks)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.chunk_pre, d.n_chunks)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.active, d.n_chunks)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.g2buf, (uint64_t)d.n_chunks * kChunk)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.apply_partial, kApplyGrid)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.fired, p.max_spikes + 1u)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.summary, ABNN_SUMMARY_WORDS)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
+    *out = b;
+    return ABNN_OK;
+}
+
+abnn_status abnn_brain_destroy(abnn_brain* b)
+{
+    if (!b) return ABNN_OK;
+    (void)hipSetDevice(b->device);
+    (void)hipDeviceSynchronize();
+    free_all(b);
+    delete b;
+    return ABNN_OK;
+}
+
+abnn_status abnn_get_dims(const abnn_brain* b, abnn_dims* out)
+{
+    REQUIRE(b && out, "null argument");
+    *out = b->dims;
+    return ABNN_OK;
+}
+
+abnn_status abnn_get_params(const abnn_brain* b, abnn_params* out)
+{
+    REQUIRE(b && out, "null argument");
+    *out = b->params;
+    return ABNN_OK;
+}
+
+abnn_status abnn_state_ptrs(abnn_brain* b, abnn_state* out)
+{
+    REQUIRE(b && out, "null argument");
+    out->synapses = reinterpret_cast<abnn_synapse*>(b->d.syn);
+    out->last_fired = b->d.last_fired;
+    out->last_visited = b->d.last_visited;
+    out->clock = b->d.clock;
+    out->reward = b->d.reward;
+    out->rbar = b->d.rbar;
+    return ABNN_OK;
+}
+
+uint64_t abnn_n_neuron(const abnn_brain* b) { return b ? b->n_nrn : 0; }
+
+abnn_status abnn_upload_synapses(abnn_brain* b, uint64_t first, const abnn_synapse* src, uint64_t n)
+{
+    REQUIRE(b && (src || n == 0), "null argument");
+    REQUIRE(first <= b->dims.n_syn && n <= b->dims.n_syn - first, "range out of bounds");
+    ST_TRY(validate_records(b, src, n));
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(b->d.syn + first, src, n * sizeof(abnn_synapse), hipMemcpyHostToDevice));
+    return ABNN_OK;
+}
+
+abnn_status abnn_download_synapses(abnn_brain* b, uint64_t first, abnn_synapse* dst, uint64_t n)
+{
+    REQUIRE(b && (dst || n == 0), "null argument");
+    REQUIRE(first <= b->dims.n_syn && n <= b->dims.n_syn - first, "range out of bounds");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(dst, b->d.syn + first, n * sizeof(abnn_synapse), hipMemcpyDeviceToHost));
+    return ABNN_OK;
+}
+
+abnn_status abnn_generate_synapses(abnn_brain* b, uint64_t seed)
+{
+    REQUIRE(b, "null argument");
+    const uint64_t n_io = (uint64_t)b->dims.n_input * b->dims.n_output;
+    REQUIRE(b->dims.syn_offset + b->dims.n_syn <= n_io || b->dims.n_hidden > 0,
+            "sparse hidden synapses need n_hidden > 0 (brain-engine.cpp:46-47)");
+    REQUIRE(b->dims.n_output > 0 || b->dims.syn_offset + b->dims.n_syn <= n_io,
+            "dense block needs n_output > 0");
+    ST_TRY(sync_all(b));
+    HIP_TRY(launch_generate(b->d, b->dims.n_input, b->dims.n_output, seed, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return ABNN_OK;
+}
+
+abnn_status abnn_checksum_synapses(abnn_brain* b, uint64_t* out)
+{
+    REQUIRE(b && out, "null argument");
+    ST_TRY(sync_all(b));
+    HIP_TRY(launch_checksum(b->d, b->u64_scratch, b->stream));
+    HIP_TRY(hipMemcpyAsync(out, b->u64_scratch, sizeof(uint64_t), hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return ABNN_OK;
+}
+
+abnn_status abnn_get_last_fired(abnn_brain* b, uint64_t first, uint64_t* out, uint64_t n)
+{
+    REQUIRE(b && (out || n == 0), "null argument");
+    REQUIRE(first <= b->n_nrn && n <= b->n_nrn - first, "range out of bounds");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(out, b->d.last_fired + first, n * 8, hipMemcpyDeviceToHost));
+    return ABNN_OK;
+}
+
+abnn_status abnn_set_last_fired(abnn_brain* b, uint64_t first, const uint64_t* src, uint64_t n)
+{
+    REQUIRE(b && (src || n == 0), "null argument");
+    REQUIRE(first <= b->n_nrn && n <= b->n_nrn - first, "range out of bounds");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(b->d.last_fired + first, src, n * 8, hipMemcpyHostToDevice));
+    return ABNN_OK;
+}
+
+abnn_status abnn_get_last_visited(abnn_brain* b, uint64_t first, uint64_t* out, uint64_t n)
+{
+    REQUIRE(b && (out || n == 0), "null argument");
+    REQUIRE(first <= b->n_nrn && n <= b->n_nrn - first, "range out of bounds");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(out, b->d.last_visited + first, n * 8, hipMemcpyDeviceToHost));
+    return ABNN_OK;
+}
+
+abnn_status abnn_set_last_visited(abnn_brain* b, uint64_t first, const uint64_t* src, uint64_t n)
+{
+    REQUIRE(b && (src || n == 0), "null argument");
+    REQUIRE(first <= b->n_nrn && n <= b->n_nrn - first, "range out of bounds");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(b->d.last_visited + first, src, n * 8, hipMemcpyHostToDevice));
+    return ABNN_OK;
+}
+
+abnn_status abnn_set_timestamps(abnn_brain* b, const uint32_t* idx, uint64_t n, uint64_t value)
+{
+    REQUIRE(b && (idx || n == 0), "null argument");
+    for (uint64_t i = 0; i < n; ++i) REQUIRE(idx[i] < b->n_nrn, "neuron index out of range");
+    ST_TRY(sync_all(b));
+    ST_TRY(ensure_idx_scratch(b, n));
+    HIP_TRY(hipMemcpy(b->idx_scratch, idx, n * 4, hipMemcpyHostToDevice));
+    HIP_TRY(launch_stamp_list(b->d, b->idx_scratch, n, nullptr, value, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return ABNN_OK;
+}
+
+abnn_status abnn_get_scalars(abnn_brain* b, abnn_scalars* out)
+{
+    REQUIRE(b && out, "null argument");
+    ST_TRY(sync_all(b));
+    uint64_t blk[2];
+    HIP_TRY(hipMemcpy(blk, b->scalar_block, sizeof(blk), hipMemcpyDeviceToHost));
+    out->clock = blk[0];
+    std::memcpy(&out->reward, reinterpret_cast<char*>(blk) + 8, 4);
+    std::memcpy(&out->rbar, reinterpret_cast<char*>(blk) + 12, 4);
+    return ABNN_OK;
+}
+
+abnn_status abnn_set_scalars(abnn_brain* b, const abnn_scalars* in)
+{
+    REQUIRE(b && in, "null argument");
+    ST_TRY(sync_all(b));
+    uint64_t blk[2];
+    blk[0] = in->clock;
+    std::memcpy(reinterpret_cast<char*>(blk) + 8, &in->reward, 4);
+    std::memcpy(reinterpret_cast<char*>(blk) + 12, &in->rbar, 4);
+    HIP_TRY(hipMemcpy(b->scalar_block, blk, sizeof(blk), hipMemcpyHostToDevice));
+    b->clock_host = in->clock;
+    return ABNN_OK;
+}
+
+abnn_status abnn_set_reward(abnn_brain* b, float r)
+{
+    REQUIRE(b, "null argument");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(b->d.reward, &r, 4, hipMemcpyHostToDevice));
+    return ABNN_OK;
+}
+
+abnn_status abnn_inject_inputs(abnn_brain* b, const float* v, uint32_t n, float hz)
+{
+    REQUIRE(b && (v || n == 0), "null argument");
+    REQUIRE(n == b->dims.n_input, "inject_inputs: size must equal n_input (brain.cpp:75)");
+    // pTick = hz * kTickNS * NSEC_PER_SEC, all in float (brain.cpp:76)
+    float p_tick = hz * (float)b->params.tick_ns;
+    p_tick = p_tick * (float)1000000000ull;
+    std::vector<uint32_t> idx;
+    for (uint32_t i = 0; i < n; ++i) {
+        b->rng += 0x9E3779B97F4A7C15ull;  // SplitMix64 step
+        uint64_t z = b->rng;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z = z ^ (z >> 31);
+        const float uni = (float)(z >> 40) * (1.0f / 16777216.0f);
+        if (uni < p_tick * v[i]) idx.push_back(i);  // brain.cpp:82
+    }
+    ST_TRY(sync_all(b));
+    if (idx.empty()) return ABNN_OK;
+    ST_TRY(ensure_idx_scratch(b, idx.size()));
+    HIP_TRY(hipMemcpy(b->idx_scratch, idx.data(), idx.size() * 4, hipMemcpyHostToDevice));
+    // lastFired[i] = clock, read on the device
+    HIP_TRY(launch_stamp_list(b->d, b->idx_scratch, idx.size(), b->d.clock, 0, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    return ABNN_OK;
+}
+
+abnn_status abnn_read_outputs(abnn_brain* b, uint8_t* out, uint32_t n)
+{
+    REQUIRE(b && (out || n == 0), "null argument");
+    REQUIRE(n == b->dims.n_output, "read_outputs: size must equal n_output");
+    ST_TRY(sync_all(b));
+    std::vector<uint64_t> lf(n);
+    uint64_t now = 0;
+    if (n) HIP_TRY(hipMemcpy(lf.data(), b->d.last_fired + b->dims.n_input, n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&now, b->d.clock, 8, hipMemcpyDeviceToHost));
+    const uint64_t start = now > 1 ? now - 1 : 0;  // brain.cpp:151
+    for (uint32_t o = 0; o < n; ++o) {
+        const uint64_t ts = lf[o];
+        out[o] = (ts != 0 && ts >= start && ts < now) ? 1 : 0;  // brain.cpp:153-154
+    }
+    return ABNN_OK;
+}
+
+abnn_status abnn_set_auto_stimulus(abnn_brain* b, uint64_t first, uint64_t count)
+{
+    REQUIRE(b, "null argument");
+    REQUIRE(count == 0 || (first < b->n_nrn && count <= b->n_nrn - first), "range out of bounds");
+    b->stim_first = count ? first : 0;
+    b->stim_count = count;
+    return ABNN_OK;
+}
+
+abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream)
+{
+    REQUIRE(b, "null argument");
+    HIP_TRY(hipSetDevice(b->device));
+    hipStream_t s = pick(b, stream);
+    for (uint32_t i = 0; i < passes; ++i) {
+        // the host reads the clock at encode time, before the pass (brain.cpp:127-128)
+        const bool renorm = b->clock_host > b->params.renorm_thresh;
+        ST_TRY(run_gate(b, b->d.summary, s));
+        HIP_TRY(launch_apply(b->d, b->kp, b->d.summary, 1, 0, b->d.fired, s));
+        ST_TRY(run_commit(b, b->d.summary, 1, b->d.fired, renorm, s));
+    }
+    return ABNN_OK;
+}
+
+abnn_status abnn_synchronize(abnn_brain* b, void* stream)
+{
+    REQUIRE(b, "null argument");
+    HIP_TRY(hipSetDevice(b->device));
+    if (stream) HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return sync_all(b);
+}
+
+abnn_status abnn_shard_gate(abnn_brain* b, int64_t* summary_dev, void* stream)
+{
+    REQUIRE(b && summary_dev, "null argument");
+    HIP_TRY(hipSetDevice(b->device));
+    hipStream_t s = pick(b, stream);
+    b->pending_renorm = b->clock_host > b->params.renorm_thresh;
+    return run_gate(b, summary_dev, s);
+}
+
+abnn_status abnn_shard_apply(abnn_brain* b, const int64_t* summaries_dev, uint32_t world,
+                             uint32_t rank, int32_t* fired_dev, void* stream)
+{
+    REQUIRE(b && summaries_dev && fired_dev, "null argument");
+    REQUIRE(world >= 1 && rank < world, "bad world/rank");
+    HIP_TRY(hipSetDevice(b->device));
+    hipStream_t s = pick(b, stream);
+    HIP_TRY(hipMemsetAsync(fired_dev, 0, (size_t)b->params.max_spikes * 4, s));
+    HIP_TRY(launch_apply(b->d, b->kp, summaries_dev, world, rank, fired_dev, s));
+    return ABNN_OK;
+}
+
+abnn_status abnn_shard_commit(abnn_brain* b, const int64_t* summaries_dev, uint32_t world,
+                              const int32_t* fired_dev, void* stream)
+{
+    REQUIRE(b && summaries_dev && fired_dev, "null argument");
+    REQUIRE(world >= 1, "bad world");
+    HIP_TRY(hipSetDevice(b->device));
+    hipStream_t s = pick(b, stream);
+    const bool renorm = b->pending_renorm;
+    b->pending_renorm = false;
+    return run_commit(b, summaries_dev, world, fired_dev, renorm, s);
+}
+
+abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out)
+{
+    REQUIRE(b && out, "null argument");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(out, &b->d.work->stats, sizeof(abnn_stats), hipMemcpyDeviceToHost));
+    return ABNN_OK;
+}
+
+abnn_status abnn_reset_stats(abnn_brain* b)
+{
+    REQUIRE(b, "null argument");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemset(&b->d.work->stats, 0, sizeof(abnn_stats)));
+    return ABNN_OK;
+}
+
+abnn_status abnn_enable_timing(abnn_brain* b, int on)
+{
+    REQUIRE(b, "null argument");
+    ST_TRY(sync_all(b));
+    b->timing = on != 0;
+    b->events_used = 0;
+    return ABNN_OK;
+}
+
+abnn_status abnn_get_kernel_time(abnn_brain* b, double* ms_total, uint64_t* launches)
+{
+    REQUIRE(b && ms_total && launches, "null argument");
+    ST_TRY(sync_all(b));
+    double tot = 0;
+    for (size_t i = 0; i < b->events_used; ++i) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, b->events[i].a, b->events[i].b));
+        tot += ms;
+    }
+    *ms_total = tot;
+    *launches = b->events_used;
+    b->events_used = 0;
+    return ABNN_OK;
+}
+
+// ---- persistence -----------------------------------------------------------
+
+abnn_status abnn_save_bnn(abnn_brain* b, const char* path)
+{
+    REQUIRE(b && path, "null argument");
+    REQUIRE(b->dims.n_syn <= 0xFFFFFFFFull && b->n_nrn <= 0xFFFFFFFFull,
+            ".bnn header holds u32 sizes (brain.cpp:163-164)");
+    ST_TRY(sync_all(b));
+    FILE* f = std::fopen(path, "wb");
+    if (!f) {
+        set_err(std::string("cannot open ") + path);
+        return ABNN_ERR_IO;
+    }
+    const uint32_t hdr[2] = {(uint32_t)b->dims.n_syn, (uint32_t)b->n_nrn};  // brain.cpp:163-164
+    bool ok = std::fwrite(hdr, 4, 2, f) == 2;
+    std::vector<abnn_synapse> buf;
+    for (uint64_t i = 0; ok && i < b->dims.n_syn; i += kIoRecs) {
+        const uint64_t n = std::min<uint64_t>(kIoRecs, b->dims.n_syn - i);
+        buf.resize(n);
+        if (hipMemcpy(buf.data(), b->d.syn + i, n * 16, hipMemcpyDeviceToHost) != hipSuccess) {
+            std::fclose(f);
+            set_err("hipMemcpy D2H failed");
+            return ABNN_ERR_HIP;
+        }
+        ok = std::fwrite(buf.data(), 16, n, f) == n;  // brain.cpp:165-166
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok) {
+        set_err(std::string("write failed: ") + path);
+        return ABNN_ERR_IO;
+    }
+    return ABNN_OK;
+}
+
+abnn_status abnn_load_bnn(abnn_brain* b, const char* path)
+{
+    REQUIRE(b && path, "null argument");
+    FILE* f = std::fopen(path, "rb");
+    if (!f) {
+        set_err(std::string("cannot open ") + path);
+        return ABNN_ERR_IO;
+    }
+    uint32_t hdr[2] = {0, 0};
+    if (std::fread(hdr, 4, 2, f) != 2) {
+        std::fclose(f);
+        set_err("short .bnn header");
+        return ABNN_ERR_IO;
+    }
+    if (!(hdr[0] == b->dims.n_syn && hdr[1] == b->n_nrn)) {  // brain.cpp:174
+        std::fclose(f);
+        set_err(".bnn header does not match this brain");
+        return ABNN_ERR_SIZE_MISMATCH;
+    }
+    abnn_status st = sync_all(b);
+    if (st != ABNN_OK) {
+        std::fclose(f);
+        return st;
+    }
+    std::vector<abnn_synapse> buf;
+    for (uint64_t i = 0; i < b->dims.n_syn; i += kIoRecs) {
+        const uint64_t n = std::min<uint64_t>(kIoRecs, b->dims.n_syn - i);
+        buf.resize(n);
+        if (std::fread(buf.data(), 16, n, f) != n) {
+            std::fclose(f);
+            set_err("short .bnn body");
+            return ABNN_ERR_IO;
+        }
+        st = validate_records(b, buf.data(), n);
+        if (st == ABNN_OK && hipMemcpy(b->d.syn + i, buf.data(), n * 16, hipMemcpyHostToDevice) != hipSuccess) {
+            set_err("hipMemcpy H2D failed");
+            st = ABNN_ERR_HIP;
+        }
+        if (st != ABNN_OK) {
+            std::fclose(f);
+            return st;
+        }
+    }
+    std::fclose(f);
+    return ABNN_OK;
+}
+
+abnn_status abnn_save_flat(abnn_brain* b, const char* path)
+{
+    REQUIRE(b && path, "null argument");
+    REQUIRE(b->dims.n_syn <= 0xFFFFFFFFull && b->n_nrn <= 0xFFFFFFFFull,
+            "flat header holds u32 sizes (README §2.1)");
+    ST_TRY(sync_all(b));
+    FILE* f = std::fopen(path, "wb");
+    if (!f) {
+        set_err(std::string("cannot open ") + path);
+        return ABNN_ERR_IO;
+    }
+    uint32_t hdr[4] = {(uint32_t)b->dims.n_syn, (uint32_t)b->n_nrn, 0, 0};
+    bool ok = std::fwrite(hdr, 4, 4, f) == 4;
+    std::vector<abnn_synapse> buf;
+    std::vector<uint32_t> pairs;
+    std::vector<float> ws;
+    // synapses (src, dst) pairs, then weights: two sweeps
+    for (int sweep = 0; ok && sweep < 2; ++sweep) {
+        for (uint64_t i = 0; ok && i < b->dims.n_syn; i += kIoRecs) {
+            const uint64_t n = std::min<uint64_t>(kIoRecs, b->dims.n_syn - i);
+            buf.resize(n);
+            if (hipMemcpy(buf.data(), b->d.syn + i, n * 16, hipMemcpyDeviceToHost) != hipSuccess) {
+                ok = false;
+                break;
+            }
+            if (sweep == 0) {
+                pairs.resize(2 * n);
+                for (uint64_t k = 0; k < n; ++k) {
+                    pairs[2 * k] = buf[k].src;
+                    pairs[2 * k + 1] = buf[k].dst;
+                }
+                ok = std::fwrite(pairs.data(), 8, n, f) == n;
+            } else {
+                ws.resize(n);
+                for (uint64_t k = 0; k < n; ++k) ws[k] = buf[k].w;
+                ok = std::fwrite(ws.data(), 4, n, f) == n;
+            }
+        }
+    }
+    std::vector<uint64_t> ts(b->n_nrn);
+    for (int arr = 0; ok && arr < 2; ++arr) {
+        uint64_t* src = arr == 0 ? b->d.last_fired : b->d.last_visited;
+        if (b->n_nrn && hipMemcpy(ts.data(), src, b->n_nrn * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+            ok = false;
+            break;
+        }
+        ok = std::fwrite(ts.data(), 8, b->n_nrn, f) == b->n_nrn;
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok) {
+        set_err(std::string("flat save failed: ") + path);
+        return ABNN_ERR_IO;
+    }
+    return ABNN_OK;
+}
+
+abnn_status abnn_load_flat(abnn_brain* b, const char* path)
+{
+    REQUIRE(b && path, "null argument");
+    FILE* f = std::fopen(path, "rb");
+    if (!f) {
+        set_err(std::string("cannot open ") + path);
+        return ABNN_ERR_IO;
+    }
+    uint32_t hdr[4] = {0, 0, 0, 0};
+    if (std::fread(hdr, 4, 4, f) != 4) {
+        std::fclose(f);
+        set_err("short flat header");
+        return ABNN_ERR_IO;
+    }
+    if (!(hdr[0] == b->dims.n_syn && hdr[1] == b->n_nrn)) {
+        std::fclose(f);
+        set_err("flat header does not match this brain");
+        return ABNN_ERR_SIZE_MISMATCH;
+    }
+    abnn_status st = sync_all(b);
+    if (st != ABNN_OK) {
+        std::fclose(f);
+        return st;
+    }
+    const uint64_t N = b->dims.n_syn;
+    const long pairs_at = 16, weights_at = 16 + (long)(8 * N);
+    std::vector<abnn_synapse> buf;
+    std::vector<uint32_t> pairs;
+    std::vector<float> ws;
+    bool ok = true;
+    for (uint64_t i = 0; ok && i < N; i += kIoRecs) {
+        const uint64_t n = std::min<uint64_t>(kIoRecs, N - i);
+        pairs.resize(2 * n);
+        ws.resize(n);
+        buf.resize(n);
+        ok = std::fseek(f, pairs_at + (long)(8 * i), SEEK_SET) == 0 &&
+             std::fread(pairs.data(), 8, n, f) == n &&
+             std::fseek(f, weights_at + (long)(4 * i), SEEK_SET) == 0 &&
+             std::fread(ws.data(), 4, n, f) == n;
+        if (!ok) break;
+        for (uint64_t k = 0; k < n; ++k) buf[k] = {pairs[2 * k], pairs[2 * k + 1], ws[k], 0.0f};
+        st = validate_records(b, buf.data(), n);
+        if (st != ABNN_OK) {
+            std::fclose(f);
+            return st;
+        }
+        ok = hipMemcpy(b->d.syn + i, buf.data(), n * 16, hipMemcpyHostToDevice) == hipSuccess;
+    }
+    std::vector<uint64_t> ts(b->n_nrn);
+    if (ok) ok = std::fseek(f, weights_at + (long)(4 * N), SEEK_SET) == 0;
+    for (int arr = 0; ok && arr < 2; ++arr) {
+        ok = std::fread(ts.data(), 8, b->n_nrn, f) == b->n_nrn;
+        uint64_t* dst = arr == 0 ? b->d.last_fired : b->d.last_visited;
+        if (ok && b->n_nrn)
+            ok = hipMemcpy(dst, ts.data(), b->n_nrn * 8, hipMemcpyHostToDevice) == hipSuccess;
+    }
+    std::fclose(f);
+    if (!ok) {
+        set_err(std::string("flat load failed: ") + path);
+        return ABNN_ERR_IO;
+    }
+    return ABNN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,605 @@
+// kernels.hip -- CDNA4 (gfx950) kernels of one C1 traversal pass.
+//
+// Reference hot path: monte_carlo_traversal (abnn/src/core/kernels/brain.metal:41-130)
+// and renormalise_clock_and_times (brain.metal:135-145).  The pass is split into
+// launches that each do one HBM-friendly thing:
+//
+//   k_bitmap   : lastFired (u64, 8 B/neuron) -> 1 recent-spike bit per neuron
+//                (now - lastFired <= WINDOW_PRE), plus the fused stimulus stamp.
+//                The pre-spike gate of every event (brain.metal:73-77) then reads
+//                one bit of an L2-resident bitmap instead of a random 8-B word.
+//   k_gate     : the streaming kernel.  One 16-B SynapsePacked per event, non-
+//                temporal dwordx4 loads, 1 KiB per wave-instruction; pre-gate
+//                via the bitmap; refractory gate (brain.metal:79-83) via a real
+//                8-B gather for the few events that pass; spike-candidate test
+//                (brain.metal:91-92); stable in-order compaction of the gated
+//                events into the chunk's region (wave ballots + 2 KiB of LDS).
+//   k_scan     : one workgroup: exclusive prefix of candidate counts over chunks
+//                = the ordered global spike budget of schedule C1
+//                (brain.metal:85-98 without its races).
+//   k_apply    : weight update (brain.metal:101-122) of the gated events that
+//                still had budget, spike list in budget order.
+//   k_finalize : deferred lastFired stamps (brain.metal:125-126), rBar EWMA
+//                (brain.metal:110-113), one clock tick (brain.metal:129).
+//   k_renorm   : brain.metal:135-145 with the base read once (no race).
+//
+// All fp32 arithmetic is compiled with -ffp-contract=off and written operation
+// for operation like the oracle, so weights are bit-identical to the CPU.
+#include "engine.h"
+
+#pragma clang fp contract(off)
+
+namespace abnn {
+
+KernelParams to_kernel_params(const abnn_params& p)
+{
+    KernelParams k;
+    k.base_scale = p.base_scale;
+    k.target_rate_hz = p.target_rate_hz;
+    k.eta_home = p.eta_home;
+    k.eta_reward = p.eta_reward;
+    k.alpha_rbar = p.alpha_rbar;
+    k.a_ltp = p.a_ltp;
+    k.a_ltd = p.a_ltd;
+    k.w_min = p.w_min;
+    k.w_max = p.w_max;
+    k.refractory = p.refractory;
+    k.window_pre = p.window_pre;
+    k.clock_inc = p.clock_inc;
+    k.max_spikes = p.max_spikes;
+    k.track_visits = p.track_visits;
+    return k;
+}
+
+namespace {
+
+// rand01, brain.metal:15-19.
+__device__ __forceinline__ float rand01(uint32_t s)
+{
+    s ^= s << 13;
+    s ^= s >> 17;
+    s ^= s << 5;
+    return (float)(s & 0xFFFFFFu) * (1.0f / 16777216.0f);
+}
+
+// Metal clamp(x, lo, hi) = min(max(x, lo), hi), written as selects so the
+// result is bit-identical to the C oracle (no NaN canonicalisation).
+__device__ __forceinline__ float clampf(float x, float lo, float hi)
+{
+    float m = x > lo ? x : lo;
+    return m < hi ? m : hi;
+}
+
+__device__ __forceinline__ bool spike_candidate(const KernelParams& kp, float w, uint64_t tg,
+                                                uint64_t now)
+{
+    float prob = clampf((w * w) * kp.base_scale, 0.0f, 1.0f);      // brain.metal:91
+    return prob > rand01((uint32_t)tg ^ (uint32_t)now);             // brain.metal:92
+}
+
+__device__ __forceinline__ float updated_weight(const KernelParams& kp, float w, bool fired,
+                                                float R, float rb, float isi)
+{
+    float dW = fired ? kp.a_ltp * (1.0f - w) : (-kp.a_ltd) * w;     // brain.metal:101-102
+    dW = dW + (kp.eta_reward * (R - rb)) * (fired ? 1.0f : 0.0f);   // brain.metal:105-107
+    float est_hz = isi > 0.0f ? 1e6f / isi : 0.0f;                  // brain.metal:116-117
+    dW = dW + (kp.eta_home * (kp.target_rate_hz - est_hz)) * w;     // brain.metal:118
+    return clampf(w + dW, kp.w_min, kp.w_max);                      // brain.metal:121
+}
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// Streaming 16-B load that should not displace the L2/MALL-resident neuron
+// state (bitmap, lastFired): non-temporal dwordx4.
+__device__ __forceinline__ uint4 load_stream16(const uint4* p)
+{
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k)
+{
+    uint64_t z = seed + (k + 1u) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float unit24(uint64_t x)
+{
+    return (float)(x >> 40) * (1.0f / 16777216.0f);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Exclusive scan of one u64 per thread over a kScanThreads workgroup.
+__device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total, uint64_t* s_wave)
+{
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr uint32_t nw = kScanThreads / 64;
+    uint64_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint64_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) s_wave[wid] = inc;
+    __syncthreads();
+    uint64_t before = 0, tot = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        uint64_t x = s_wave[w];
+        if (w < wid) before += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return before + inc - v;
+}
+
+// ---------------------------------------------------------------------------
+// k_bitmap: bit i = (now - lastFired[i]) <= window_pre; stimulus stamp fused.
+__global__ __launch_bounds__(kBlock) void k_bitmap(DeviceState d, KernelParams kp,
+                                                   uint64_t stim_first, uint64_t stim_count)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t now = *d.clock;
+    bool bit = false;
+    if (i < d.n_nrn) {
+        uint64_t L;
+        if (i - stim_first < stim_count) {  // unsigned range test
+            L = now;
+            d.last_fired[i] = now;          // Brain::inject_inputs, brain.cpp:82
+        } else {
+            L = __builtin_nontemporal_load(d.last_fired + i);
+        }
+        bit = (now - L) <= (uint64_t)kp.window_pre;
+    }
+    const uint64_t m = __ballot(bit);
+    if ((threadIdx.x & 63) == 0 && i < d.n_nrn) d.bitmap[i >> 6] = m;
+}
+
+// ---------------------------------------------------------------------------
+// k_gate: the streaming kernel (see file header).
+template <bool kTrack>
+__global__ __launch_bounds__(kBlock) void k_gate(DeviceState d, KernelParams kp)
+{
+    __shared__ uint32_t s_g2[kEvPerThread][kWaves];
+    __shared__ uint32_t s_c[kEvPerThread][kWaves];
+    __shared__ uint32_t s_g1[kWaves];
+
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t c = blockIdx.x;
+    const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
+    const uint64_t base = (uint64_t)c * kChunk;
+    const uint32_t* bm = reinterpret_cast<const uint32_t*>(d.bitmap);
+
+    uint4 rec[kEvPerThread];
+    uint32_t valid = 0;
+    if (base + kChunk <= d.events) {
+#pragma unroll
+        for (int k = 0; k < kEvPerThread; ++k)
+            rec[k] = load_stream16(d.syn + base + k * kBlock + tid);  // brain.metal:70
+        valid = (1u << kEvPerThread) - 1u;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kEvPerThread; ++k) {
+            const uint64_t t = base + k * kBlock + tid;
+            if (t < d.events) {
+                rec[k] = load_stream16(d.syn + t);
+                valid |= 1u << k;
+            } else {
+                rec[k] = make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
+    }
+
+    // Pre-spike gate, brain.metal:73-77: one bit per source neuron.
+    uint32_t g1m = 0;
+#pragma unroll
+    for (int k = 0; k < kEvPerThread; ++k) {
+        // records are validated on upload (src, dst < N_NRN); the guard only
+        // keeps a corrupted record from faulting the device
+        const uint32_t src = rec[k].x < d.n_nrn ? rec[k].x : 0u;
+        const uint32_t word = bm[src >> 5];
+        if (((valid >> k) & 1u) && rec[k].x < d.n_nrn && rec[k].y < d.n_nrn &&
+            ((word >> (src & 31u)) & 1u))
+            g1m |= 1u << k;
+    }
+
+    // Refractory gate, brain.metal:79-83: real 8-B gather of lastFired[dst].
+    uint64_t ld[kEvPerThread];
+#pragma unroll
+    for (int k = 0; k < kEvPerThread; ++k)
+        ld[k] = ((g1m >> k) & 1u) ? d.last_fired[rec[k].y] : 0ull;
+
+    uint32_t g2m = 0, cm = 0;
+#pragma unroll
+    for (int k = 0; k < kEvPerThread; ++k) {
+        if (((g1m >> k) & 1u) && (now - ld[k]) > (uint64_t)kp.refractory) {
+            g2m |= 1u << k;
+            const uint64_t tg = d.syn_offset + base + k * kBlock + tid;
+            if (spike_candidate(kp, __uint_as_float(rec[k].z), tg, now)) cm |= 1u << k;
+        }
+    }
+
+    if (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
+#pragma unroll
+        for (int k = 0; k < kEvPerThread; ++k)
+            if (((valid >> k) & 1u) && rec[k].y < d.n_nrn) d.last_visited[rec[k].y] = now;
+    }
+
+    // In-order compaction: event order inside the chunk is (k, wave, lane).
+    uint32_t mb_g2[kEvPerThread], mb_c[kEvPerThread];
+    uint32_t g1cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kEvPerThread; ++k) {
+        const uint64_t bg = __ballot((g2m >> k) & 1u);
+        const uint64_t bc = __ballot((cm >> k) & 1u);
+        const uint64_t b1 = __ballot((g1m >> k) & 1u);
+        mb_g2[k] = mbcnt64(bg);
+        mb_c[k] = mbcnt64(bc);
+        g1cnt += (uint32_t)__popcll(b1);
+        if (lane == 0) {
+            s_g2[k][wid] = (uint32_t)__popcll(bg);
+            s_c[k][wid] = (uint32_t)__popcll(bc);
+        }
+    }
+    if (lane == 0) s_g1[wid] = g1cnt;
+    __syncthreads();
+
+    uint32_t run_g2 = 0, run_c = 0;
+#pragma unroll
+    for (int k = 0; k < kEvPerThread; ++k) {
+        uint32_t bw_g2 = 0, bw_c = 0, tot_g2 = 0, tot_c = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < (uint32_t)kWaves; ++w) {
+            const uint32_t a = s_g2[k][w], b = s_c[k][w];
+            bw_g2 += w < wid ? a : 0u;
+            bw_c += w < wid ? b : 0u;
+            tot_g2 += a;
+            tot_c += b;
+        }
+        if ((g2m >> k) & 1u) {
+            const uint32_t slot = run_g2 + bw_g2 + mb_g2[k];
+            const uint32_t pre = run_c + bw_c + mb_c[k];
+            uint4 e;
+            e.x = (uint32_t)(k * kBlock + tid) | (pre << 11) | (((cm >> k) & 1u) << 22);
+            e.y = rec[k].y;
+            e.z = rec[k].z;
+            e.w = __float_as_uint((float)(now - ld[k]));  // isi, brain.metal:116
+            d.g2buf[base + slot] = e;
+        }
+        run_g2 += tot_g2;
+        run_c += tot_c;
+    }
+    if (tid == 0) {
+        d.chunk_cnt[c] = make_uint4(run_g2, run_c, s_g1[0] + s_g1[1] + s_g1[2] + s_g1[3], 0u);
+        if (c == 0) d.work->t0_g2 = (d.syn_offset == 0 && (g2m & 1u)) ? 1u : 0u;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_scan: ordered spike budget over chunks (one workgroup).
+__global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelParams kp,
+                                                       int64_t* summary_out)
+{
+    __shared__ uint64_t s_wave[kScanThreads / 64];
+    __shared__ uint64_t s_red[3][kScanThreads / 64];
+    const uint32_t n = d.n_chunks, tid = threadIdx.x;
+    const uint32_t per = (n + kScanThreads - 1) / kScanThreads;
+    const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
+    const uint64_t budget = kp.max_spikes;
+
+    uint64_t cand = 0, g2 = 0, g1 = 0;
+    for (uint32_t c = lo; c < hi; ++c) {
+        const uint4 v = d.chunk_cnt[c];
+        g2 += v.x;
+        cand += v.y;
+        g1 += v.z;
+    }
+    uint64_t cand_total;
+    const uint64_t excl = block_exclusive_scan(cand, &cand_total, s_wave);
+
+    // totals of g1 / g2 (for statistics)
+    const uint64_t wg2 = wave_sum(g2), wg1 = wave_sum(g1);
+    if ((tid & 63) == 0) {
+        s_red[0][tid >> 6] = wg2;
+        s_red[1][tid >> 6] = wg1;
+    }
+
+    uint64_t pre = excl;
+    uint64_t nact = 0;
+    for (uint32_t c = lo; c < hi; ++c) {
+        const uint4 v = d.chunk_cnt[c];
+        d.chunk_pre[c] = (uint32_t)(pre < budget ? pre : budget);
+        nact += (v.x > 0 && pre < budget) ? 1u : 0u;
+        pre += v.y;
+    }
+    uint64_t act_total;
+    uint64_t act_pos = block_exclusive_scan(nact, &act_total, s_wave);
+    pre = excl;
+    for (uint32_t c = lo; c < hi; ++c) {
+        const uint4 v = d.chunk_cnt[c];
+        if (v.x > 0 && pre < budget) d.active[act_pos++] = c;
+        pre += v.y;
+    }
+    if (tid == 0) {
+        uint64_t tg2 = 0, tg1 = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) {
+            tg2 += s_red[0][w];
+            tg1 += s_red[1][w];
+        }
+        const uint64_t capped = cand_total < budget ? cand_total : budget;
+        summary_out[0] = (int64_t)capped;
+        summary_out[1] = (int64_t)d.work->t0_g2;
+        summary_out[2] = (int64_t)d.events;
+        summary_out[3] = (int64_t)tg2;
+        d.work->n_active = (uint32_t)act_total;
+        d.work->events = d.events;
+        d.work->g1 = tg1;
+        d.work->g2 = tg2;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_apply: weight update of the gated events that still had budget.
+__global__ __launch_bounds__(kBlock) void k_apply(DeviceState d, KernelParams kp,
+                                                  const int64_t* summaries, uint32_t world,
+                                                  uint32_t rank, int32_t* fired)
+{
+    __shared__ uint32_t s_u[kWaves], s_f[kWaves];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t budget = kp.max_spikes;
+    const float R = *d.reward, rb = *d.rbar;  // pass-start values (C1), brain.metal:105-106
+    uint64_t off = 0;
+    for (uint32_t r = 0; r < rank && r < world; ++r)
+        off += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 0];
+    off = off < budget ? off : budget;
+
+    const uint32_t n_act = d.work->n_active;
+    uint32_t upd = 0, nf = 0;
+    for (uint32_t i = blockIdx.x; i < n_act; i += gridDim.x) {
+        const uint32_t c = d.active[i];
+        const uint64_t P = off + d.chunk_pre[c];
+        if (P >= budget) continue;
+        const uint32_t n = d.chunk_cnt[c].x;
+        const uint64_t base = (uint64_t)c * kChunk;
+        for (uint32_t j = tid; j < n; j += kBlock) {
+            const uint4 e = d.g2buf[base + j];
+            const uint64_t pre = P + ((e.x >> 11) & 0x7FFu);
+            if (pre >= budget) continue;  // budget == 0 at this event: brain.metal:85-88
+            const bool f = (e.x >> 22) & 1u;
+            const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.w));
+            float* wp = reinterpret_cast<float*>(d.syn + base + (e.x & 0x7FFu)) + 2;
+            *wp = w;                                  // brain.metal:122 (src/dst/pad unchanged)
+            ++upd;
+            if (f) {
+                fired[pre] = (int32_t)e.y;            // spike list in budget order
+                ++nf;
+            }
+        }
+    }
+    const uint32_t wu = wave_sum(upd), wf = wave_sum(nf);
+    if ((tid & 63) == 0) {
+        s_u[tid >> 6] = wu;
+        s_f[tid >> 6] = wf;
+    }
+    __syncthreads();
+    if (tid == 0)
+        d.apply_partial[blockIdx.x] =
+            make_uint2(s_u[0] + s_u[1] + s_u[2] + s_u[3], s_f[0] + s_f[1] + s_f[2] + s_f[3]);
+}
+
+// ---------------------------------------------------------------------------
+// k_finalize: stamps, rBar, clock tick, statistics (one workgroup).
+__global__ __launch_bounds__(kBlock) void k_finalize(DeviceState d, KernelParams kp,
+                                                     const int64_t* summaries, uint32_t world,
+                                                     const int32_t* fired)
+{
+    __shared__ uint32_t s_u[kWaves], s_f[kWaves];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t now = *d.clock;
+    const uint64_t budget = kp.max_spikes;
+    uint64_t total = 0, events = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+        total += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 0];
+        events += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 2];
+    }
+    const uint64_t n_fired = total < budget ? total : budget;
+    for (uint64_t i = tid; i < n_fired; i += kBlock)
+        d.last_fired[(uint32_t)fired[i]] = now;      // brain.metal:125-126, deferred
+
+    uint32_t upd = 0, nf = 0;
+    for (uint32_t i = tid; i < (uint32_t)kApplyGrid; i += kBlock) {
+        const uint2 v = d.apply_partial[i];
+        upd += v.x;
+        nf += v.y;
+    }
+    upd = wave_sum(upd);
+    nf = wave_sum(nf);
+    if ((tid & 63) == 0) {
+        s_u[tid >> 6] = upd;
+        s_f[tid >> 6] = nf;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const float R = *d.reward, rb = *d.rbar;
+        if (summaries[1] != 0 && budget > 0)
+            *d.rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
+        if (events > 0) *d.clock = now + kp.clock_inc; // brain.metal:129
+        PassWork* w = d.work;
+        w->stats.passes += 1;
+        w->stats.events += w->events;
+        w->stats.pre_gated += w->g1;
+        w->stats.post_gated += w->g2;
+        w->stats.updated += s_u[0] + s_u[1] + s_u[2] + s_u[3];
+        w->stats.fired += s_f[0] + s_f[1] + s_f[2] + s_f[3];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_renorm: brain.metal:135-145; base (= the ticked clock) passed by the host.
+__global__ __launch_bounds__(kBlock) void k_renorm(DeviceState d, uint64_t base)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < d.n_nrn) d.last_fired[i] -= base;
+    if (i == 0) *d.clock = 0;
+}
+
+// ---------------------------------------------------------------------------
+// k_generate: synthetic graph (recipe of brain-engine.cpp:31-53, portable RNG).
+__global__ __launch_bounds__(kBlock) void k_generate(DeviceState d, uint32_t n_in, uint32_t n_out,
+                                                     uint64_t seed)
+{
+    const uint64_t n_io = (uint64_t)n_in * n_out;
+    const uint64_t lo = (uint64_t)n_in + n_out;
+    const uint64_t range = d.n_nrn - lo;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < d.n_syn; k += stride) {
+        const uint64_t i = d.syn_offset + k;
+        const uint64_t x2 = splitmix64_at(seed, 3u * i + 2u);
+        uint4 r;
+        if (i < n_io) {
+            r.x = (uint32_t)(i / n_out);
+            r.y = n_in + (uint32_t)(i % n_out);
+            r.z = __float_as_uint(0.4f + unit24(x2) * (0.8f - 0.4f));
+        } else {
+            const uint64_t x0 = splitmix64_at(seed, 3u * i + 0u);
+            const uint64_t x1 = splitmix64_at(seed, 3u * i + 1u);
+            r.x = (uint32_t)(lo + (((x0 >> 32) * range) >> 32));
+            r.y = (uint32_t)(lo + (((x1 >> 32) * range) >> 32));
+            r.z = __float_as_uint(0.1f + unit24(x2) * (0.2f - 0.1f));
+        }
+        r.w = 0u;
+        d.syn[k] = r;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_checksum(DeviceState d, uint64_t* out)
+{
+    __shared__ uint64_t s[kWaves];
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t acc = 0;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < d.n_syn; k += stride) {
+        const uint4 r = d.syn[k];
+        const uint64_t i = d.syn_offset + k;
+        const uint64_t a = ((uint64_t)r.x << 32) | r.y;
+        const uint64_t b = ((uint64_t)r.z << 32) | r.w;
+        acc += mix64(a ^ mix64(b + i * 0x9E3779B97F4A7C15ull));
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd((unsigned long long*)out, (unsigned long long)(s[0] + s[1] + s[2] + s[3]));
+}
+
+__global__ __launch_bounds__(kBlock) void k_stamp_list(DeviceState d, const uint32_t* idx,
+                                                       uint64_t n, const uint64_t* value_dev,
+                                                       uint64_t value)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t v = value_dev ? *value_dev : value;
+    if (i < n && idx[i] < d.n_nrn) d.last_fired[idx[i]] = v;
+}
+
+inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,
+                         uint64_t stim_count, hipStream_t s)
+{
+    if (d.n_nrn == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bitmap, dim3(blocks_for(d.n_nrn)), dim3(kBlock), 0, s, d, kp, stim_first,
+                       stim_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s)
+{
+    if (d.n_chunks == 0) return hipSuccess;
+    if (kp.track_visits)
+        hipLaunchKernelGGL(k_gate<true>, dim3(d.n_chunks), dim3(kBlock), 0, s, d, kp);
+    else
+        hipLaunchKernelGGL(k_gate<false>, dim3(d.n_chunks), dim3(kBlock), 0, s, d, kp);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int64_t* summary_out,
+                       hipStream_t s)
+{
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, d, kp, summary_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
+                        uint32_t world, uint32_t rank, int32_t* fired, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_apply, dim3(kApplyGrid), dim3(kBlock), 0, s, d, kp, summaries, world,
+                       rank, fired);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
+                           uint32_t world, const int32_t* fired, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, s, d, kp, summaries, world, fired);
+    return hipGetLastError();
+}
+
+hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_renorm, dim3(blocks_for(d.n_nrn > 0 ? d.n_nrn : 1)), dim3(kBlock), 0, s,
+                       d, base);
+    return hipGetLastError();
+}
+
+hipError_t launch_generate(const DeviceState& d, uint32_t n_in, uint32_t n_out, uint64_t seed,
+                           hipStream_t s)
+{
+    if (d.n_syn == 0) return hipSuccess;
+    uint32_t grid = blocks_for(d.n_syn);
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(k_generate, dim3(grid), dim3(kBlock), 0, s, d, n_in, n_out, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_checksum(const DeviceState& d, uint64_t* out_dev, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(out_dev, 0, sizeof(uint64_t), s);
+    if (e != hipSuccess || d.n_syn == 0) return e;
+    uint32_t grid = blocks_for(d.n_syn);
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(k_checksum, dim3(grid), dim3(kBlock), 0, s, d, out_dev);
+    return hipGetLastError();
+}
+
+hipError_t launch_stamp_list(const DeviceState& d, const uint32_t* idx_dev, uint64_t n,
+                             const uint64_t* value_dev, uint64_t value, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_stamp_list, dim3(blocks_for(n)), dim3(kBlock), 0, s, d, idx_dev, n,
+                       value_dev, value);
+    return hipGetLastError();
+}
+
+}  // namespace abnn

@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Benchmark: traversal events/s of the C1 synapse sweep on MI355X.
+
+Workload (BASELINE.json configs[2], constants.h defaults): N_NRN = 5,000,512
+(256 in + 256 out + 5M hidden), N_SYN = 1e9 (16 GB of 16-B SynapsePacked in
+HBM), EVENTS_PER_PASS = 150M (150,000,128 visits per pass).  Synthetic graph =
+the build_random_graph recipe (brain-engine.cpp:31-53) with the portable RNG,
+generated on the GPU; every pass stamps all 256 inputs.
+
+One "step" = one whole pass: stimulus + bitmap + streaming gate + budget scan +
+apply + finalize (+ the two exchanges at N>1).  `value` = visited events of all
+ranks per second over the K timed steps (max over ranks of the wall time).
+
+N > 1 (torchrun, one process per GPU, RCCL): the 1B-synapse graph is split in
+N contiguous shards; every GPU sweeps 150M events of its shard per pass
+(capped by the shard: 125M at N = 8), so per-GPU work is fixed -> "weak".
+
+Extra JSON fields: `roofline` (the gate kernel: algorithmic bytes per launch /
+its HIP-event-timed average duration vs 8 TB/s) and `cpu_baseline` (the
+threaded C oracle on this host, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-passes", type=int, default=3)
+    return ap.parse_args()
+
+
+def algorithmic_bytes(stats: dict, track_visits: bool) -> int:
+    """SURVEY.md §8(d) per-event figure for the gate kernel's share of a pass:
+    16 B SynapsePacked read + 8 B lastFired[src] per visited event (+8 B
+    lastVisited write with track_visits) and 8 B lastFired[dst] per pre-gated
+    event.  (The 16 B write-back per update and 8 B per spike happen in the
+    apply/finalize kernels and are reported separately.)"""
+    e = stats["events"]
+    return 24 * e + (8 * e if track_visits else 0) + 8 * stats["pre_gated"]
+
+
+def load_traffic(config: str):
+    p = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def cpu_baseline(wl, threads: int, timed_passes: int) -> dict:
+    """The threaded C oracle ("port") on the host cores, same workload.  The sweep
+    only ever touches the first E synapses, so the sample holds exactly those and
+    produces the identical pass results; 6 untimed passes reach the steady state."""
+    from oracle import oracle as O
+
+    E = O.visited_events(wl.events, wl.n_syn)
+    ob = O.OracleBrain(wl.n_input, wl.n_output, wl.n_hidden, E, wl.events)
+    ob.build_random_graph(1, nthreads=threads)
+    ob.set_auto_stimulus(0, wl.n_input)
+    ob.pass_threaded(6, nthreads=threads)
+    t0 = time.perf_counter()
+    ob.pass_threaded(timed_passes, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": timed_passes * E / dt, "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"first {E:,} synapses of the {wl.name} graph (all the sweep touches), "
+                      f"{wl.n_neuron:,} neurons, 6 untimed + {timed_passes} timed passes, "
+                      f"oracle_pass_threaded with {threads} threads"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    from abnn_amd import CONFIGS, Brain
+    from abnn_amd.shard import ShardedBrain, TorchComm
+
+    wl = CONFIGS[args.config]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    if world > 1:
+        sb = ShardedBrain(TorchComm(), wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events,
+                          device=local_rank)
+        brain = sb.brain
+        step = sb.step
+    else:
+        brain = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, device=local_rank)
+        step = brain.encode_traversal
+    brain.build_random_graph(1)
+    brain.set_auto_stimulus(0, wl.n_input)
+    local_events = brain.visited_events()
+
+    def sync():
+        brain.synchronize()
+        torch.cuda.synchronize(local_rank)
+        if dist is not None:
+            dist.barrier()
+
+    step(args.warmup)
+    sync()
+    brain.reset_stats()
+    brain.enable_timing(True)
+    sync()
+    t0 = time.perf_counter()
+    step(args.steps)
+    sync()
+    dt = time.perf_counter() - t0
+    gate_ms, launches = brain.kernel_time()
+    stats = brain.stats()
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        ev = torch.tensor([stats["events"]], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
+        total_events = float(ev.item())
+    else:
+        total_events = float(stats["events"])
+
+    if rank == 0:
+        value = total_events / dt
+        avg_gate_ms = gate_ms / max(1, launches)
+        bytes_per_launch = algorithmic_bytes(stats, bool(brain.params.track_visits)) / max(1, launches)
+        achieved = bytes_per_launch / (avg_gate_ms * 1e-3) / 1e9
+        traffic = load_traffic(args.config) if world == 1 else None
+        roofline = {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic.get("bytes_per_launch") if traffic else None,
+            "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4),
+            "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "bytes_formula": "24*E + 8*G1 (SURVEY §8d; E visited, G1 pre-gated)",
+            "pass_ms": round(dt / args.steps * 1e3, 4),
+        }
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+            cpu = cpu_baseline(wl, threads, args.cpu_passes)
+        out = {
+            "metric": "traversal events/sec at 1B synapses, 5M neurons; achieved HBM GB/s",
+            "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (build_random_graph recipe, portable RNG, generated on GPU)",
+            "config": {
+                "workload": f"{wl.name}: {wl.note}", "n_neuron": wl.n_neuron, "n_syn": wl.n_syn,
+                "events_per_pass_per_gpu": wl.events, "visited_events_per_pass_per_gpu": local_events,
+                "parallelism": f"synapse-shard dp{world}" if world > 1 else "single GPU",
+                "pre_gated_frac": stats["pre_gated"] / max(1, stats["events"]),
+                "spikes_per_pass": stats["fired"] / max(1, stats["passes"]),
+            },
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

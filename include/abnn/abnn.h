@@ -1,0 +1,254 @@
+/*
+ * abnn.h -- C-ABI of the MI355X-native Monte-Carlo synapse traversal engine.
+ *
+ * This is the drop-in boundary for the reference's hot path:
+ *   - the host class `Brain`            (abnn/src/core/brain/brain.h:24-83,
+ *                                        abnn/src/core/brain/brain.cpp:21-178)
+ *   - the kernel buffer-index ABI of    `monte_carlo_traversal`
+ *                                       (abnn/src/core/kernels/brain.metal:41-58)
+ *     and `renormalise_clock_and_times` (brain.metal:135-145)
+ * Paths are relative to the reference root.  Every entry point below names the
+ * reference interface it replaces.
+ *
+ * Rules of the boundary:
+ *   - plain C types only (no torch, no HIP types: streams are `void*` that hold
+ *     a hipStream_t, NULL = the handle's own stream);
+ *   - every function returns an abnn_status; no exception crosses the ABI
+ *     (the reference threw a *pointer* `new std::exception()` from Brain::load,
+ *     brain.cpp:174 -- here that case is ABNN_ERR_SIZE_MISMATCH);
+ *   - device pointers returned by abnn_state_ptrs are BORROWED (the handle
+ *     owns them), exactly like the unretained MTL::Buffer getters of
+ *     brain.h:54-58;
+ *   - a handle is not thread-safe: the caller serialises (the reference drove
+ *     one Brain from one worker thread, brain-engine.cpp:193-201).
+ *
+ * Semantics: every pass executes the deterministic legal schedule "C1" of the
+ * reference kernel: events in increasing tid order, an
+ * ordered global spike budget, all reads of lastFired/clock/rBar observe the
+ * pass-start values, stores become visible at pass end.
+ */
+#ifndef ABNN_ABNN_H
+#define ABNN_ABNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ABNN_ABI_VERSION 1
+
+typedef enum abnn_status {
+    ABNN_OK = 0,
+    ABNN_ERR_INVALID = 1,        /* bad argument / shape                          */
+    ABNN_ERR_HIP = 2,            /* a HIP runtime call failed (see abnn_last_error) */
+    ABNN_ERR_OOM = 3,            /* device or host allocation failed              */
+    ABNN_ERR_SIZE_MISMATCH = 4,  /* .bnn header does not match (brain.cpp:174)    */
+    ABNN_ERR_IO = 5,             /* file open/read/write failed                   */
+    ABNN_ERR_NO_DEVICE = 6       /* no HIP device / bad ordinal                   */
+} abnn_status;
+
+/* SynapsePacked -- brain.metal:11, brain.h:21, README §2.2.  16 bytes, AoS. */
+typedef struct abnn_synapse {
+    uint32_t src;
+    uint32_t dst;
+    float w;
+    float pad; /* always 0, never read (brain.metal:11) */
+} abnn_synapse;
+
+/* Sizes fixed at construction: Brain(nInput, nOutput, nHidden, nSynapses,
+ * eventsPerPass), brain.h:27-31.  N_NRN = n_input + n_output + n_hidden
+ * (brain.cpp:24).  64-bit where the reference used uint32_t (4B synapses). */
+typedef struct abnn_dims {
+    uint32_t n_input;            /* 256 (constants.h:2)                         */
+    uint32_t n_output;           /* 256 (constants.h:3)                         */
+    uint64_t n_hidden;           /* 5'000'000 (constants.h:4)                   */
+    uint64_t n_syn;              /* synapses held by THIS handle (its shard)    */
+    uint64_t events_per_pass;    /* EVENTS_PER_PASS (constants.h:11); visited
+                                    events per pass are
+                                    min(roundup(events,256), n_syn) (brain.cpp:117,
+                                    brain.metal:61)                            */
+    uint64_t syn_offset;         /* global id of local synapse 0 (sharding; 0)   */
+    uint64_t global_events;      /* sum over shards of visited events per pass;
+                                    0 = this handle alone (used for the clock
+                                    tick rule, brain.metal:61,129)             */
+} abnn_dims;
+
+/* Every knob of the path with the reference default (abnn_default_params). */
+typedef struct abnn_params {
+    float base_scale;        /* 0.8f    BASE_SCALE      brain.metal:22 */
+    uint32_t refractory;     /* 2       REFRACTORY      brain.metal:23 */
+    uint32_t window_pre;     /* 5       WINDOW_PRE      brain.metal:24 */
+    uint32_t clock_inc;      /* 1       CLOCK_INC       brain.metal:26 */
+    float target_rate_hz;    /* 1000    TARGET_RATE_HZ  brain.metal:28 */
+    float eta_home;          /* 1e-6    ETA_HOME        brain.metal:29 */
+    float eta_reward;        /* 1e-3    ETA_REWARD      brain.metal:30 */
+    float alpha_rbar;        /* 1e-3    ALPHA_RBAR      brain.metal:31 */
+    float a_ltp;             /* 0.04f   _aLTP           constants.h:16 */
+    float a_ltd;             /* 0.02f   _aLTD           constants.h:17 */
+    float w_min;             /* 0.001f  _wMin           constants.h:18 */
+    float w_max;             /* 1.0f    _wMax           constants.h:19 */
+    uint32_t max_spikes;     /* 2560    kMaxSpikes      brain.h:18     */
+    uint32_t tick_ns;        /* 1000    kTickNS         brain.h:17     */
+    uint32_t tau_vis;        /* 50000   brain.cpp:102 (bound, unused: brain.metal:47) */
+    uint32_t tau_pre;        /* 50000   brain.cpp:102 (bound, unused: brain.metal:48) */
+    uint64_t renorm_thresh;  /* 4000000 kRenormThresh   brain.h:19     */
+    uint32_t track_visits;   /* 0: lastVisited untouched (reference code,
+                                brain.metal:44); 1: lastVisited[dst] = now for
+                                every visited event (README §4)        */
+    uint32_t reserved0;
+    uint64_t seed;           /* seed of the handle's host RNG (inject_inputs) */
+} abnn_params;
+
+/* Scalar state (brain.cpp:57-60): clock, reward, running-average reward. */
+typedef struct abnn_scalars {
+    uint64_t clock;          /* u64 (u32 in brain.cpp:57; identical < 2^32) */
+    float reward;
+    float rbar;
+} abnn_scalars;
+
+/* Cumulative per-handle pass statistics (for the roofline byte count). */
+typedef struct abnn_stats {
+    uint64_t passes;
+    uint64_t events;         /* E: visited events                        */
+    uint64_t pre_gated;      /* G1: passed the pre-spike gate (brain.metal:73-77) */
+    uint64_t post_gated;     /* passed the refractory gate (brain.metal:79-83)   */
+    uint64_t updated;        /* G2: reached the weight update (budget > 0)       */
+    uint64_t fired;          /* F: spikes emitted (lastFired stamps)             */
+} abnn_stats;
+
+/* Borrowed device pointers (brain.h:54-58 buffer getters). */
+typedef struct abnn_state {
+    abnn_synapse* synapses;  /* n_syn records (bufSyn_)                  */
+    uint64_t* last_fired;    /* N_NRN (bufLastFire_)                     */
+    uint64_t* last_visited;  /* N_NRN (bufLastVisit_)                    */
+    uint64_t* clock;         /* 1 (bufClock_)                            */
+    float* reward;           /* 1 (bufReward_)                           */
+    float* rbar;             /* 1 (bufRBar_)                             */
+} abnn_state;
+
+typedef struct abnn_brain abnn_brain;
+
+/* ---- library ------------------------------------------------------------ */
+int abnn_abi_version(void);
+const char* abnn_status_string(abnn_status s);
+/* Last error message of the calling thread (empty string if none). */
+const char* abnn_last_error(void);
+/* Reference defaults for every knob (brain.metal:22-31, constants.h:16-19,
+ * brain.h:17-19, brain.cpp:102). */
+void abnn_default_params(abnn_params* out);
+/* Number of HIP devices visible (0 without a GPU; never fails). */
+int abnn_device_count(void);
+
+/* ---- lifetime: Brain::Brain + build_pipeline + build_buffers -------------
+ * brain.cpp:21-26 (ctor), brain.cpp:38-48 (build_pipeline: kernels are
+ * compiled in, nothing to build), brain.cpp:52-69 (build_buffers: allocate
+ * and zero; budget = kMaxSpikes; reward = rBar = 0; clock = 0).            */
+abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params,
+                              int device, abnn_brain** out);
+/* ~Brain / release_all, brain.cpp:27-34. */
+abnn_status abnn_brain_destroy(abnn_brain* b);
+abnn_status abnn_get_dims(const abnn_brain* b, abnn_dims* out);
+abnn_status abnn_get_params(const abnn_brain* b, abnn_params* out);
+abnn_status abnn_state_ptrs(abnn_brain* b, abnn_state* out);
+/* n_neuron() = n_input + n_output + n_hidden (brain.h:51). */
+uint64_t abnn_n_neuron(const abnn_brain* b);
+
+/* ---- synapses ------------------------------------------------------------ */
+/* Host -> device copy of records [first, first+n) (the reference wrote the
+ * Managed buffer directly, brain-engine.cpp:37-52). */
+abnn_status abnn_upload_synapses(abnn_brain* b, uint64_t first,
+                                 const abnn_synapse* src, uint64_t n);
+abnn_status abnn_download_synapses(abnn_brain* b, uint64_t first,
+                                   abnn_synapse* dst, uint64_t n);
+/* Synthetic graph with the recipe of build_random_graph (brain-engine.cpp:31-53)
+ * and this library's portable counter-based RNG: global record
+ * i < n_input*n_output is the dense block {i/n_out, n_in + i%n_out,
+ * w~U(0.4,0.8)}; the rest {src,dst ~ U[n_in+n_out, N_NRN-1], w~U(0.1,0.2)}.
+ * Generated on the device, shard-aware (uses syn_offset).                   */
+abnn_status abnn_generate_synapses(abnn_brain* b, uint64_t seed);
+/* Order-sensitive 64-bit checksum of the local synapse array (device-side). */
+abnn_status abnn_checksum_synapses(abnn_brain* b, uint64_t* out);
+
+/* ---- neuron timestamps / scalars ----------------------------------------- */
+abnn_status abnn_get_last_fired(abnn_brain* b, uint64_t first, uint64_t* out, uint64_t n);
+abnn_status abnn_set_last_fired(abnn_brain* b, uint64_t first, const uint64_t* src, uint64_t n);
+abnn_status abnn_get_last_visited(abnn_brain* b, uint64_t first, uint64_t* out, uint64_t n);
+abnn_status abnn_set_last_visited(abnn_brain* b, uint64_t first, const uint64_t* src, uint64_t n);
+/* lastFired[idx[i]] = value for i < n (teacher / input spikes written by the
+ * host, brain.cpp:82, brain-engine.cpp:131). */
+abnn_status abnn_set_timestamps(abnn_brain* b, const uint32_t* idx, uint64_t n, uint64_t value);
+abnn_status abnn_get_scalars(abnn_brain* b, abnn_scalars* out);
+abnn_status abnn_set_scalars(abnn_brain* b, const abnn_scalars* in);
+/* *reward = r (brain-engine.cpp:180-182). */
+abnn_status abnn_set_reward(abnn_brain* b, float r);
+
+/* ---- pass-boundary hooks --------------------------------------------------
+ * Brain::inject_inputs(vals, hz), brain.cpp:73-83: for every input i,
+ * lastFired[i] = clock when uni() < hz*kTickNS*NSEC_PER_SEC * v[i]; uni() is
+ * the handle's seeded host RNG (params.seed) instead of a random_device mt19937.
+ * n must equal n_input (the reference asserts it, brain.cpp:75).            */
+abnn_status abnn_inject_inputs(abnn_brain* b, const float* v, uint32_t n, float hz);
+/* Brain::read_outputs(), brain.cpp:145-157: out[o] = 1 iff
+ * ts = lastFired[n_input+o] != 0 && start <= ts < now, start = now>1 ? now-1 : 0.
+ * n must equal n_output.                                                     */
+abnn_status abnn_read_outputs(abnn_brain* b, uint8_t* out, uint32_t n);
+/* Stamp lastFired[first, first+count) = clock at the start of EVERY pass
+ * (fused into the pass; the bench stimulus of SURVEY §8d).  count = 0 = off. */
+abnn_status abnn_set_auto_stimulus(abnn_brain* b, uint64_t first, uint64_t count);
+
+/* ---- passes: Brain::encode_traversal + commit/wait ------------------------
+ * brain.cpp:87-141 + brain-engine.cpp:136-141.  Enqueues `passes` whole C1
+ * passes (traversal + clock tick + renormalisation when the pass-start clock
+ * exceeds renorm_thresh) on `stream` (NULL = the handle's stream).  Returns
+ * without waiting; abnn_synchronize waits.                                    */
+abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream);
+abnn_status abnn_synchronize(abnn_brain* b, void* stream);
+
+/* ---- sharded passes (synapse-shard data parallelism) --------
+ * One pass on rank r of W = three calls with two tiny exchanges between them:
+ *   abnn_shard_gate   -> writes this shard's summary (ABNN_SUMMARY_WORDS int64)
+ *                        to `summary_dev`;
+ *   [all-gather the W summaries into `summaries_dev` (W*ABNN_SUMMARY_WORDS)]
+ *   abnn_shard_apply  -> zeroes `fired_dev` (max_spikes int32) and writes this
+ *                        shard's spikes at their global budget positions;
+ *   [all-reduce(SUM) `fired_dev` across ranks]
+ *   abnn_shard_commit -> stamps lastFired, updates rBar, ticks the clock,
+ *                        renormalises if due.
+ * All pointers are device pointers; the exchanges are the caller's (RCCL via
+ * torch.distributed in abnn_amd/shard.py).  W = 1 with the local summary is
+ * exactly abnn_traverse.                                                     */
+#define ABNN_SUMMARY_WORDS 4 /* {spike candidates (capped), t0 updated, events, g2} */
+abnn_status abnn_shard_gate(abnn_brain* b, int64_t* summary_dev, void* stream);
+abnn_status abnn_shard_apply(abnn_brain* b, const int64_t* summaries_dev,
+                             uint32_t world, uint32_t rank, int32_t* fired_dev,
+                             void* stream);
+abnn_status abnn_shard_commit(abnn_brain* b, const int64_t* summaries_dev,
+                              uint32_t world, const int32_t* fired_dev,
+                              void* stream);
+
+/* ---- statistics / timing ---------------------------------------------------- */
+abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out);   /* synchronises */
+abnn_status abnn_reset_stats(abnn_brain* b);
+/* When on, every pass records HIP events around the gate (streaming) kernel on
+ * the stream it is launched on; abnn_get_kernel_time returns the summed
+ * milliseconds and the launch count since the last reset.                  */
+abnn_status abnn_enable_timing(abnn_brain* b, int on);
+abnn_status abnn_get_kernel_time(abnn_brain* b, double* ms_total, uint64_t* launches);
+
+/* ---- persistence ------------------------------------------------------------
+ * .bnn = u32 N_SYN, u32 N_NRN, N_SYN x 16-B SynapsePacked (Brain::save/load,
+ * brain.cpp:161-178).  Load of a mismatched header -> ABNN_ERR_SIZE_MISMATCH.  */
+abnn_status abnn_save_bnn(abnn_brain* b, const char* path);
+abnn_status abnn_load_bnn(abnn_brain* b, const char* path);
+/* README §2 flat buffer: 16-B header {u32 N_SYN, u32 N_NRN, 8 B pad},
+ * synapses (u32 src, u32 dst) x N_SYN, weights f32 x N_SYN,
+ * lastFiredNS u64 x N_NRN, lastVisitedNS u64 x N_NRN.                         */
+abnn_status abnn_save_flat(abnn_brain* b, const char* path);
+abnn_status abnn_load_flat(abnn_brain* b, const char* path);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+#endif /* ABNN_ABNN_H */

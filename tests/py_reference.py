@@ -1,0 +1,135 @@
+"""Independent pure-Python restatement of brain.metal for SMALL cases.
+
+Test infrastructure: written as an emulator of the Metal kernel's threads
+(abnn/src/core/kernels/brain.metal:41-130) rather than as the C1 loop of the C
+oracle, so the two restatements can check each other.  Metal relaxed atomics
+are modelled as "cells": every load of lastF / clock / rBar returns the value
+at kernel start (schedule C1), stores land in a pending set applied when the
+kernel ends; the budget cell is sequentially consistent in tid order.  fp32
+arithmetic uses numpy.float32 scalars so every operation rounds to fp32 on its
+own (the C oracle and the HIP kernels are built with -ffp-contract=off).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+F = np.float32
+U32 = 0xFFFFFFFF
+U64 = 0xFFFFFFFFFFFFFFFF
+
+
+def rand01(s: int) -> np.float32:
+    s &= U32
+    s ^= (s << 13) & U32
+    s ^= s >> 17
+    s ^= (s << 5) & U32
+    return F(s & 0xFFFFFF) * F(1.0 / 16777216.0)
+
+
+def metal_clamp(x, lo, hi):
+    return min(max(x, lo), hi)
+
+
+class Cell:
+    """A device atomic with deferred visibility (C1)."""
+
+    def __init__(self, v):
+        self.v = v
+        self.pending = None
+
+    def load(self):
+        return self.v
+
+    def store(self, v):
+        self.pending = v
+
+    def commit(self):
+        if self.pending is not None:
+            self.v, self.pending = self.pending, None
+
+
+class MetalEmu:
+    """State of one Brain: synapse list, lastFired cells, scalars."""
+
+    def __init__(self, syn_src, syn_dst, syn_w, n_nrn, events, params):
+        self.src = [int(x) for x in syn_src]
+        self.dst = [int(x) for x in syn_dst]
+        self.w = [F(x) for x in syn_w]
+        self.lastF = [0] * n_nrn
+        self.lastV = [0] * n_nrn
+        self.clock = 0
+        self.reward = F(0.0)
+        self.rbar = F(0.0)
+        self.events = int(events)
+        self.p = params
+        self.stim = (0, 0)
+
+    def kernel(self):
+        """One dispatch of monte_carlo_traversal over roundup(EVENTS,256) threads."""
+        p = self.p
+        n_syn = len(self.src)
+        grid = (self.events + 255) // 256 * 256
+        lastF = [Cell(v) for v in self.lastF]
+        clock = Cell(self.clock)
+        rbar = Cell(self.rbar)
+        budget = p["max_spikes"]   # host reset, brain.cpp:90 (sequentially consistent)
+        now_tg = clock.load()      # every TG caches the same pass-start value under C1
+        ticked = False
+        for tid in range(grid):
+            if tid >= n_syn:
+                break                               # brain.metal:61
+            now = now_tg
+            lp = lastF[self.src[tid]].load()
+            if (now - lp) & U64 > p["window_pre"]:
+                ticked |= tid == 0
+                continue
+            ld = lastF[self.dst[tid]].load()
+            if (now - ld) & U64 <= p["refractory"]:
+                ticked |= tid == 0
+                continue
+            if budget == 0:
+                ticked |= tid == 0
+                continue
+            w = self.w[tid]
+            prob = metal_clamp(F(w * w) * F(p["base_scale"]), F(0.0), F(1.0))
+            fired = prob > rand01((tid & U32) ^ (now & U32))
+            if fired:
+                old = budget
+                budget -= 1
+                if old == 0:
+                    fired = False
+            dW = F(F(p["a_ltp"]) * F(F(1.0) - w)) if fired else F(F(-p["a_ltd"]) * w)
+            R = self.reward
+            rb = rbar.load()
+            dW = F(dW + F(F(F(p["eta_reward"]) * F(R - rb)) * F(1.0 if fired else 0.0)))
+            if tid == 0:
+                rbar.store(F(rb + F(F(p["alpha_rbar"]) * F(R - rb))))
+            isi = F((now - ld) & U64)
+            est = F(F(1e6) / isi) if isi > F(0.0) else F(0.0)
+            dW = F(dW + F(F(F(p["eta_home"]) * F(F(p["target_rate_hz"]) - est)) * w))
+            self.w[tid] = metal_clamp(F(w + dW), F(p["w_min"]), F(p["w_max"]))
+            if fired:
+                lastF[self.dst[tid]].store(now)
+            ticked |= tid == 0
+        for c in lastF:
+            c.commit()
+        rbar.commit()
+        self.lastF = [c.v for c in lastF]
+        self.rbar = rbar.v
+        if ticked:
+            self.clock = (now_tg + p["clock_inc"]) & U64
+        if p.get("track_visits"):
+            for tid in range(min(grid, n_syn)):
+                self.lastV[self.dst[tid]] = now_tg
+
+    def one_pass(self):
+        """run_one_pass minus the host driver: stimulus, kernel, renorm (brain.cpp:87-141)."""
+        first, count = self.stim
+        for i in range(first, first + count):
+            self.lastF[i] = self.clock
+        renorm = self.clock > self.p["renorm_thresh"]   # host read before the pass
+        self.kernel()
+        if renorm:                                      # brain.metal:135-145
+            base = self.clock
+            self.lastF = [(v - base) & U64 for v in self.lastF]
+            self.clock = 0

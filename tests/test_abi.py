@@ -1,0 +1,105 @@
+"""CPU checks of the drop-in boundary: the HIP library loads, exports every
+symbol include/abnn/abnn.h declares, the ctypes mirrors match the C layouts,
+and the no-GPU path fails loudly instead of falling back."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "abnn", "abnn.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*(abnn_[a-z0-9_]+)\s*\(",
+                                 src, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from abnn_amd import _lib
+
+    lib = C.CDLL(_lib.LIB_PATH)
+    names = declared_functions()
+    assert len(names) >= 35
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert set(names) == bound, set(names) ^ bound
+
+
+def test_struct_layouts_match_c(tmp_path):
+    from abnn_amd import _lib
+    from oracle import oracle as O
+
+    prog = tmp_path / "sz.c"
+    prog.write_text('#include "abnn/abnn.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+                    'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(abnn_synapse),'
+                    'sizeof(abnn_dims), sizeof(abnn_params), sizeof(abnn_scalars), sizeof(abnn_stats),'
+                    'sizeof(abnn_state), offsetof(abnn_params, renorm_thresh));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(prog)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    want = [16, C.sizeof(_lib.Dims), C.sizeof(_lib.Params), C.sizeof(_lib.Scalars),
+            C.sizeof(_lib.Stats), C.sizeof(_lib.State), _lib.Params.renorm_thresh.offset]
+    assert got == want
+    assert C.sizeof(O.Params) == C.sizeof(_lib.Params) and C.sizeof(O.Dims) == C.sizeof(_lib.Dims)
+
+
+def test_default_params_equal_oracle():
+    from abnn_amd import _lib
+    from oracle import oracle as O
+
+    a, b = _lib.default_params(), O.default_params()
+    for name, _ in _lib.Params._fields_:
+        assert getattr(a, name) == getattr(b, name), name
+
+
+def test_abi_version_and_status_strings():
+    from abnn_amd import _lib
+
+    lib = _lib.load()
+    assert lib.abnn_abi_version() == 1
+    assert lib.abnn_status_string(0) == b"ok"
+    assert lib.abnn_status_string(4) == b"size mismatch"
+
+
+def test_no_gpu_fails_loudly():
+    import abnn_amd
+
+    if abnn_amd.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(abnn_amd.AbnnError) as e:
+        abnn_amd.Brain(256, 256, 488, 10_000, 100_000)
+    assert e.value.status == 6  # ABNN_ERR_NO_DEVICE
+
+
+def test_missing_library_is_an_import_error(monkeypatch, tmp_path):
+    from abnn_amd import _lib
+
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(ImportError):
+        _lib.load()
+
+
+def test_gpu_kernels_built_for_gfx950():
+    from abnn_amd import _lib
+
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"k_gate" in data
+
+
+def test_shard_partition_helpers():
+    from abnn_amd.shard import global_events, shard_ranges
+
+    r = shard_ranges(10, 3)
+    assert r == [(0, 4), (4, 7), (7, 10)]
+    assert shard_ranges(1_000_000_000, 8)[7] == (875_000_000, 1_000_000_000)
+    assert global_events(1_000_000_000, 150_000_000, 1) == 150_000_128
+    assert global_events(1_000_000_000, 150_000_000, 8) == 1_000_000_000
+    assert global_events(1_000_000_000, 150_000_000, 2) == 2 * 150_000_128

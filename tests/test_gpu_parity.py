@@ -1,0 +1,283 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the CPU oracle, bit-exact.
+
+Weights: bit-exact fp32 (both sides round every operation, -ffp-contract=off).
+Timestamps, clock, spike counts: bit-exact integers.  rBar: bit-exact fp32.
+(The oracle itself is "parity unpinned" against the Metal reference: DESIGN.md §3.)
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(n_hidden, n_syn, events, seed=1, stim=True, syn_offset=0, global_events=0, **params):
+    import abnn_amd
+    from oracle import oracle as O
+
+    g = abnn_amd.Brain(256, 256, n_hidden, n_syn, events, syn_offset=syn_offset,
+                       global_events=global_events, **params)
+    g.build_random_graph(seed)
+    o = O.OracleBrain(256, 256, n_hidden, n_syn, events, syn_offset=syn_offset,
+                      global_events=global_events, **params)
+    o.build_random_graph(seed, nthreads=16)
+    if stim:
+        g.set_auto_stimulus(0, 256)
+        o.set_auto_stimulus(0, 256)
+    return g, o
+
+
+def _assert_same(g, o, what=""):
+    syn = g.download_synapses()
+    assert np.array_equal(syn.view(np.uint32), o.syn.view(np.uint32)), f"synapses differ {what}"
+    assert np.array_equal(g.last_fired(), o.last_fired), f"lastFired differs {what}"
+    sg, so = g.scalars(), o.scalars()
+    assert sg["clock"] == so["clock"], what
+    assert np.float32(sg["rbar"]) == np.float32(so["rbar"]), what
+
+
+def test_generator_parity(gpu):
+    g, o = _pair(99_488, 3_000_000, 1000)
+    assert g.checksum() == o.checksum()
+    assert np.array_equal(g.download_synapses().view(np.uint32), o.syn.view(np.uint32))
+
+
+def test_config1_every_pass(gpu):
+    # BASELINE configs[0]: 1k neurons, 10k synapses, 100k events (10k visits)
+    g, o = _pair(488, 10_000, 100_000)
+    for k in range(64):
+        if k == 20:
+            g.set_reward(1.0)
+            o.set_reward(1.0)
+        g.encode_traversal(1)
+        o.pass_serial()
+        _assert_same(g, o, f"pass {k}")
+    assert g.stats() == o.stats()
+
+
+def test_c2_lite_every_pass(gpu):
+    # 100k neurons, 1M synapses: all-gated passes 3-5, then the budget-saturated steady state
+    g, o = _pair(99_488, 1_000_000, 1_000_000)
+    for k in range(12):
+        g.encode_traversal(1)
+        o.pass_threaded(nthreads=16)
+        _assert_same(g, o, f"pass {k}")
+    assert g.stats() == o.stats()
+
+
+def test_config2_full_state(gpu):
+    # BASELINE configs[1]: 100k neurons, 10M synapses, 10M events per pass
+    g, o = _pair(99_488, 10_000_000, 10_000_000)
+    for k in range(10):
+        if k == 7:
+            g.set_reward(-0.25)
+            o.set_reward(-0.25)
+        g.encode_traversal(1)
+        o.pass_threaded(nthreads=16)
+        if k in (3, 6, 9):
+            _assert_same(g, o, f"pass {k}")
+    assert g.stats() == o.stats()
+
+
+@pytest.mark.parametrize("over", [
+    dict(max_spikes=1), dict(max_spikes=0), dict(max_spikes=200_000),
+    dict(refractory=0, window_pre=0), dict(events=777_777), dict(events=3_000_000),
+    dict(events=100), dict(renorm_thresh=5), dict(track_visits=1),
+    dict(a_ltp=0.5, a_ltd=0.3, eta_home=1e-3, base_scale=3.0),
+])
+def test_edge_cases(gpu, over):
+    over = dict(over)
+    events = over.pop("events", 1_500_000)
+    g, o = _pair(50_000, 2_000_000, events, seed=5, **over)
+    for k in range(14):
+        if k == 9:
+            g.set_reward(0.5)
+            o.set_reward(0.5)
+        g.encode_traversal(1)
+        o.pass_threaded(nthreads=16)
+    _assert_same(g, o, str(over))
+    if over.get("track_visits"):
+        assert np.array_equal(g.last_visited(), o.last_visited)
+    if over.get("renorm_thresh"):
+        assert g.scalars()["clock"] < 8
+    assert g.stats() == o.stats()
+
+
+def test_empty_and_tiny(gpu):
+    import abnn_amd
+
+    b = abnn_amd.Brain(256, 256, 10, 0, 1000)
+    b.encode_traversal(3)
+    assert b.scalars()["clock"] == 0  # brain.metal:61: no thread, no tick
+    g, o = _pair(10, 1, 1)
+    g.encode_traversal(6)
+    o.pass_serial(6)
+    _assert_same(g, o)
+
+
+def test_inject_inputs_and_read_outputs(gpu):
+    g, o = _pair(488, 10_000, 100_000, stim=False, seed=9)
+    v = (np.arange(256) % 3 == 0).astype(np.float32) * 0.5
+    for k in range(12):
+        g.inject_inputs(v, 1000.0)
+        o.inject_inputs(v, 1000.0)
+        g.encode_traversal(1)
+        o.pass_serial()
+        assert np.array_equal(g.read_outputs(), o.read_outputs())
+    _assert_same(g, o)
+    g.set_timestamps([300, 301], 5)
+    o.set_timestamps([300, 301], 5)
+    assert np.array_equal(g.last_fired(), o.last_fired)
+
+
+def _virtual_shard_run(world, n_syn, events, passes, n_hidden=30_000, seed=4):
+    """`world` shard handles on one GPU driven phase by phase (what RCCL does across GPUs)."""
+    import torch
+
+    import abnn_amd
+    from abnn_amd.shard import global_events, shard_ranges
+
+    ge = global_events(n_syn, events, world)
+    shards = []
+    for lo, hi in shard_ranges(n_syn, world):
+        b = abnn_amd.Brain(256, 256, n_hidden, hi - lo, events, syn_offset=lo, global_events=ge)
+        b.build_random_graph(seed)
+        b.set_auto_stimulus(0, 256)
+        shards.append(b)
+    dev = torch.device("cuda", 0)
+    summ = torch.zeros(world, 4, dtype=torch.int64, device=dev)
+    fired = torch.zeros(world, 2560, dtype=torch.int32, device=dev)
+    tot = torch.zeros(2560, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for k in range(passes):
+        if k == 6:
+            for b in shards:
+                b.set_reward(0.125)
+        for r, b in enumerate(shards):
+            b.shard_gate(summ[r].data_ptr(), stream)
+        for r, b in enumerate(shards):
+            b.shard_apply(summ.data_ptr(), world, r, fired[r].data_ptr(), stream)
+        torch.sum(fired, dim=0, dtype=torch.int32, out=tot)
+        for b in shards:
+            b.shard_commit(summ.data_ptr(), world, tot.data_ptr(), stream)
+    torch.cuda.synchronize()
+    return shards
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_virtual_shards_equal_unsharded_gpu(gpu, world):
+    n_syn, passes = 2_000_000, 10
+    shards = _virtual_shard_run(world, n_syn, n_syn, passes)
+    g, o = _pair(30_000, n_syn, n_syn, seed=4)
+    for k in range(passes):
+        if k == 6:
+            g.set_reward(0.125)
+        g.encode_traversal(1)
+    syn = np.concatenate([b.download_synapses() for b in shards])
+    assert np.array_equal(syn.view(np.uint32), g.download_synapses().view(np.uint32))
+    for b in shards:
+        assert np.array_equal(b.last_fired(), g.last_fired())
+        assert b.scalars() == g.scalars()
+
+
+def test_virtual_shards_partial_sweep_vs_oracle_shards(gpu):
+    # events < shard size: each shard sweeps only its first `events` (config 4 shape)
+    from abnn_amd.shard import global_events, shard_ranges
+    from oracle import oracle as O
+
+    world, n_syn, events, passes = 4, 4_000_000, 600_000, 9
+    shards = _virtual_shard_run(world, n_syn, events, passes)
+    ge = global_events(n_syn, events, world)
+    obs = []
+    for lo, hi in shard_ranges(n_syn, world):
+        ob = O.OracleBrain(256, 256, 30_000, hi - lo, events, syn_offset=lo, global_events=ge)
+        ob.build_random_graph(4, nthreads=16)
+        ob.set_auto_stimulus(0, 256)
+        obs.append(ob)
+    for k in range(passes):
+        if k == 6:
+            for ob in obs:
+                ob.set_reward(0.125)
+        summ = np.zeros((world, 4), dtype=np.int64)
+        for r, ob in enumerate(obs):
+            ob.shard_gate(summ[r])
+        fired = np.zeros((world, 2560), dtype=np.int32)
+        for r, ob in enumerate(obs):
+            ob.shard_apply(summ.reshape(-1), world, r, fired[r])
+        tot = fired.sum(axis=0).astype(np.int32)
+        for ob in obs:
+            ob.shard_commit(summ.reshape(-1), world, tot)
+    for b, ob in zip(shards, obs):
+        _assert_same(b, ob, "shard")
+
+
+def test_save_load_roundtrips(gpu, tmp_path):
+    import abnn_amd
+
+    g, o = _pair(488, 10_000, 100_000)
+    g.encode_traversal(9)
+    p = tmp_path / "model.bnn"
+    g.save(p)
+    raw = p.read_bytes()
+    assert len(raw) == 8 + 16 * 10_000
+    assert np.frombuffer(raw[:8], dtype=np.uint32).tolist() == [10_000, 1000]  # brain.cpp:163-164
+    h = abnn_amd.Brain(256, 256, 488, 10_000, 100_000)
+    h.load(p)
+    assert np.array_equal(h.download_synapses().view(np.uint32), g.download_synapses().view(np.uint32))
+    bad = abnn_amd.Brain(256, 256, 489, 10_000, 100_000)
+    with pytest.raises(abnn_amd.AbnnError) as e:
+        bad.load(p)
+    assert e.value.status == 4  # ABNN_ERR_SIZE_MISMATCH (brain.cpp:174 threw a pointer)
+    f = tmp_path / "full.flat"
+    g.save_flat(f)
+    assert os.path.getsize(f) == 16 + 10_000 * 12 + 1000 * 16
+    h2 = abnn_amd.Brain(256, 256, 488, 10_000, 100_000)
+    h2.load_flat(f)
+    assert np.array_equal(h2.download_synapses().view(np.uint32), g.download_synapses().view(np.uint32))
+    assert np.array_equal(h2.last_fired(), g.last_fired())
+
+
+def test_timing_and_stats_api(gpu):
+    g, _ = _pair(99_488, 1_000_000, 1_000_000)
+    g.enable_timing(True)
+    g.encode_traversal(5)
+    ms, n = g.kernel_time()
+    assert n == 5 and ms > 0
+    st = g.stats()
+    assert st["passes"] == 5 and st["events"] == 5 * 1_000_000
+
+
+@pytest.mark.slow
+def test_config3_full_size_parity(gpu):
+    """BASELINE configs[2] on one GPU: 5,000,512 neurons, 1B synapses (16 GB), 150M events.
+
+    The sweep touches only the first E = 150,000,128 records, so the CPU oracle
+    holds just those; everything else is checked by the additive checksum."""
+    import abnn_amd
+    from oracle import oracle as O
+
+    n_hidden, n_syn, events = 5_000_000, 1_000_000_000, 150_000_000
+    g = abnn_amd.Brain(256, 256, n_hidden, n_syn, events)
+    g.build_random_graph(1)
+    E = g.visited_events()
+    assert E == 150_000_128
+    ck_cpu = 0
+    step = 50_000_000
+    for first in range(0, n_syn, step):
+        part = O.gen_synapses(first, min(step, n_syn - first), 256, 256, 5_000_512, 1, nthreads=16)
+        ck_cpu = (ck_cpu + O.checksum(part, first)) % (1 << 64)
+    del part
+    assert g.checksum() == ck_cpu
+    o = O.OracleBrain(256, 256, n_hidden, E, events)
+    o.build_random_graph(1, nthreads=16)
+    g.set_auto_stimulus(0, 256)
+    o.set_auto_stimulus(0, 256)
+    g.encode_traversal(8)
+    o.pass_threaded(8, nthreads=16)
+    head = g.download_synapses(0, E)
+    assert np.array_equal(head.view(np.uint32), o.syn.view(np.uint32))
+    assert np.array_equal(g.last_fired(), o.last_fired)
+    assert g.scalars()["clock"] == o.clock
+    st_g, st_o = g.stats(), o.stats()
+    assert st_g == st_o

@@ -1,0 +1,212 @@
+"""CPU tests of the oracle: known answers, restatement cross-check, threaded and
+sharded phases vs the serial C1 loop.  (Parity against the reference itself is
+UNPINNED -- DESIGN.md §3.)"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from py_reference import MetalEmu, rand01 as py_rand01
+
+PARAMS = dict(base_scale=0.8, refractory=2, window_pre=5, clock_inc=1, target_rate_hz=1000.0,
+              eta_home=1e-6, eta_reward=1e-3, alpha_rbar=0.001, a_ltp=0.04, a_ltd=0.02,
+              w_min=0.001, w_max=1.0, max_spikes=2560, renorm_thresh=4_000_000)
+
+
+def test_rand01_known_answers():
+    # brain.metal:15-19 by hand: s=1 -> 1^(1<<13)=8193 -> ^>>17 = 8193 -> ^(8193<<5)=270369
+    assert O.rand01(0) == 0.0
+    assert O.rand01(1) == np.float32(270369 / 16777216.0)
+    for s in [2, 3, 12345, 0xFFFFFFFF, 0x80000000, 0xDEADBEEF]:
+        assert O.rand01(s) == float(py_rand01(s))
+
+
+def test_default_params_match_reference_constants():
+    p = O.default_params()
+    assert np.float32(p.base_scale) == np.float32(0.8)
+    assert (p.refractory, p.window_pre, p.clock_inc, p.max_spikes) == (2, 5, 1, 2560)
+    assert np.float32(p.a_ltp) == np.float32(0.04) and np.float32(p.a_ltd) == np.float32(0.02)
+    assert np.float32(p.w_min) == np.float32(0.001) and p.w_max == 1.0
+    assert p.renorm_thresh == 4_000_000 and (p.tau_vis, p.tau_pre) == (50_000, 50_000)
+
+
+def test_generator_recipe():
+    n_in, n_out, n_nrn = 256, 256, 100_000
+    s = O.gen_synapses(0, 200_000, n_in, n_out, n_nrn, seed=1, nthreads=4)
+    dense = s[: n_in * n_out]
+    idx = np.arange(n_in * n_out)
+    assert np.array_equal(dense["src"], idx // n_out)
+    assert np.array_equal(dense["dst"], n_in + idx % n_out)
+    assert dense["w"].min() >= np.float32(0.4) and dense["w"].max() < np.float32(0.8)
+    hid = s[n_in * n_out:]
+    assert hid["src"].min() >= 512 and hid["src"].max() < n_nrn
+    assert hid["dst"].min() >= 512 and hid["dst"].max() < n_nrn
+    assert hid["w"].min() >= np.float32(0.1) and hid["w"].max() < np.float32(0.2)
+    assert np.all(s["pad"] == 0)
+    # counter-based: any slice is reproducible independently, any thread count
+    part = O.gen_synapses(123_457, 1000, n_in, n_out, n_nrn, seed=1, nthreads=1)
+    assert np.array_equal(part.view(np.uint32), s[123_457:124_457].view(np.uint32))
+    other = O.gen_synapses(0, 1000, n_in, n_out, n_nrn, seed=2)
+    assert not np.array_equal(other.view(np.uint32), s[:1000].view(np.uint32))
+
+
+def test_checksum_is_position_sensitive():
+    s = O.gen_synapses(0, 5000, 256, 256, 1000, seed=1)
+    c = O.checksum(s)
+    s2 = s.copy()
+    s2[[10, 11]] = s2[[11, 10]]
+    assert O.checksum(s2) != c
+    s3 = s.copy()
+    s3["w"][4999] = np.nextafter(s3["w"][4999], np.float32(1))
+    assert O.checksum(s3) != c
+    assert O.checksum(s[100:], first_global=100) + O.checksum(s[:100]) == c
+
+
+def _emu_from(ob: O.OracleBrain, events):
+    p = dict(PARAMS)
+    for k in p:
+        p[k] = getattr(ob.p, k)
+    p["track_visits"] = ob.p.track_visits
+    e = MetalEmu(ob.syn["src"], ob.syn["dst"], ob.syn["w"], ob.n_neuron(), events, p)
+    return e
+
+
+def _compare(ob, emu):
+    assert ob.clock == emu.clock
+    assert np.array_equal(ob.last_fired, np.array(emu.lastF, dtype=np.uint64))
+    w = np.array(emu.w, dtype=np.float32)
+    assert np.array_equal(ob.syn["w"].view(np.uint32), w.view(np.uint32))
+    assert np.float32(ob.s.rbar) == emu.rbar
+
+
+@pytest.mark.parametrize("case", ["c1", "hidden", "reward", "renorm", "visits"])
+def test_serial_oracle_matches_python_restatement(case):
+    n_hidden, n_syn, events, passes = 488, 10_000, 100_000, 10
+    over = {}
+    if case == "hidden":
+        n_hidden, n_syn, events, passes = 3000, 90_000, 20_000, 9
+    if case == "renorm":
+        over["renorm_thresh"] = 4
+        passes = 12
+    if case == "visits":
+        over["track_visits"] = 1
+    ob = O.OracleBrain(256, 256, n_hidden, n_syn, events, **over)
+    ob.build_random_graph(seed=7)
+    ob.set_auto_stimulus(0, 256)
+    emu = _emu_from(ob, events)
+    emu.stim = (0, 256)
+    for k in range(passes):
+        if case == "reward" and k == 4:
+            ob.set_reward(0.75)
+            emu.reward = np.float32(0.75)
+        ob.pass_serial()
+        emu.one_pass()
+        _compare(ob, emu)
+    if case == "visits":
+        assert np.array_equal(ob.last_visited, np.array(emu.lastV, dtype=np.uint64))
+    if case == "renorm":
+        assert ob.clock < 10  # renormalised at least once
+
+
+def _run(kind, nthreads=1, world=1, passes=8, **kw):
+    n_hidden = kw.pop("n_hidden", 20_000)
+    n_syn = kw.pop("n_syn", 300_000)
+    events = kw.pop("events", 250_000)
+    ob = O.OracleBrain(256, 256, n_hidden, n_syn, events, **kw)
+    ob.build_random_graph(seed=3)
+    ob.set_auto_stimulus(0, 256)
+    for k in range(passes):
+        if k == 5:
+            ob.set_reward(-0.5)
+        if kind == "serial":
+            ob.pass_serial()
+        else:
+            ob.pass_threaded(nthreads=nthreads)
+    return ob
+
+
+@pytest.mark.parametrize("nthreads", [1, 2, 3, 8, 17])
+def test_threaded_equals_serial(nthreads):
+    a = _run("serial")
+    b = _run("threaded", nthreads=nthreads)
+    assert a.clock == b.clock
+    assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32))
+    assert np.array_equal(a.last_fired, b.last_fired)
+    assert np.float32(a.s.rbar) == np.float32(b.s.rbar)
+    sa, sb = a.stats(), b.stats()
+    assert sa == sb
+
+
+def test_threaded_equals_serial_small_budget_and_edges():
+    for kw in [dict(max_spikes=1), dict(max_spikes=0), dict(max_spikes=1_000_000),
+               dict(events=1), dict(events=300_000 + 1000), dict(refractory=0, window_pre=0)]:
+        a = _run("serial", passes=7, **dict(kw))
+        b = _run("threaded", nthreads=5, passes=7, **dict(kw))
+        assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32)), kw
+        assert np.array_equal(a.last_fired, b.last_fired), kw
+        assert a.clock == b.clock, kw
+
+
+def test_empty_graph_never_ticks():
+    ob = O.OracleBrain(256, 256, 10, 0, 1000)
+    ob.pass_serial(3)
+    assert ob.clock == 0  # brain.metal:61 returns before any tick
+    ob2 = O.OracleBrain(256, 256, 10, 100, 0)
+    ob2.pass_serial(2)
+    assert ob2.clock == 0  # empty grid
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_shard_phases_equal_serial_full_sweep(world):
+    # events >= shard size: every shard sweeps its whole range -> global order = unsharded full sweep
+    n_syn = 300_000
+    shards = _sharded_full(world)
+    ref = _run("serial", passes=8, n_hidden=20_000, n_syn=n_syn, events=n_syn)
+    syn = np.concatenate([s.syn for s in shards])
+    assert np.array_equal(syn.view(np.uint32), ref.syn.view(np.uint32))
+    for s in shards:
+        assert np.array_equal(s.last_fired, ref.last_fired)
+        assert s.clock == ref.clock
+        assert np.float32(s.s.rbar) == np.float32(ref.s.rbar)
+
+
+def _sharded_full(world, passes=8):
+    from abnn_amd.shard import shard_ranges, global_events
+
+    n_hidden, n_syn, events = 20_000, 300_000, 300_000
+    ge = global_events(n_syn, events, world)
+    shards = []
+    for lo, hi in shard_ranges(n_syn, world):
+        ob = O.OracleBrain(256, 256, n_hidden, hi - lo, events, syn_offset=lo, global_events=ge)
+        ob.build_random_graph(seed=3)
+        ob.set_auto_stimulus(0, 256)
+        shards.append(ob)
+    for k in range(passes):
+        if k == 5:
+            for ob in shards:
+                ob.set_reward(-0.5)
+        summ = np.zeros((world, 4), dtype=np.int64)
+        for r, ob in enumerate(shards):
+            ob.shard_gate(summ[r])
+        fired = np.zeros((world, 2560), dtype=np.int32)
+        for r, ob in enumerate(shards):
+            ob.shard_apply(summ.reshape(-1), world, r, fired[r])
+        tot = fired.sum(axis=0).astype(np.int32)
+        for ob in shards:
+            ob.shard_commit(summ.reshape(-1), world, tot)
+    return shards
+
+
+def test_inject_and_read_outputs():
+    ob = O.OracleBrain(256, 256, 488, 10_000, 100_000)
+    ob.build_random_graph(seed=1)
+    v = np.zeros(256, dtype=np.float32)
+    v[::3] = 0.5
+    ob.s.clock = 7
+    ob.inject_inputs(v, 1000.0)
+    fired = np.nonzero(ob.last_fired[:256] == 7)[0]
+    assert np.array_equal(fired, np.arange(0, 256, 3))  # pTick ~ 1e15: every v>0 fires
+    ob.last_fired[256 + 5] = 7
+    ob.last_fired[256 + 6] = 6
+    ob.s.clock = 8
+    out = ob.read_outputs()
+    assert out[5] and not out[6] and out.sum() == 1

@@ -1,0 +1,97 @@
+"""world_size-2 (and 3) multi-process test of the sharded pass on CPU over gloo.
+
+Every rank runs the product's exchange logic (abnn_amd.shard.sharded_pass +
+TorchComm + shard_ranges/global_events) with a CPU stand-in engine built on the
+oracle's shard phases; the result must equal the unsharded serial C1 run
+bit-for-bit.  The GPU engine plugs into the same sharded_pass (tests/test_gpu_*).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+N_HIDDEN, N_SYN, PASSES = 20_000, 300_000, 9
+
+
+class CpuShardEngine:
+    def __init__(self, ob):
+        self.ob = ob
+
+    def gate(self, summary):
+        self.ob.shard_gate(summary.numpy())
+
+    def apply(self, summaries, world, rank, fired):
+        self.ob.shard_apply(summaries.numpy(), world, rank, fired.numpy())
+
+    def commit(self, summaries, world, fired):
+        self.ob.shard_commit(summaries.numpy(), world, fired.numpy())
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, events, track):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+    from abnn_amd.shard import TorchComm, global_events, shard_ranges, sharded_pass
+    from oracle import oracle as O
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = TorchComm()
+        lo, hi = shard_ranges(N_SYN, world)[rank]
+        ge = global_events(N_SYN, events, world)
+        ob = O.OracleBrain(256, 256, N_HIDDEN, hi - lo, events, syn_offset=lo, global_events=ge,
+                           track_visits=track)
+        ob.build_random_graph(seed=11, nthreads=2)
+        ob.set_auto_stimulus(0, 256)
+        eng = CpuShardEngine(ob)
+        summary = torch.zeros(4, dtype=torch.int64)
+        gathered = torch.zeros(4 * world, dtype=torch.int64)
+        fired = torch.zeros(2560, dtype=torch.int32)
+        for k in range(PASSES):
+            if k == 6:
+                ob.set_reward(0.25)
+            sharded_pass(eng, comm, summary, gathered, fired)
+        if track:  # lazy lastVisited merge (all-reduce MAX)
+            t = torch.from_numpy(ob.last_visited.view(np.int64).copy())
+            comm.all_reduce_max(t)
+            ob.last_visited[:] = t.numpy().view(np.uint64)
+
+        # unsharded reference, computed independently on every rank
+        ref = O.OracleBrain(256, 256, N_HIDDEN, N_SYN, events if world == 1 else N_SYN,
+                            track_visits=track)
+        ref.build_random_graph(seed=11, nthreads=2)
+        ref.set_auto_stimulus(0, 256)
+        for k in range(PASSES):
+            if k == 6:
+                ref.set_reward(0.25)
+            ref.pass_serial()
+        assert np.array_equal(ob.syn.view(np.uint32), ref.syn[lo:hi].view(np.uint32))
+        assert np.array_equal(ob.last_fired, ref.last_fired)
+        assert ob.clock == ref.clock
+        assert np.float32(ob.s.rbar) == np.float32(ref.s.rbar)
+        if track:
+            assert np.array_equal(ob.last_visited, ref.last_visited)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,track", [(2, 0), (3, 0), (2, 1)])
+def test_sharded_gloo_equals_unsharded(world, track):
+    # events >= every shard's size: each shard sweeps its whole range, so the
+    # rank-ordered union is the unsharded full sweep
+    mp.spawn(_worker, args=(world, _free_port(), N_SYN, track), nprocs=world, join=True)
