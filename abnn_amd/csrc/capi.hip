@@ -1,7 +1,9 @@
 // capi.hip -- implementation of the C-ABI (include/abnn/abnn.h) over the HIP
 // kernels of kernels.hip.  Replaces the Metal host class Brain
 // (abnn/src/core/brain/brain.{h,cpp}); each function cites what it replaces.
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -51,8 +53,7 @@ struct abnn_brain {
     abnn_params params{};
     KernelParams kp{};
     int device = 0;
-    hipStream_t stream = nullptr;
-    hipStream_t last_stream = nullptr;
+    hipStream_t stream = nullptr;  // default stream of state accessors (the null stream)
     uint64_t n_nrn = 0;
     DeviceState d{};
     void* scalar_block = nullptr;  // clock | reward | rbar
@@ -70,20 +71,15 @@ struct abnn_brain {
 
 namespace {
 
-hipStream_t pick(abnn_brain* b, void* s)
-{
-    hipStream_t st = s ? static_cast<hipStream_t>(s) : b->stream;
-    b->last_stream = st;
-    return st;
-}
+// Pass functions run on the caller's stream (NULL = the default stream).
+hipStream_t pick(abnn_brain*, void* s) { return static_cast<hipStream_t>(s); }
 
-// State accessors run on the handle's stream after everything enqueued on it
-// and on the stream of the last pass has completed.
+// State accessors are synchronous: they wait for all work on the handle's
+// device (whatever stream it was enqueued on), then copy on the default stream.
 abnn_status sync_all(abnn_brain* b)
 {
     HIP_TRY(hipSetDevice(b->device));
-    if (b->last_stream && b->last_stream != b->stream) HIP_TRY(hipStreamSynchronize(b->last_stream));
-    HIP_TRY(hipStreamSynchronize(b->stream));
+    HIP_TRY(hipDeviceSynchronize());
     return ABNN_OK;
 }
 
@@ -91,17 +87,16 @@ void free_all(abnn_brain* b)
 {
     if (!b) return;
     (void)hipSetDevice(b->device);
-    void* ptrs[] = {b->d.syn,        b->d.last_fired, b->d.last_visited, b->scalar_block,
-                    b->d.bitmap,     b->d.chunk_cnt,  b->d.chunk_pre,    b->d.active,
-                    b->d.g2buf,      b->d.apply_partial, b->d.fired,     b->d.summary,
-                    b->d.work,       b->idx_scratch,  b->u64_scratch};
+    void* ptrs[] = {b->d.syn,       b->d.last_fired, b->d.last_visited,  b->scalar_block,
+                    b->d.bitmap,    b->d.filter,     b->d.block_tot,     b->d.block_pre,
+                    b->d.tile_pre,  b->d.g2buf,      b->d.apply_partial, b->d.fired,
+                    b->d.summary,   b->d.work,       b->idx_scratch,     b->u64_scratch};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : b->events) {
         (void)hipEventDestroy(e.a);
         (void)hipEventDestroy(e.b);
     }
-    if (b->stream) (void)hipStreamDestroy(b->stream);
 }
 
 template <typename T>
@@ -270,7 +265,19 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     else abnn_default_params(&p);
     REQUIRE(p.max_spikes < (1u << 30), "max_spikes too large");
     const uint64_t E = visited_events(*dims);
-    REQUIRE(E / kChunk < 0xFFFFFFFFull, "too many events for one handle");
+    // Gate kernel shape: threads per workgroup x events per thread (ABNN_GATE="512x8").
+    uint32_t gate_block = 512, gate_k = 8;
+    if (const char* env = std::getenv("ABNN_GATE")) {
+        unsigned gb = 0, gk = 0;
+        if (std::sscanf(env, "%ux%u", &gb, &gk) == 2) {
+            gate_block = gb;
+            gate_k = gk;
+        }
+    }
+    REQUIRE(gate_shape_supported(gate_block, gate_k), "unsupported ABNN_GATE shape");
+    const uint64_t iter_events = (uint64_t)gate_block * gate_k;
+    const uint64_t iters = (E + iter_events - 1) / iter_events;
+    REQUIRE(iters < 0x7FFFFFFFull, "too many events for one handle");
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -292,8 +299,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
         delete b;
         return s;
     };
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
-        set_err("hipSetDevice/hipStreamCreate failed");
+    if (hipSetDevice(device) != hipSuccess) {
+        set_err("hipSetDevice failed");
         return fail(ABNN_ERR_HIP);
     }
     DeviceState& d = b->d;
@@ -301,7 +308,22 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.n_nrn = n_nrn;
     d.events = E;
     d.syn_offset = dims->syn_offset;
-    d.n_chunks = (uint32_t)((E + kChunk - 1) / kChunk);
+    d.gate_block = gate_block;
+    d.gate_k = gate_k;
+    d.iter_events = (uint32_t)iter_events;
+    d.iters = (uint32_t)iters;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+        cus = 256;
+    // one wave of persistent workgroups: as many as are resident (each keeps the
+    // 64 KiB filter in LDS, so at most two per CU)
+    int per_cu = gate_blocks_per_cu(gate_block, gate_k, p.track_visits != 0);
+    if (per_cu <= 0) per_cu = 1;
+    if (per_cu > 2) per_cu = 2;
+    uint64_t G = std::min<uint64_t>(iters, std::min<uint64_t>((uint64_t)cus * per_cu, kMaxGateBlocks));
+    d.gate_blocks = (uint32_t)G;
+    d.n_bitmap_words = (uint32_t)(2 * ((n_nrn + 63) / 64));
+    d.filter_exact = d.n_bitmap_words <= (uint32_t)kFilterWords ? 1u : 0u;
     abnn_status s;
     // build_buffers, brain.cpp:52-69: allocate and zero every buffer.
     if ((s = dalloc(&d.syn, dims->n_syn)) != ABNN_OK) return fail(s);
@@ -313,11 +335,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.clock = sb;
     d.reward = reinterpret_cast<float*>(sb + 1);
     d.rbar = d.reward + 1;
-    if ((s = dalloc(&d.bitmap, (n_nrn + 63) / 64 + 1)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.chunk_cnt, d.n_chunks)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.chunk_pre, d.n_chunks)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.active, d.n_chunks)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.g2buf, (uint64_t)d.n_chunks * kChunk)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.filter, kFilterWords)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.block_tot, G)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.block_pre, G)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.tile_pre, G + 1)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.g2buf, iters * iter_events)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.apply_partial, kApplyGrid)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.fired, p.max_spikes + 1u)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.summary, ABNN_SUMMARY_WORDS)) != ABNN_OK) return fail(s);
@@ -561,7 +584,7 @@ abnn_status abnn_synchronize(abnn_brain* b, void* stream)
 {
     REQUIRE(b, "null argument");
     HIP_TRY(hipSetDevice(b->device));
-    if (stream) HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
     return sync_all(b);
 }
 

@@ -10,19 +10,18 @@
 
 namespace abnn {
 
-// One 256-thread workgroup streams one chunk of kChunk consecutive events,
-// kEvPerThread per lane, lane-contiguous (event = chunk*kChunk + k*256 + tid)
-// so every wave-instruction reads 1 KiB of consecutive 16-B records.
-constexpr int kBlock = 256;
-constexpr int kEvPerThread = 8;
-constexpr int kChunk = kBlock * kEvPerThread;  // 2048 events
-constexpr int kWaves = kBlock / 64;
-constexpr int kApplyGrid = 1024;    // persistent grid of the apply kernel
-constexpr int kScanThreads = 1024;  // single-workgroup chunk scan
+// Pre-spike filter kept in LDS by every gate workgroup: the exact recent-spike
+// bitmap folded modulo kFilterWords 32-bit words (512 Ki bits = 64 KiB).  When
+// the bitmap itself fits (N_NRN <= 512 Ki) the filter IS the bitmap.
+constexpr int kFilterWords = 16384;
+constexpr int kApplyBlock = 256;   // one apply tile = 256 gated events
+constexpr int kApplyGrid = 1024;   // persistent grid of the apply kernel
+constexpr int kScanThreads = 1024; // one thread per gate workgroup in the scan
+constexpr int kMaxGateBlocks = kScanThreads;
 
 // Per-pass bookkeeping in device memory (one per handle).
 struct alignas(16) PassWork {
-    uint32_t n_active;     // chunks queued for the apply kernel
+    uint32_t total_tiles;  // apply tiles queued this pass
     uint32_t t0_g2;        // global event 0 passed both gates this pass
     uint64_t events;       // visited events of this shard this pass
     uint64_t g1;           // passed the pre-gate
@@ -38,12 +37,13 @@ struct DeviceState {
     uint64_t* clock;          // [1]
     float* reward;            // [1]
     float* rbar;              // [1]
-    uint64_t* bitmap;         // [ceil(n_nrn/64)] recent-spike bit per neuron
-    uint4* chunk_cnt;         // [n_chunks] {g2, candidates, g1, 0}
-    uint32_t* chunk_pre;      // [n_chunks] exclusive candidate prefix (capped)
-    uint32_t* active;         // [n_chunks] chunk ids for the apply kernel
-    uint4* g2buf;             // [n_chunks*kChunk] gated entries, per-chunk regions
-    uint2* apply_partial;     // [kApplyGrid] {updated, fired} per apply block
+    uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
+    uint32_t* filter;         // [kFilterWords] folded bitmap
+    uint4* block_tot;         // [gate_blocks] {gated, candidates, pre-gated, t0}
+    uint32_t* block_pre;      // [gate_blocks] exclusive candidate prefix (capped)
+    uint32_t* tile_pre;       // [gate_blocks + 1] exclusive prefix of apply tiles
+    uint4* g2buf;             // [iters * iter_events] gated entries, per-workgroup regions
+    uint2* apply_partial;     // [kApplyGrid] {updated, fired} per apply workgroup
     int32_t* fired;           // [max_spikes] internal spike list (world = 1)
     int64_t* summary;         // [ABNN_SUMMARY_WORDS] internal (world = 1)
     PassWork* work;
@@ -51,7 +51,13 @@ struct DeviceState {
     uint64_t n_nrn;
     uint64_t events;          // visited events per pass (local)
     uint64_t syn_offset;
-    uint32_t n_chunks;
+    uint32_t n_bitmap_words;  // 2 * ceil(n_nrn / 64)
+    uint32_t filter_exact;    // bitmap fits the filter: no global confirmation
+    uint32_t gate_blocks;     // persistent gate workgroups G
+    uint32_t iters;           // ceil(events / iter_events)
+    uint32_t iter_events;     // gate_block * gate_k events per workgroup iteration
+    uint32_t gate_block;      // threads per gate workgroup
+    uint32_t gate_k;          // events per thread per iteration
 };
 
 struct KernelParams {
@@ -62,6 +68,11 @@ struct KernelParams {
 };
 
 KernelParams to_kernel_params(const abnn_params& p);
+
+// Gate kernel shapes compiled in (threads per workgroup x events per thread).
+bool gate_shape_supported(uint32_t block, uint32_t k);
+// Resident gate workgroups per CU for a shape (occupancy API; 0 on failure).
+int gate_blocks_per_cu(uint32_t block, uint32_t k, bool track);
 
 // Launchers (all asynchronous on `s`).
 hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,

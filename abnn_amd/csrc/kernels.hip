@@ -1,24 +1,29 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of one C1 traversal pass.
 //
 // Reference hot path: monte_carlo_traversal (abnn/src/core/kernels/brain.metal:41-130)
-// and renormalise_clock_and_times (brain.metal:135-145).  The pass is split into
-// launches that each do one HBM-friendly thing:
+// and renormalise_clock_and_times (brain.metal:135-145).  One pass = six launches,
+// each doing one HBM-friendly thing:
 //
-//   k_bitmap   : lastFired (u64, 8 B/neuron) -> 1 recent-spike bit per neuron
-//                (now - lastFired <= WINDOW_PRE), plus the fused stimulus stamp.
-//                The pre-spike gate of every event (brain.metal:73-77) then reads
-//                one bit of an L2-resident bitmap instead of a random 8-B word.
-//   k_gate     : the streaming kernel.  One 16-B SynapsePacked per event, non-
-//                temporal dwordx4 loads, 1 KiB per wave-instruction; pre-gate
-//                via the bitmap; refractory gate (brain.metal:79-83) via a real
-//                8-B gather for the few events that pass; spike-candidate test
-//                (brain.metal:91-92); stable in-order compaction of the gated
-//                events into the chunk's region (wave ballots + 2 KiB of LDS).
-//   k_scan     : one workgroup: exclusive prefix of candidate counts over chunks
-//                = the ordered global spike budget of schedule C1
-//                (brain.metal:85-98 without its races).
-//   k_apply    : weight update (brain.metal:101-122) of the gated events that
-//                still had budget, spike list in budget order.
+//   k_bitmap   : lastFired (u64, 8 B/neuron, read once) -> exact recent-spike
+//                bitmap, bit i = (now - lastFired[i]) <= WINDOW_PRE; the
+//                per-pass stimulus stamp is fused here.
+//   k_fold     : bitmap folded modulo 512 Ki bits -> the 64 KiB pre-spike filter.
+//   k_gate     : THE streaming kernel.  Persistent workgroups, each sweeping one
+//                contiguous range of events with non-temporal dwordx4 loads of
+//                the 16-B SynapsePacked records (1 KiB per wave-instruction,
+//                next iteration's loads in flight while the current one is
+//                gated).  Pre-spike gate (brain.metal:73-77) = one LDS filter
+//                bit (+ an L2 bitmap word on a filter hit unless the filter is
+//                exact); refractory gate (brain.metal:79-83) = a real 8-B gather
+//                of lastFired[dst] for the few events that pass; spike-candidate
+//                test (brain.metal:91-92); gated events are compacted in event
+//                order into the workgroup's region with their workgroup-local
+//                candidate prefix.
+//   k_scan     : one workgroup: exclusive candidate prefix over the gate
+//                workgroups = the ordered global spike budget of schedule C1
+//                (brain.metal:85-98 without its races) + the apply tiling.
+//   k_apply    : weight update (brain.metal:101-122) of every gated event that
+//                still had budget; spikes land at their budget position.
 //   k_finalize : deferred lastFired stamps (brain.metal:125-126), rBar EWMA
 //                (brain.metal:110-113), one clock tick (brain.metal:129).
 //   k_renorm   : brain.metal:135-145 with the base read once (no race).
@@ -155,12 +160,17 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total, uint64_t* 
     return before + inc - v;
 }
 
+__device__ __forceinline__ uint64_t range_begin(uint32_t b, uint32_t iters, uint32_t G)
+{
+    return (uint64_t)b * iters / G;
+}
+
 // ---------------------------------------------------------------------------
 // k_bitmap: bit i = (now - lastFired[i]) <= window_pre; stimulus stamp fused.
-__global__ __launch_bounds__(kBlock) void k_bitmap(DeviceState d, KernelParams kp,
-                                                   uint64_t stim_first, uint64_t stim_count)
+__global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
+                                                uint64_t stim_first, uint64_t stim_count)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint64_t now = *d.clock;
     bool bit = false;
     if (i < d.n_nrn) {
@@ -174,186 +184,205 @@ __global__ __launch_bounds__(kBlock) void k_bitmap(DeviceState d, KernelParams k
         bit = (now - L) <= (uint64_t)kp.window_pre;
     }
     const uint64_t m = __ballot(bit);
-    if ((threadIdx.x & 63) == 0 && i < d.n_nrn) d.bitmap[i >> 6] = m;
+    if ((threadIdx.x & 63) == 0 && i < d.n_nrn)
+        reinterpret_cast<uint64_t*>(d.bitmap)[i >> 6] = m;
+}
+
+// k_fold: filter[j] = OR over m of bitmap[j + m * kFilterWords].
+__global__ __launch_bounds__(256) void k_fold(DeviceState d)
+{
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= (uint32_t)kFilterWords) return;
+    uint32_t v = 0;
+    for (uint32_t w = j; w < d.n_bitmap_words; w += kFilterWords) v |= d.bitmap[w];
+    d.filter[j] = v;
 }
 
 // ---------------------------------------------------------------------------
 // k_gate: the streaming kernel (see file header).
-template <bool kTrack>
-__global__ __launch_bounds__(kBlock) void k_gate(DeviceState d, KernelParams kp)
+template <int BLOCK, int K, bool kTrack>
+__global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
-    __shared__ uint32_t s_g2[kEvPerThread][kWaves];
-    __shared__ uint32_t s_c[kEvPerThread][kWaves];
-    __shared__ uint32_t s_g1[kWaves];
+    constexpr int NW = BLOCK / 64;
+    constexpr uint32_t IE = BLOCK * K;
+    __shared__ uint32_t s_filter[kFilterWords];
+    __shared__ uint32_t s_g2[2][K][NW];
+    __shared__ uint32_t s_c[2][K][NW];
+    __shared__ uint32_t s_g1[NW];
 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t c = blockIdx.x;
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint64_t it_begin = range_begin(b, d.iters, G), it_end = range_begin(b + 1, d.iters, G);
+    const uint64_t region = it_begin * IE;
     const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
-    const uint64_t base = (uint64_t)c * kChunk;
-    const uint32_t* bm = reinterpret_cast<const uint32_t*>(d.bitmap);
+    const uint32_t budget = kp.max_spikes;
+    const bool exact = d.filter_exact != 0;
 
-    uint4 rec[kEvPerThread];
-    uint32_t valid = 0;
-    if (base + kChunk <= d.events) {
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(d.filter);
+        uint4* dst = reinterpret_cast<uint4*>(s_filter);
+        for (int i = tid; i < kFilterWords / 4; i += BLOCK) dst[i] = src[i];
+    }
+
+    uint4 nxt[K];
+    auto issue = [&](uint64_t it) {
+        const uint64_t base = it * IE;
+        if (base + IE <= d.events) {
 #pragma unroll
-        for (int k = 0; k < kEvPerThread; ++k)
-            rec[k] = load_stream16(d.syn + base + k * kBlock + tid);  // brain.metal:70
-        valid = (1u << kEvPerThread) - 1u;
-    } else {
+            for (int k = 0; k < K; ++k) nxt[k] = load_stream16(d.syn + base + k * BLOCK + tid);
+        } else {
 #pragma unroll
-        for (int k = 0; k < kEvPerThread; ++k) {
-            const uint64_t t = base + k * kBlock + tid;
-            if (t < d.events) {
-                rec[k] = load_stream16(d.syn + t);
-                valid |= 1u << k;
-            } else {
-                rec[k] = make_uint4(0u, 0u, 0u, 0u);
+            for (int k = 0; k < K; ++k) {
+                const uint64_t t = base + k * BLOCK + tid;
+                nxt[k] = t < d.events ? load_stream16(d.syn + t) : make_uint4(0u, 0u, 0u, 0u);
             }
         }
-    }
-
-    // Pre-spike gate, brain.metal:73-77: one bit per source neuron.
-    uint32_t g1m = 0;
-#pragma unroll
-    for (int k = 0; k < kEvPerThread; ++k) {
-        // records are validated on upload (src, dst < N_NRN); the guard only
-        // keeps a corrupted record from faulting the device
-        const uint32_t src = rec[k].x < d.n_nrn ? rec[k].x : 0u;
-        const uint32_t word = bm[src >> 5];
-        if (((valid >> k) & 1u) && rec[k].x < d.n_nrn && rec[k].y < d.n_nrn &&
-            ((word >> (src & 31u)) & 1u))
-            g1m |= 1u << k;
-    }
-
-    // Refractory gate, brain.metal:79-83: real 8-B gather of lastFired[dst].
-    uint64_t ld[kEvPerThread];
-#pragma unroll
-    for (int k = 0; k < kEvPerThread; ++k)
-        ld[k] = ((g1m >> k) & 1u) ? d.last_fired[rec[k].y] : 0ull;
-
-    uint32_t g2m = 0, cm = 0;
-#pragma unroll
-    for (int k = 0; k < kEvPerThread; ++k) {
-        if (((g1m >> k) & 1u) && (now - ld[k]) > (uint64_t)kp.refractory) {
-            g2m |= 1u << k;
-            const uint64_t tg = d.syn_offset + base + k * kBlock + tid;
-            if (spike_candidate(kp, __uint_as_float(rec[k].z), tg, now)) cm |= 1u << k;
-        }
-    }
-
-    if (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
-#pragma unroll
-        for (int k = 0; k < kEvPerThread; ++k)
-            if (((valid >> k) & 1u) && rec[k].y < d.n_nrn) d.last_visited[rec[k].y] = now;
-    }
-
-    // In-order compaction: event order inside the chunk is (k, wave, lane).
-    uint32_t mb_g2[kEvPerThread], mb_c[kEvPerThread];
-    uint32_t g1cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kEvPerThread; ++k) {
-        const uint64_t bg = __ballot((g2m >> k) & 1u);
-        const uint64_t bc = __ballot((cm >> k) & 1u);
-        const uint64_t b1 = __ballot((g1m >> k) & 1u);
-        mb_g2[k] = mbcnt64(bg);
-        mb_c[k] = mbcnt64(bc);
-        g1cnt += (uint32_t)__popcll(b1);
-        if (lane == 0) {
-            s_g2[k][wid] = (uint32_t)__popcll(bg);
-            s_c[k][wid] = (uint32_t)__popcll(bc);
-        }
-    }
-    if (lane == 0) s_g1[wid] = g1cnt;
+    };
+    if (it_begin < it_end) issue(it_begin);
     __syncthreads();
 
-    uint32_t run_g2 = 0, run_c = 0;
+    uint32_t g2_run = 0, c_run = 0, g1_wave = 0, t0 = 0;
+    uint32_t par = 0;
+    for (uint64_t it = it_begin; it < it_end; ++it, par ^= 1u) {
+        uint4 rec[K];
 #pragma unroll
-    for (int k = 0; k < kEvPerThread; ++k) {
-        uint32_t bw_g2 = 0, bw_c = 0, tot_g2 = 0, tot_c = 0;
+        for (int k = 0; k < K; ++k) rec[k] = nxt[k];
+        if (it + 1 < it_end) issue(it + 1);  // next iteration's records in flight
+        const uint64_t base = it * IE;
+
+        // Pre-spike gate, brain.metal:73-77.
+        uint32_t g1m = 0;
 #pragma unroll
-        for (uint32_t w = 0; w < (uint32_t)kWaves; ++w) {
-            const uint32_t a = s_g2[k][w], b = s_c[k][w];
-            bw_g2 += w < wid ? a : 0u;
-            bw_c += w < wid ? b : 0u;
-            tot_g2 += a;
-            tot_c += b;
+        for (int k = 0; k < K; ++k) {
+            const uint32_t s = rec[k].x, ds = rec[k].y;
+            const bool ok = base + k * BLOCK + tid < d.events && s < d.n_nrn && ds < d.n_nrn;
+            const uint32_t fw = s_filter[(s >> 5) & (kFilterWords - 1)];
+            if (ok && ((fw >> (s & 31u)) & 1u)) g1m |= 1u << k;
         }
-        if ((g2m >> k) & 1u) {
-            const uint32_t slot = run_g2 + bw_g2 + mb_g2[k];
-            const uint32_t pre = run_c + bw_c + mb_c[k];
-            uint4 e;
-            e.x = (uint32_t)(k * kBlock + tid) | (pre << 11) | (((cm >> k) & 1u) << 22);
-            e.y = rec[k].y;
-            e.z = rec[k].z;
-            e.w = __float_as_uint((float)(now - ld[k]));  // isi, brain.metal:116
-            d.g2buf[base + slot] = e;
+        if (!exact) {  // confirm filter hits on the exact (L2-resident) bitmap
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if ((g1m >> k) & 1u) {
+                    const uint32_t s = rec[k].x;
+                    if (!((d.bitmap[s >> 5] >> (s & 31u)) & 1u)) g1m &= ~(1u << k);
+                }
         }
-        run_g2 += tot_g2;
-        run_c += tot_c;
+
+        // Refractory gate, brain.metal:79-83: real 8-B gather of lastFired[dst].
+        uint64_t ld[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) ld[k] = ((g1m >> k) & 1u) ? d.last_fired[rec[k].y] : 0ull;
+
+        uint32_t g2m = 0, cm = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (((g1m >> k) & 1u) && (now - ld[k]) > (uint64_t)kp.refractory) {
+                g2m |= 1u << k;
+                const uint64_t tg = d.syn_offset + base + k * BLOCK + tid;
+                if (spike_candidate(kp, __uint_as_float(rec[k].z), tg, now)) cm |= 1u << k;
+            }
+        }
+        if (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (base + k * BLOCK + tid < d.events && rec[k].y < d.n_nrn)
+                    d.last_visited[rec[k].y] = now;
+        }
+        if (it == 0 && tid == 0 && d.syn_offset == 0 && (g2m & 1u)) t0 = 1;
+
+        // In-order compaction: event order inside an iteration is (k, wave, lane).
+        uint32_t mb_g2[K], mb_c[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t bg = __ballot((g2m >> k) & 1u);
+            const uint64_t bc = __ballot((cm >> k) & 1u);
+            g1_wave += (uint32_t)__popcll(__ballot((g1m >> k) & 1u));
+            mb_g2[k] = mbcnt64(bg);
+            mb_c[k] = mbcnt64(bc);
+            if (lane == 0) {
+                s_g2[par][k][wid] = (uint32_t)__popcll(bg);
+                s_c[par][k][wid] = (uint32_t)__popcll(bc);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            uint32_t bw_g2 = 0, bw_c = 0, tot_g2 = 0, tot_c = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
+                const uint32_t a = s_g2[par][k][w], c = s_c[par][k][w];
+                bw_g2 += w < wid ? a : 0u;
+                bw_c += w < wid ? c : 0u;
+                tot_g2 += a;
+                tot_c += c;
+            }
+            if ((g2m >> k) & 1u) {
+                const uint32_t slot = g2_run + bw_g2 + mb_g2[k];
+                const uint32_t pre = c_run + bw_c + mb_c[k];
+                uint4 e;
+                e.x = (uint32_t)(base - region) + k * BLOCK + tid;  // event, relative to the region
+                e.y = (pre < budget ? pre : budget) | (((cm >> k) & 1u) << 31);
+                e.z = rec[k].z;                                        // w
+                e.w = __float_as_uint((float)(now - ld[k]));          // isi, brain.metal:116
+                d.g2buf[region + slot] = e;
+            }
+            g2_run += tot_g2;
+            c_run += tot_c;
+        }
     }
+    if (lane == 0) s_g1[wid] = g1_wave;
+    if (tid == 0 && t0) d.work->t0_g2 = 1;
+    __syncthreads();
     if (tid == 0) {
-        d.chunk_cnt[c] = make_uint4(run_g2, run_c, s_g1[0] + s_g1[1] + s_g1[2] + s_g1[3], 0u);
-        if (c == 0) d.work->t0_g2 = (d.syn_offset == 0 && (g2m & 1u)) ? 1u : 0u;
+        uint32_t g1 = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) g1 += s_g1[w];
+        d.block_tot[b] = make_uint4(g2_run, c_run, g1, 0u);
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_scan: ordered spike budget over chunks (one workgroup).
+// k_scan: ordered spike budget over the gate workgroups (one workgroup).
 __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelParams kp,
                                                        int64_t* summary_out)
 {
     __shared__ uint64_t s_wave[kScanThreads / 64];
-    __shared__ uint64_t s_red[3][kScanThreads / 64];
-    const uint32_t n = d.n_chunks, tid = threadIdx.x;
-    const uint32_t per = (n + kScanThreads - 1) / kScanThreads;
-    const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
+    __shared__ uint64_t s_red[2][kScanThreads / 64];
+    const uint32_t tid = threadIdx.x, G = d.gate_blocks;
     const uint64_t budget = kp.max_spikes;
-
-    uint64_t cand = 0, g2 = 0, g1 = 0;
-    for (uint32_t c = lo; c < hi; ++c) {
-        const uint4 v = d.chunk_cnt[c];
-        g2 += v.x;
-        cand += v.y;
-        g1 += v.z;
-    }
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (tid < G) v = d.block_tot[tid];
     uint64_t cand_total;
-    const uint64_t excl = block_exclusive_scan(cand, &cand_total, s_wave);
-
-    // totals of g1 / g2 (for statistics)
-    const uint64_t wg2 = wave_sum(g2), wg1 = wave_sum(g1);
+    const uint64_t excl = block_exclusive_scan(v.y, &cand_total, s_wave);
+    const uint64_t tiles =
+        (tid < G && v.x > 0 && excl < budget) ? (v.x + kApplyBlock - 1) / kApplyBlock : 0;
+    uint64_t tiles_total;
+    const uint64_t tpre = block_exclusive_scan(tiles, &tiles_total, s_wave);
+    if (tid < G) {
+        d.block_pre[tid] = (uint32_t)(excl < budget ? excl : budget);
+        d.tile_pre[tid] = (uint32_t)tpre;
+    }
+    const uint64_t wg2 = wave_sum((uint64_t)v.x), wg1 = wave_sum((uint64_t)v.z);
     if ((tid & 63) == 0) {
         s_red[0][tid >> 6] = wg2;
         s_red[1][tid >> 6] = wg1;
     }
-
-    uint64_t pre = excl;
-    uint64_t nact = 0;
-    for (uint32_t c = lo; c < hi; ++c) {
-        const uint4 v = d.chunk_cnt[c];
-        d.chunk_pre[c] = (uint32_t)(pre < budget ? pre : budget);
-        nact += (v.x > 0 && pre < budget) ? 1u : 0u;
-        pre += v.y;
-    }
-    uint64_t act_total;
-    uint64_t act_pos = block_exclusive_scan(nact, &act_total, s_wave);
-    pre = excl;
-    for (uint32_t c = lo; c < hi; ++c) {
-        const uint4 v = d.chunk_cnt[c];
-        if (v.x > 0 && pre < budget) d.active[act_pos++] = c;
-        pre += v.y;
-    }
+    __syncthreads();
     if (tid == 0) {
         uint64_t tg2 = 0, tg1 = 0;
         for (int w = 0; w < kScanThreads / 64; ++w) {
             tg2 += s_red[0][w];
             tg1 += s_red[1][w];
         }
+        d.tile_pre[G] = (uint32_t)tiles_total;
         const uint64_t capped = cand_total < budget ? cand_total : budget;
+        const uint32_t t0 = d.work->t0_g2;
         summary_out[0] = (int64_t)capped;
-        summary_out[1] = (int64_t)d.work->t0_g2;
+        summary_out[1] = (int64_t)t0;
         summary_out[2] = (int64_t)d.events;
         summary_out[3] = (int64_t)tg2;
-        d.work->n_active = (uint32_t)act_total;
+        d.work->total_tiles = (uint32_t)tiles_total;
+        d.work->t0_g2 = 0;  // re-armed for the next pass
         d.work->events = d.events;
         d.work->g1 = tg1;
         d.work->g2 = tg2;
@@ -362,11 +391,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelPara
 
 // ---------------------------------------------------------------------------
 // k_apply: weight update of the gated events that still had budget.
-__global__ __launch_bounds__(kBlock) void k_apply(DeviceState d, KernelParams kp,
-                                                  const int64_t* summaries, uint32_t world,
-                                                  uint32_t rank, int32_t* fired)
+__global__ __launch_bounds__(kApplyBlock) void k_apply(DeviceState d, KernelParams kp,
+                                                       const int64_t* summaries, uint32_t world,
+                                                       uint32_t rank, int32_t* fired)
 {
-    __shared__ uint32_t s_u[kWaves], s_f[kWaves];
+    __shared__ uint32_t s_u[kApplyBlock / 64], s_f[kApplyBlock / 64];
     const uint32_t tid = threadIdx.x;
     const uint64_t budget = kp.max_spikes;
     const float R = *d.reward, rb = *d.rbar;  // pass-start values (C1), brain.metal:105-106
@@ -375,27 +404,32 @@ __global__ __launch_bounds__(kBlock) void k_apply(DeviceState d, KernelParams kp
         off += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 0];
     off = off < budget ? off : budget;
 
-    const uint32_t n_act = d.work->n_active;
+    const uint32_t G = d.gate_blocks, T = d.work->total_tiles, IE = d.iter_events;
     uint32_t upd = 0, nf = 0;
-    for (uint32_t i = blockIdx.x; i < n_act; i += gridDim.x) {
-        const uint32_t c = d.active[i];
-        const uint64_t P = off + d.chunk_pre[c];
-        if (P >= budget) continue;
-        const uint32_t n = d.chunk_cnt[c].x;
-        const uint64_t base = (uint64_t)c * kChunk;
-        for (uint32_t j = tid; j < n; j += kBlock) {
-            const uint4 e = d.g2buf[base + j];
-            const uint64_t pre = P + ((e.x >> 11) & 0x7FFu);
-            if (pre >= budget) continue;  // budget == 0 at this event: brain.metal:85-88
-            const bool f = (e.x >> 22) & 1u;
-            const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.w));
-            float* wp = reinterpret_cast<float*>(d.syn + base + (e.x & 0x7FFu)) + 2;
-            *wp = w;                                  // brain.metal:122 (src/dst/pad unchanged)
-            ++upd;
-            if (f) {
-                fired[pre] = (int32_t)e.y;            // spike list in budget order
-                ++nf;
-            }
+    for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
+        uint32_t lo = 0, hi = G;  // largest b with tile_pre[b] <= tile
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (d.tile_pre[mid] <= tile) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t b = lo;
+        const uint64_t P = off + d.block_pre[b];
+        const uint32_t j = (tile - d.tile_pre[b]) * kApplyBlock + tid;
+        if (P >= budget || j >= d.block_tot[b].x) continue;
+        const uint64_t region = range_begin(b, d.iters, G) * IE;
+        const uint4 e = d.g2buf[region + j];
+        const uint64_t pre = P + (e.y & 0x7FFFFFFFu);
+        if (pre >= budget) continue;  // budget == 0 at this event: brain.metal:85-88
+        const bool f = (e.y >> 31) != 0;
+        const uint64_t t = region + e.x;
+        const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.w));
+        uint32_t* rec = reinterpret_cast<uint32_t*>(d.syn + t);
+        rec[2] = __float_as_uint(w);       // brain.metal:122 (src/dst/pad unchanged)
+        ++upd;
+        if (f) {
+            fired[pre] = (int32_t)rec[1];  // dst, spike list in budget order
+            ++nf;
         }
     }
     const uint32_t wu = wave_sum(upd), wf = wave_sum(nf);
@@ -411,11 +445,11 @@ __global__ __launch_bounds__(kBlock) void k_apply(DeviceState d, KernelParams kp
 
 // ---------------------------------------------------------------------------
 // k_finalize: stamps, rBar, clock tick, statistics (one workgroup).
-__global__ __launch_bounds__(kBlock) void k_finalize(DeviceState d, KernelParams kp,
-                                                     const int64_t* summaries, uint32_t world,
-                                                     const int32_t* fired)
+__global__ __launch_bounds__(256) void k_finalize(DeviceState d, KernelParams kp,
+                                                  const int64_t* summaries, uint32_t world,
+                                                  const int32_t* fired)
 {
-    __shared__ uint32_t s_u[kWaves], s_f[kWaves];
+    __shared__ uint32_t s_u[4], s_f[4];
     const uint32_t tid = threadIdx.x;
     const uint64_t now = *d.clock;
     const uint64_t budget = kp.max_spikes;
@@ -425,11 +459,12 @@ __global__ __launch_bounds__(kBlock) void k_finalize(DeviceState d, KernelParams
         events += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 2];
     }
     const uint64_t n_fired = total < budget ? total : budget;
-    for (uint64_t i = tid; i < n_fired; i += kBlock)
-        d.last_fired[(uint32_t)fired[i]] = now;      // brain.metal:125-126, deferred
-
+    for (uint64_t i = tid; i < n_fired; i += 256) {
+        const uint32_t n = (uint32_t)fired[i];
+        if (n < d.n_nrn) d.last_fired[n] = now;  // brain.metal:125-126, deferred
+    }
     uint32_t upd = 0, nf = 0;
-    for (uint32_t i = tid; i < (uint32_t)kApplyGrid; i += kBlock) {
+    for (uint32_t i = tid; i < (uint32_t)kApplyGrid; i += 256) {
         const uint2 v = d.apply_partial[i];
         upd += v.x;
         nf += v.y;
@@ -458,23 +493,23 @@ __global__ __launch_bounds__(kBlock) void k_finalize(DeviceState d, KernelParams
 
 // ---------------------------------------------------------------------------
 // k_renorm: brain.metal:135-145; base (= the ticked clock) passed by the host.
-__global__ __launch_bounds__(kBlock) void k_renorm(DeviceState d, uint64_t base)
+__global__ __launch_bounds__(256) void k_renorm(DeviceState d, uint64_t base)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < d.n_nrn) d.last_fired[i] -= base;
     if (i == 0) *d.clock = 0;
 }
 
 // ---------------------------------------------------------------------------
 // k_generate: synthetic graph (recipe of brain-engine.cpp:31-53, portable RNG).
-__global__ __launch_bounds__(kBlock) void k_generate(DeviceState d, uint32_t n_in, uint32_t n_out,
-                                                     uint64_t seed)
+__global__ __launch_bounds__(256) void k_generate(DeviceState d, uint32_t n_in, uint32_t n_out,
+                                                  uint64_t seed)
 {
     const uint64_t n_io = (uint64_t)n_in * n_out;
     const uint64_t lo = (uint64_t)n_in + n_out;
     const uint64_t range = d.n_nrn - lo;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < d.n_syn; k += stride) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < d.n_syn; k += stride) {
         const uint64_t i = d.syn_offset + k;
         const uint64_t x2 = splitmix64_at(seed, 3u * i + 2u);
         uint4 r;
@@ -494,12 +529,12 @@ __global__ __launch_bounds__(kBlock) void k_generate(DeviceState d, uint32_t n_i
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_checksum(DeviceState d, uint64_t* out)
+__global__ __launch_bounds__(256) void k_checksum(DeviceState d, uint64_t* out)
 {
-    __shared__ uint64_t s[kWaves];
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    __shared__ uint64_t s[4];
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
     uint64_t acc = 0;
-    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < d.n_syn; k += stride) {
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < d.n_syn; k += stride) {
         const uint4 r = d.syn[k];
         const uint64_t i = d.syn_offset + k;
         const uint64_t a = ((uint64_t)r.x << 32) | r.y;
@@ -509,39 +544,83 @@ __global__ __launch_bounds__(kBlock) void k_checksum(DeviceState d, uint64_t* ou
     acc = wave_sum(acc);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd((unsigned long long*)out, (unsigned long long)(s[0] + s[1] + s[2] + s[3]));
+    if (threadIdx.x == 0)
+        atomicAdd((unsigned long long*)out, (unsigned long long)(s[0] + s[1] + s[2] + s[3]));
 }
 
-__global__ __launch_bounds__(kBlock) void k_stamp_list(DeviceState d, const uint32_t* idx,
-                                                       uint64_t n, const uint64_t* value_dev,
-                                                       uint64_t value)
+__global__ __launch_bounds__(256) void k_stamp_list(DeviceState d, const uint32_t* idx,
+                                                    uint64_t n, const uint64_t* value_dev,
+                                                    uint64_t value)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint64_t v = value_dev ? *value_dev : value;
     if (i < n && idx[i] < d.n_nrn) d.last_fired[idx[i]] = v;
 }
 
-inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
+inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
+
+template <int BLOCK, int K>
+hipError_t launch_gate_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
+{
+    if (kp.track_visits)
+        hipLaunchKernelGGL((k_gate<BLOCK, K, true>), dim3(d.gate_blocks), dim3(BLOCK), 0, s, d, kp);
+    else
+        hipLaunchKernelGGL((k_gate<BLOCK, K, false>), dim3(d.gate_blocks), dim3(BLOCK), 0, s, d, kp);
+    return hipGetLastError();
+}
 
 }  // namespace
+
+template <int BLOCK, int K>
+int occupancy_shape(bool track)
+{
+    int n = 0;
+    hipError_t e = track ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, true>, BLOCK, 0)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, false>, BLOCK, 0);
+    return e == hipSuccess ? n : 0;
+}
+
+int gate_blocks_per_cu(uint32_t block, uint32_t k, bool track)
+{
+    switch (block * 100 + k) {
+        case 25608: return occupancy_shape<256, 8>(track);
+        case 25616: return occupancy_shape<256, 16>(track);
+        case 51204: return occupancy_shape<512, 4>(track);
+        case 51208: return occupancy_shape<512, 8>(track);
+        case 102404: return occupancy_shape<1024, 4>(track);
+    }
+    return 0;
+}
+
+bool gate_shape_supported(uint32_t block, uint32_t k)
+{
+    return (block == 256 && (k == 8 || k == 16)) || (block == 512 && (k == 4 || k == 8)) ||
+           (block == 1024 && k == 4);
+}
 
 hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,
                          uint64_t stim_count, hipStream_t s)
 {
     if (d.n_nrn == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_bitmap, dim3(blocks_for(d.n_nrn)), dim3(kBlock), 0, s, d, kp, stim_first,
+    hipLaunchKernelGGL(k_bitmap, dim3(blocks_for(d.n_nrn)), dim3(256), 0, s, d, kp, stim_first,
                        stim_count);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_fold, dim3(kFilterWords / 256), dim3(256), 0, s, d);
     return hipGetLastError();
 }
 
 hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s)
 {
-    if (d.n_chunks == 0) return hipSuccess;
-    if (kp.track_visits)
-        hipLaunchKernelGGL(k_gate<true>, dim3(d.n_chunks), dim3(kBlock), 0, s, d, kp);
-    else
-        hipLaunchKernelGGL(k_gate<false>, dim3(d.n_chunks), dim3(kBlock), 0, s, d, kp);
-    return hipGetLastError();
+    if (d.gate_blocks == 0) return hipSuccess;
+    switch (d.gate_block * 100 + d.gate_k) {
+        case 25608: return launch_gate_shape<256, 8>(d, kp, s);
+        case 25616: return launch_gate_shape<256, 16>(d, kp, s);
+        case 51204: return launch_gate_shape<512, 4>(d, kp, s);
+        case 51208: return launch_gate_shape<512, 8>(d, kp, s);
+        case 102404: return launch_gate_shape<1024, 4>(d, kp, s);
+    }
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int64_t* summary_out,
@@ -554,7 +633,7 @@ hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int64_t* su
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
                         uint32_t world, uint32_t rank, int32_t* fired, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_apply, dim3(kApplyGrid), dim3(kBlock), 0, s, d, kp, summaries, world,
+    hipLaunchKernelGGL(k_apply, dim3(kApplyGrid), dim3(kApplyBlock), 0, s, d, kp, summaries, world,
                        rank, fired);
     return hipGetLastError();
 }
@@ -562,14 +641,14 @@ hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int6
 hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
                            uint32_t world, const int32_t* fired, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, s, d, kp, summaries, world, fired);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, d, kp, summaries, world, fired);
     return hipGetLastError();
 }
 
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_renorm, dim3(blocks_for(d.n_nrn > 0 ? d.n_nrn : 1)), dim3(kBlock), 0, s,
-                       d, base);
+    hipLaunchKernelGGL(k_renorm, dim3(blocks_for(d.n_nrn > 0 ? d.n_nrn : 1)), dim3(256), 0, s, d,
+                       base);
     return hipGetLastError();
 }
 
@@ -579,7 +658,7 @@ hipError_t launch_generate(const DeviceState& d, uint32_t n_in, uint32_t n_out, 
     if (d.n_syn == 0) return hipSuccess;
     uint32_t grid = blocks_for(d.n_syn);
     if (grid > 8192) grid = 8192;
-    hipLaunchKernelGGL(k_generate, dim3(grid), dim3(kBlock), 0, s, d, n_in, n_out, seed);
+    hipLaunchKernelGGL(k_generate, dim3(grid), dim3(256), 0, s, d, n_in, n_out, seed);
     return hipGetLastError();
 }
 
@@ -589,7 +668,7 @@ hipError_t launch_checksum(const DeviceState& d, uint64_t* out_dev, hipStream_t 
     if (e != hipSuccess || d.n_syn == 0) return e;
     uint32_t grid = blocks_for(d.n_syn);
     if (grid > 4096) grid = 4096;
-    hipLaunchKernelGGL(k_checksum, dim3(grid), dim3(kBlock), 0, s, d, out_dev);
+    hipLaunchKernelGGL(k_checksum, dim3(grid), dim3(256), 0, s, d, out_dev);
     return hipGetLastError();
 }
 
@@ -597,8 +676,8 @@ hipError_t launch_stamp_list(const DeviceState& d, const uint32_t* idx_dev, uint
                              const uint64_t* value_dev, uint64_t value, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_stamp_list, dim3(blocks_for(n)), dim3(kBlock), 0, s, d, idx_dev, n,
-                       value_dev, value);
+    hipLaunchKernelGGL(k_stamp_list, dim3(blocks_for(n)), dim3(256), 0, s, d, idx_dev, n, value_dev,
+                       value);
     return hipGetLastError();
 }
 

@@ -12,7 +12,9 @@
  *
  * Rules of the boundary:
  *   - plain C types only (no torch, no HIP types: streams are `void*` that hold
- *     a hipStream_t, NULL = the handle's own stream);
+ *     a hipStream_t, NULL = the default stream).  Pass functions
+ *     (abnn_traverse, abnn_shard_*) only enqueue on that stream; every other
+ *     function is synchronous and first waits for all work on the device;
  *   - every function returns an abnn_status; no exception crosses the ABI
  *     (the reference threw a *pointer* `new std::exception()` from Brain::load,
  *     brain.cpp:174 -- here that case is ABNN_ERR_SIZE_MISMATCH);
@@ -201,8 +203,8 @@ abnn_status abnn_set_auto_stimulus(abnn_brain* b, uint64_t first, uint64_t count
 /* ---- passes: Brain::encode_traversal + commit/wait ------------------------
  * brain.cpp:87-141 + brain-engine.cpp:136-141.  Enqueues `passes` whole C1
  * passes (traversal + clock tick + renormalisation when the pass-start clock
- * exceeds renorm_thresh) on `stream` (NULL = the handle's stream).  Returns
- * without waiting; abnn_synchronize waits.                                    */
+ * exceeds renorm_thresh) on `stream` (NULL = the default stream).  Returns
+ * without waiting; abnn_synchronize waits for `stream` and the device.       */
 abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream);
 abnn_status abnn_synchronize(abnn_brain* b, void* stream);
 
