@@ -88,9 +88,10 @@ void free_all(abnn_brain* b)
     if (!b) return;
     (void)hipSetDevice(b->device);
     void* ptrs[] = {b->d.syn,       b->d.last_fired, b->d.last_visited,  b->scalar_block,
-                    b->d.bitmap,    b->d.filter,     b->d.block_tot,     b->d.block_pre,
-                    b->d.tile_pre,  b->d.g2buf,      b->d.apply_partial, b->d.fired,
-                    b->d.summary,   b->d.work,       b->idx_scratch,     b->u64_scratch};
+                    b->d.bitmap,    b->d.filter,     b->d.range_tot,     b->d.range_tile0,
+                    b->d.tile_cnt,  b->d.tile_pre,   b->d.g2buf,         b->d.apply_partial,
+                    b->d.fired,     b->d.summary,    b->d.work,          b->idx_scratch,
+                    b->u64_scratch,  b->d.tile_range};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : b->events) {
@@ -179,6 +180,7 @@ abnn_status run_gate(abnn_brain* b, int64_t* summary_out, hipStream_t s)
     ST_TRY(time_begin(b, s, &ev));
     HIP_TRY(launch_gate(b->d, b->kp, s));
     if (ev) HIP_TRY(hipEventRecord(ev->b, s));
+    HIP_TRY(launch_refrac(b->d, b->kp, s));
     HIP_TRY(launch_scan(b->d, b->kp, summary_out, s));
     return ABNN_OK;
 }
@@ -275,7 +277,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
         }
     }
     REQUIRE(gate_shape_supported(gate_block, gate_k), "unsupported ABNN_GATE shape");
-    const uint64_t iter_events = (uint64_t)gate_block * gate_k;
+    const uint64_t iter_events = 64ull * gate_k;  // one wave iteration
     const uint64_t iters = (E + iter_events - 1) / iter_events;
     REQUIRE(iters < 0x7FFFFFFFull, "too many events for one handle");
 
@@ -321,7 +323,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (per_cu <= 0) per_cu = 1;
     if (per_cu > 2) per_cu = 2;
     uint64_t G = std::min<uint64_t>(iters, std::min<uint64_t>((uint64_t)cus * per_cu, kMaxGateBlocks));
+    // ranges are per wave; the last workgroup may own fewer than one iteration each
+    const uint64_t waves = gate_block / 64;
+    G = std::min<uint64_t>(G, (iters + waves - 1) / waves);
+    if (G == 0 && iters > 0) G = 1;
     d.gate_blocks = (uint32_t)G;
+    d.n_ranges = (uint32_t)(G * waves);
     d.n_bitmap_words = (uint32_t)(2 * ((n_nrn + 63) / 64));
     d.filter_exact = d.n_bitmap_words <= (uint32_t)kFilterWords ? 1u : 0u;
     abnn_status s;
@@ -337,9 +344,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.rbar = d.reward + 1;
     if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.filter, kFilterWords)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.block_tot, G)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.block_pre, G)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.tile_pre, G + 1)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.range_tot, d.n_ranges)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.range_tile0, d.n_ranges)) != ABNN_OK) return fail(s);
+    const uint64_t max_tiles = E / kApplyBlock + d.n_ranges + 1;
+    if ((s = dalloc(&d.tile_cnt, max_tiles)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.tile_range, max_tiles)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.tile_pre, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.g2buf, iters * iter_events)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.apply_partial, kApplyGrid)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.fired, p.max_spikes + 1u)) != ABNN_OK) return fail(s);

@@ -14,14 +14,14 @@ namespace abnn {
 // bitmap folded modulo kFilterWords 32-bit words (512 Ki bits = 64 KiB).  When
 // the bitmap itself fits (N_NRN <= 512 Ki) the filter IS the bitmap.
 constexpr int kFilterWords = 16384;
-constexpr int kApplyBlock = 256;   // one apply tile = 256 gated events
+constexpr int kApplyBlock = 256;   // one tile = 256 consecutive pre-gated events of a range
 constexpr int kApplyGrid = 1024;   // persistent grid of the apply kernel
-constexpr int kScanThreads = 1024; // one thread per gate workgroup in the scan
-constexpr int kMaxGateBlocks = kScanThreads;
+constexpr int kScanThreads = 1024; // the range scan is one workgroup
+constexpr int kMaxGateBlocks = 1024;
 
 // Per-pass bookkeeping in device memory (one per handle).
 struct alignas(16) PassWork {
-    uint32_t total_tiles;  // apply tiles queued this pass
+    uint32_t total_tiles;  // tiles of pre-gated entries this pass
     uint32_t t0_g2;        // global event 0 passed both gates this pass
     uint64_t events;       // visited events of this shard this pass
     uint64_t g1;           // passed the pre-gate
@@ -39,10 +39,12 @@ struct DeviceState {
     float* rbar;              // [1]
     uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
     uint32_t* filter;         // [kFilterWords] folded bitmap
-    uint4* block_tot;         // [gate_blocks] {gated, candidates, pre-gated, t0}
-    uint32_t* block_pre;      // [gate_blocks] exclusive candidate prefix (capped)
-    uint32_t* tile_pre;       // [gate_blocks + 1] exclusive prefix of apply tiles
-    uint4* g2buf;             // [iters * iter_events] gated entries, per-workgroup regions
+    uint4* range_tot;         // [n_ranges] {pre-gated entries, 0, 0, 0}
+    uint32_t* range_tile0;    // [n_ranges] first entry tile of each range
+    uint32_t* tile_range;     // [max_tiles] range of each tile
+    uint2* tile_cnt;          // [max_tiles] {candidates, passed refractory} per tile
+    uint32_t* tile_pre;       // [max_tiles] exclusive candidate prefix (capped; = budget: skip)
+    uint4* g2buf;             // [iters * iter_events] gated entries, per-range regions
     uint2* apply_partial;     // [kApplyGrid] {updated, fired} per apply workgroup
     int32_t* fired;           // [max_spikes] internal spike list (world = 1)
     int64_t* summary;         // [ABNN_SUMMARY_WORDS] internal (world = 1)
@@ -54,8 +56,9 @@ struct DeviceState {
     uint32_t n_bitmap_words;  // 2 * ceil(n_nrn / 64)
     uint32_t filter_exact;    // bitmap fits the filter: no global confirmation
     uint32_t gate_blocks;     // persistent gate workgroups G
+    uint32_t n_ranges;        // G * waves per workgroup: one contiguous range per wave
     uint32_t iters;           // ceil(events / iter_events)
-    uint32_t iter_events;     // gate_block * gate_k events per workgroup iteration
+    uint32_t iter_events;     // 64 * gate_k events per wave iteration
     uint32_t gate_block;      // threads per gate workgroup
     uint32_t gate_k;          // events per thread per iteration
 };
@@ -78,6 +81,7 @@ int gate_blocks_per_cu(uint32_t block, uint32_t k, bool track);
 hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,
                          uint64_t stim_count, hipStream_t s);
 hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s);
+hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream_t s);
 hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int64_t* summary_out,
                        hipStream_t s);
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,

@@ -8,19 +8,19 @@
 //                bitmap, bit i = (now - lastFired[i]) <= WINDOW_PRE; the
 //                per-pass stimulus stamp is fused here.
 //   k_fold     : bitmap folded modulo 512 Ki bits -> the 64 KiB pre-spike filter.
-//   k_gate     : THE streaming kernel.  Persistent workgroups, each sweeping one
-//                contiguous range of events with non-temporal dwordx4 loads of
+//   k_gate     : THE streaming kernel.  Persistent workgroups whose waves each
+//                sweep one contiguous range of events with non-temporal dwordx4 loads of
 //                the 16-B SynapsePacked records (1 KiB per wave-instruction,
 //                next iteration's loads in flight while the current one is
 //                gated).  Pre-spike gate (brain.metal:73-77) = one LDS filter
 //                bit (+ an L2 bitmap word on a filter hit unless the filter is
 //                exact); refractory gate (brain.metal:79-83) = a real 8-B gather
 //                of lastFired[dst] for the few events that pass; spike-candidate
-//                test (brain.metal:91-92); gated events are compacted in event
-//                order into the workgroup's region with their workgroup-local
-//                candidate prefix.
-//   k_scan     : one workgroup: exclusive candidate prefix over the gate
-//                workgroups = the ordered global spike budget of schedule C1
+//                test (brain.metal:91-92); each wave compacts its gated events
+//                in event order into its own region with their wave-local
+//                candidate prefix (ballots only, no barrier).
+//   k_scan     : one workgroup: exclusive candidate prefix over the wave
+//                ranges = the ordered global spike budget of schedule C1
 //                (brain.metal:85-98 without its races) + the apply tiling.
 //   k_apply    : weight update (brain.metal:101-122) of every gated event that
 //                still had budget; spikes land at their budget position.
@@ -167,25 +167,36 @@ __device__ __forceinline__ uint64_t range_begin(uint32_t b, uint32_t iters, uint
 
 // ---------------------------------------------------------------------------
 // k_bitmap: bit i = (now - lastFired[i]) <= window_pre; stimulus stamp fused.
+// A wave covers 256 neurons = four bitmap words; lane l owns neurons
+// base + 64q + l, so ballot q is word q (four coalesced 512-B loads per wave).
 __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
                                                 uint64_t stim_first, uint64_t stim_count)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const uint64_t base = wave * 256 + lane;
     const uint64_t now = *d.clock;
-    bool bit = false;
-    if (i < d.n_nrn) {
-        uint64_t L;
-        if (i - stim_first < stim_count) {  // unsigned range test
-            L = now;
-            d.last_fired[i] = now;          // Brain::inject_inputs, brain.cpp:82
-        } else {
-            L = __builtin_nontemporal_load(d.last_fired + i);
-        }
-        bit = (now - L) <= (uint64_t)kp.window_pre;
+    uint64_t L[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t i = base + 64 * q;
+        L[q] = i < d.n_nrn ? __builtin_nontemporal_load(d.last_fired + i) : ~0ull;
     }
-    const uint64_t m = __ballot(bit);
-    if ((threadIdx.x & 63) == 0 && i < d.n_nrn)
-        reinterpret_cast<uint64_t*>(d.bitmap)[i >> 6] = m;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t i = base + 64 * q;
+        bool bit = false;
+        if (i < d.n_nrn) {
+            if (i - stim_first < stim_count) {  // unsigned range test
+                L[q] = now;
+                d.last_fired[i] = now;          // Brain::inject_inputs, brain.cpp:82
+            }
+            bit = (now - L[q]) <= (uint64_t)kp.window_pre;
+        }
+        const uint64_t m = __ballot(bit);
+        if (lane == 0 && (wave * 4 + q) * 64 < d.n_nrn)
+            reinterpret_cast<uint64_t*>(d.bitmap)[wave * 4 + q] = m;
+    }
 }
 
 // k_fold: filter[j] = OR over m of bitmap[j + m * kFilterWords].
@@ -199,24 +210,30 @@ __global__ __launch_bounds__(256) void k_fold(DeviceState d)
 }
 
 // ---------------------------------------------------------------------------
-// k_gate: the streaming kernel (see file header).
+// k_gate: the streaming kernel (see file header).  Every wave owns one
+// contiguous range of events.  The hot loop holds only what a 16-B record
+// stream needs: the LDS filter, an L2 bitmap word on a filter hit, and the
+// next iteration's records in flight.  Events that pass the pre-gate (~0.2 %
+// in steady state) are staged in event order in the wave's LDS slab and
+// written out as whole-wave coalesced stores, so stores rarely sit between the
+// prefetch and its wait (vmcnt retires in issue order, stores included).
 template <int BLOCK, int K, bool kTrack>
 __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
     constexpr int NW = BLOCK / 64;
-    constexpr uint32_t IE = BLOCK * K;
+    constexpr uint32_t IE = 64 * K;
+    constexpr uint32_t kFlushAt = 32;            // staged entries before a flush
+    constexpr uint32_t kStage = kFlushAt + 64;   // one k-step adds at most 64
     __shared__ uint32_t s_filter[kFilterWords];
-    __shared__ uint32_t s_g2[2][K][NW];
-    __shared__ uint32_t s_c[2][K][NW];
-    __shared__ uint32_t s_g1[NW];
+    __shared__ uint4 s_stage[NW][kStage];
 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint64_t it_begin = range_begin(b, d.iters, G), it_end = range_begin(b + 1, d.iters, G);
+    const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
+    const uint64_t it_begin = range_begin(r, d.iters, NR), it_end = range_begin(r + 1, d.iters, NR);
     const uint64_t region = it_begin * IE;
     const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
-    const uint32_t budget = kp.max_spikes;
     const bool exact = d.filter_exact != 0;
+    uint4* stage = s_stage[wid];
 
     {
         const uint4* src = reinterpret_cast<const uint4*>(d.filter);
@@ -229,11 +246,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         const uint64_t base = it * IE;
         if (base + IE <= d.events) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) nxt[k] = load_stream16(d.syn + base + k * BLOCK + tid);
+            for (int k = 0; k < K; ++k) nxt[k] = load_stream16(d.syn + base + k * 64 + lane);
         } else {
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                const uint64_t t = base + k * BLOCK + tid;
+                const uint64_t t = base + k * 64 + lane;
                 nxt[k] = t < d.events ? load_stream16(d.syn + t) : make_uint4(0u, 0u, 0u, 0u);
             }
         }
@@ -241,128 +258,172 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     if (it_begin < it_end) issue(it_begin);
     __syncthreads();
 
-    uint32_t g2_run = 0, c_run = 0, g1_wave = 0, t0 = 0;
-    uint32_t par = 0;
-    for (uint64_t it = it_begin; it < it_end; ++it, par ^= 1u) {
+    const uint32_t nn = (uint32_t)d.n_nrn;  // N_NRN < 2^32 (checked at create)
+    uint32_t pend = 0, flushed = 0;
+    auto flush = [&]() {  // wave-uniform: write the staged entries, in order
+        if (lane < pend) d.g2buf[region + flushed + lane] = stage[lane];
+        if (lane + 64 < pend) d.g2buf[region + flushed + 64 + lane] = stage[64 + lane];
+        flushed += pend;
+        pend = 0;
+    };
+    for (uint64_t it = it_begin; it < it_end; ++it) {
         uint4 rec[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) rec[k] = nxt[k];
-        if (it + 1 < it_end) issue(it + 1);  // next iteration's records in flight
         const uint64_t base = it * IE;
-
-        // Pre-spike gate, brain.metal:73-77.
-        uint32_t g1m = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t s = rec[k].x, ds = rec[k].y;
-            const bool ok = base + k * BLOCK + tid < d.events && s < d.n_nrn && ds < d.n_nrn;
-            const uint32_t fw = s_filter[(s >> 5) & (kFilterWords - 1)];
-            if (ok && ((fw >> (s & 31u)) & 1u)) g1m |= 1u << k;
-        }
-        if (!exact) {  // confirm filter hits on the exact (L2-resident) bitmap
+        uint32_t vmask = (1u << K) - 1u;  // events of this lane that exist
+        if (base + IE > d.events) {       // only the sweep's last iteration
+            vmask = 0;
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if ((g1m >> k) & 1u) {
-                    const uint32_t s = rec[k].x;
-                    if (!((d.bitmap[s >> 5] >> (s & 31u)) & 1u)) g1m &= ~(1u << k);
-                }
+                if (base + k * 64 + lane < d.events) vmask |= 1u << k;
         }
 
-        // Refractory gate, brain.metal:79-83: real 8-B gather of lastFired[dst].
-        uint64_t ld[K];
+        // Pre-spike gate, brain.metal:73-77, first on the LDS filter: all K
+        // reads issued back to back (the word index is masked, so always in
+        // bounds), no branches.
+        uint32_t fw[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) ld[k] = ((g1m >> k) & 1u) ? d.last_fired[rec[k].y] : 0ull;
-
-        uint32_t g2m = 0, cm = 0;
+        for (int k = 0; k < K; ++k) fw[k] = s_filter[(rec[k].x >> 5) & (kFilterWords - 1)];
+        uint32_t fm = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            if (((g1m >> k) & 1u) && (now - ld[k]) > (uint64_t)kp.refractory) {
-                g2m |= 1u << k;
-                const uint64_t tg = d.syn_offset + base + k * BLOCK + tid;
-                if (spike_candidate(kp, __uint_as_float(rec[k].z), tg, now)) cm |= 1u << k;
-            }
+            const bool hit = ((fw[k] >> (rec[k].x & 31u)) & 1u) && rec[k].x < nn && rec[k].y < nn;
+            fm |= (hit ? 1u : 0u) << k;
         }
+        fm &= vmask;
+        // Filter hits are confirmed on the exact bitmap word (L2-resident);
+        // issued before the next iteration's stream loads.
+        uint32_t cw[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            cw[k] = 0xFFFFFFFFu;
+            if (!exact && ((fm >> k) & 1u)) cw[k] = d.bitmap[rec[k].x >> 5];
+        }
+        if (it + 1 < it_end) issue(it + 1);  // next iteration's records in flight
+
         if (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (base + k * BLOCK + tid < d.events && rec[k].y < d.n_nrn)
-                    d.last_visited[rec[k].y] = now;
+                if (((vmask >> k) & 1u) && rec[k].y < nn) d.last_visited[rec[k].y] = now;
         }
-        if (it == 0 && tid == 0 && d.syn_offset == 0 && (g2m & 1u)) t0 = 1;
-
-        // In-order compaction: event order inside an iteration is (k, wave, lane).
-        uint32_t mb_g2[K], mb_c[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const uint64_t bg = __ballot((g2m >> k) & 1u);
-            const uint64_t bc = __ballot((cm >> k) & 1u);
-            g1_wave += (uint32_t)__popcll(__ballot((g1m >> k) & 1u));
-            mb_g2[k] = mbcnt64(bg);
-            mb_c[k] = mbcnt64(bc);
-            if (lane == 0) {
-                s_g2[par][k][wid] = (uint32_t)__popcll(bg);
-                s_c[par][k][wid] = (uint32_t)__popcll(bc);
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            uint32_t bw_g2 = 0, bw_c = 0, tot_g2 = 0, tot_c = 0;
-#pragma unroll
-            for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
-                const uint32_t a = s_g2[par][k][w], c = s_c[par][k][w];
-                bw_g2 += w < wid ? a : 0u;
-                bw_c += w < wid ? c : 0u;
-                tot_g2 += a;
-                tot_c += c;
-            }
-            if ((g2m >> k) & 1u) {
-                const uint32_t slot = g2_run + bw_g2 + mb_g2[k];
-                const uint32_t pre = c_run + bw_c + mb_c[k];
-                uint4 e;
-                e.x = (uint32_t)(base - region) + k * BLOCK + tid;  // event, relative to the region
-                e.y = (pre < budget ? pre : budget) | (((cm >> k) & 1u) << 31);
-                e.z = rec[k].z;                                        // w
-                e.w = __float_as_uint((float)(now - ld[k]));          // isi, brain.metal:116
-                d.g2buf[region + slot] = e;
-            }
-            g2_run += tot_g2;
-            c_run += tot_c;
+            const bool g1 = ((fm >> k) & 1u) && ((cw[k] >> (rec[k].x & 31u)) & 1u);
+            const uint64_t b1 = __ballot(g1);
+            if (g1)
+                stage[pend + mbcnt64(b1)] =
+                    make_uint4((uint32_t)(base - region) + k * 64 + lane, rec[k].y, rec[k].z, 0u);
+            pend += (uint32_t)__popcll(b1);
+            if (pend >= kFlushAt) flush();
         }
     }
-    if (lane == 0) s_g1[wid] = g1_wave;
-    if (tid == 0 && t0) d.work->t0_g2 = 1;
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t g1 = 0;
+    flush();
+    if (lane == 0) d.range_tot[r] = make_uint4(flushed, 0u, 0u, 0u);
+}
+
+// ---------------------------------------------------------------------------
+// Pre-gated entries are processed as tiles of kApplyBlock consecutive entries
+// of one range; tile order = event order; tile_range[t] names the range.
+// k_tiles: one workgroup: first tile of every range and the tile -> range map.
+__global__ __launch_bounds__(kScanThreads) void k_tiles(DeviceState d)
+{
+    __shared__ uint64_t s_wave[kScanThreads / 64];
+    const uint32_t tid = threadIdx.x, NR = d.n_ranges;
+    const uint32_t per = (NR + kScanThreads - 1) / kScanThreads;
+    const uint32_t lo = min(NR, tid * per), hi = min(NR, lo + per);
+    uint64_t tiles = 0;
+    for (uint32_t r = lo; r < hi; ++r) tiles += (d.range_tot[r].x + kApplyBlock - 1) / kApplyBlock;
+    uint64_t total;
+    uint64_t t0 = block_exclusive_scan(tiles, &total, s_wave);
+    for (uint32_t r = lo; r < hi; ++r) {
+        d.range_tile0[r] = (uint32_t)t0;
+        const uint32_t nt = (d.range_tot[r].x + kApplyBlock - 1) / kApplyBlock;
+        for (uint32_t q = 0; q < nt; ++q) d.tile_range[t0 + q] = r;
+        t0 += nt;
+    }
+    if (tid == 0) d.work->total_tiles = (uint32_t)total;
+}
+
+// k_refrac: per pre-gated entry, the refractory gate with a real 8-B gather of
+// lastFired[dst] (brain.metal:79-83), the spike-candidate test
+// (brain.metal:91-92) and the homeostasis input isi (brain.metal:116); the
+// tile-local candidate prefix; written back in place.  Entry after this pass:
+// x = event - region | passed-refractory << 31, y = tile-local candidate
+// prefix | candidate << 31, z = w, w = isi.
+__global__ __launch_bounds__(kApplyBlock) void k_refrac(DeviceState d, KernelParams kp)
+{
+    __shared__ uint32_t s_c[kApplyBlock / 64], s_g[kApplyBlock / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t now = *d.clock;
+    const uint32_t T = d.work->total_tiles;
+    for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
+        const uint32_t r = d.tile_range[tile];
+        const uint32_t n = d.range_tot[r].x;
+        const uint32_t j = (tile - d.range_tile0[r]) * kApplyBlock + tid;
+        const uint64_t region = range_begin(r, d.iters, d.n_ranges) * d.iter_events;
+        const bool valid = j < n;
+        uint4 e = valid ? d.g2buf[region + j] : make_uint4(0u, 0u, 0u, 0u);
+        const uint64_t ld = valid ? d.last_fired[e.y] : 0ull;
+        const bool g2 = valid && (now - ld) > (uint64_t)kp.refractory;
+        const uint64_t tg = d.syn_offset + region + e.x;
+        const bool cand = g2 && spike_candidate(kp, __uint_as_float(e.z), tg, now);
+        const uint64_t bc = __ballot(cand), bg = __ballot(g2);
+        if (lane == 0) {
+            s_c[wid] = (uint32_t)__popcll(bc);
+            s_g[wid] = (uint32_t)__popcll(bg);
+        }
+        __syncthreads();
+        uint32_t pre = mbcnt64(bc), tc = 0, tgt = 0;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) g1 += s_g1[w];
-        d.block_tot[b] = make_uint4(g2_run, c_run, g1, 0u);
+        for (uint32_t w = 0; w < kApplyBlock / 64; ++w) {
+            pre += w < wid ? s_c[w] : 0u;
+            tc += s_c[w];
+            tgt += s_g[w];
+        }
+        if (g2 && tg == 0) d.work->t0_g2 = 1;
+        if (valid) {
+            e.x |= (g2 ? 1u : 0u) << 31;
+            e.y = pre | ((cand ? 1u : 0u) << 31);
+            e.w = __float_as_uint((float)(now - ld));
+            d.g2buf[region + j] = e;
+        }
+        if (tid == 0) d.tile_cnt[tile] = make_uint2(tc, tgt);
+        __syncthreads();
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_scan: ordered spike budget over the gate workgroups (one workgroup).
+// k_scan: ordered spike budget over the tiles (one workgroup, in event order).
 __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelParams kp,
                                                        int64_t* summary_out)
 {
     __shared__ uint64_t s_wave[kScanThreads / 64];
     __shared__ uint64_t s_red[2][kScanThreads / 64];
-    const uint32_t tid = threadIdx.x, G = d.gate_blocks;
+    const uint32_t tid = threadIdx.x, T = d.work->total_tiles;
+    const uint32_t per = (T + kScanThreads - 1) / kScanThreads;
+    const uint32_t lo = min(T, tid * per), hi = min(T, lo + per);
     const uint64_t budget = kp.max_spikes;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (tid < G) v = d.block_tot[tid];
-    uint64_t cand_total;
-    const uint64_t excl = block_exclusive_scan(v.y, &cand_total, s_wave);
-    const uint64_t tiles =
-        (tid < G && v.x > 0 && excl < budget) ? (v.x + kApplyBlock - 1) / kApplyBlock : 0;
-    uint64_t tiles_total;
-    const uint64_t tpre = block_exclusive_scan(tiles, &tiles_total, s_wave);
-    if (tid < G) {
-        d.block_pre[tid] = (uint32_t)(excl < budget ? excl : budget);
-        d.tile_pre[tid] = (uint32_t)tpre;
+
+    uint64_t cand = 0, g2 = 0;
+    for (uint32_t t = lo; t < hi; ++t) {
+        const uint2 v = d.tile_cnt[t];  // {candidates, passed refractory}
+        cand += v.x;
+        g2 += v.y;
     }
-    const uint64_t wg2 = wave_sum((uint64_t)v.x), wg1 = wave_sum((uint64_t)v.z);
+    uint64_t cand_total;
+    uint64_t pre = block_exclusive_scan(cand, &cand_total, s_wave);
+    for (uint32_t t = lo; t < hi; ++t) {
+        const uint2 v = d.tile_cnt[t];
+        // a tile is applied iff some event in it passed the refractory gate
+        // while the budget lasted; inactive tiles carry the budget itself
+        d.tile_pre[t] = (uint32_t)(v.y > 0 && pre < budget ? pre : budget);
+        pre += v.x;
+    }
+    uint64_t g1 = 0;
+    const uint32_t NR = d.n_ranges, rper = (NR + kScanThreads - 1) / kScanThreads;
+    for (uint32_t r = min(NR, tid * rper); r < min(NR, tid * rper + rper); ++r) g1 += d.range_tot[r].x;
+    const uint64_t wg2 = wave_sum(g2), wg1 = wave_sum(g1);
     if ((tid & 63) == 0) {
         s_red[0][tid >> 6] = wg2;
         s_red[1][tid >> 6] = wg1;
@@ -374,14 +435,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelPara
             tg2 += s_red[0][w];
             tg1 += s_red[1][w];
         }
-        d.tile_pre[G] = (uint32_t)tiles_total;
         const uint64_t capped = cand_total < budget ? cand_total : budget;
         const uint32_t t0 = d.work->t0_g2;
         summary_out[0] = (int64_t)capped;
         summary_out[1] = (int64_t)t0;
         summary_out[2] = (int64_t)d.events;
         summary_out[3] = (int64_t)tg2;
-        d.work->total_tiles = (uint32_t)tiles_total;
         d.work->t0_g2 = 0;  // re-armed for the next pass
         d.work->events = d.events;
         d.work->g1 = tg1;
@@ -400,29 +459,25 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(DeviceState d, KernelPara
     const uint64_t budget = kp.max_spikes;
     const float R = *d.reward, rb = *d.rbar;  // pass-start values (C1), brain.metal:105-106
     uint64_t off = 0;
-    for (uint32_t r = 0; r < rank && r < world; ++r)
-        off += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 0];
+    for (uint32_t q = 0; q < rank && q < world; ++q)
+        off += (uint64_t)summaries[q * ABNN_SUMMARY_WORDS + 0];
     off = off < budget ? off : budget;
 
-    const uint32_t G = d.gate_blocks, T = d.work->total_tiles, IE = d.iter_events;
+    const uint32_t T = d.work->total_tiles;
     uint32_t upd = 0, nf = 0;
     for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
-        uint32_t lo = 0, hi = G;  // largest b with tile_pre[b] <= tile
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (d.tile_pre[mid] <= tile) lo = mid;
-            else hi = mid;
-        }
-        const uint32_t b = lo;
-        const uint64_t P = off + d.block_pre[b];
-        const uint32_t j = (tile - d.tile_pre[b]) * kApplyBlock + tid;
-        if (P >= budget || j >= d.block_tot[b].x) continue;
-        const uint64_t region = range_begin(b, d.iters, G) * IE;
+        const uint64_t P = off + d.tile_pre[tile];
+        if (P >= budget) continue;
+        const uint32_t r = d.tile_range[tile];
+        const uint32_t j = (tile - d.range_tile0[r]) * kApplyBlock + tid;
+        if (j >= d.range_tot[r].x) continue;
+        const uint64_t region = range_begin(r, d.iters, d.n_ranges) * d.iter_events;
         const uint4 e = d.g2buf[region + j];
+        if (!(e.x >> 31)) continue;   // stopped by the refractory gate
         const uint64_t pre = P + (e.y & 0x7FFFFFFFu);
         if (pre >= budget) continue;  // budget == 0 at this event: brain.metal:85-88
         const bool f = (e.y >> 31) != 0;
-        const uint64_t t = region + e.x;
+        const uint64_t t = region + (e.x & 0x7FFFFFFFu);
         const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.w));
         uint32_t* rec = reinterpret_cast<uint32_t*>(d.syn + t);
         rec[2] = __float_as_uint(w);       // brain.metal:122 (src/dst/pad unchanged)
@@ -588,6 +643,7 @@ int gate_blocks_per_cu(uint32_t block, uint32_t k, bool track)
         case 51204: return occupancy_shape<512, 4>(track);
         case 51208: return occupancy_shape<512, 8>(track);
         case 102404: return occupancy_shape<1024, 4>(track);
+        case 102408: return occupancy_shape<1024, 8>(track);
     }
     return 0;
 }
@@ -595,18 +651,27 @@ int gate_blocks_per_cu(uint32_t block, uint32_t k, bool track)
 bool gate_shape_supported(uint32_t block, uint32_t k)
 {
     return (block == 256 && (k == 8 || k == 16)) || (block == 512 && (k == 4 || k == 8)) ||
-           (block == 1024 && k == 4);
+           (block == 1024 && (k == 4 || k == 8));
 }
 
 hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,
                          uint64_t stim_count, hipStream_t s)
 {
     if (d.n_nrn == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_bitmap, dim3(blocks_for(d.n_nrn)), dim3(256), 0, s, d, kp, stim_first,
-                       stim_count);
+    hipLaunchKernelGGL(k_bitmap, dim3((uint32_t)((d.n_nrn + 1023) / 1024)), dim3(256), 0, s, d, kp,
+                       stim_first, stim_count);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fold, dim3(kFilterWords / 256), dim3(256), 0, s, d);
+    return hipGetLastError();
+}
+
+hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_tiles, dim3(1), dim3(kScanThreads), 0, s, d);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_refrac, dim3(kApplyGrid), dim3(kApplyBlock), 0, s, d, kp);
     return hipGetLastError();
 }
 
@@ -619,6 +684,7 @@ hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t
         case 51204: return launch_gate_shape<512, 4>(d, kp, s);
         case 51208: return launch_gate_shape<512, 8>(d, kp, s);
         case 102404: return launch_gate_shape<1024, 4>(d, kp, s);
+        case 102408: return launch_gate_shape<1024, 8>(d, kp, s);
     }
     return hipErrorInvalidValue;
 }

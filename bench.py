@@ -46,11 +46,18 @@ def parse():
 
 
 def algorithmic_bytes(stats: dict, track_visits: bool) -> int:
-    """SURVEY.md §8(d) per-event figure for the gate kernel's share of a pass:
-    16 B SynapsePacked read + 8 B lastFired[src] per visited event (+8 B
-    lastVisited write with track_visits) and 8 B lastFired[dst] per pre-gated
-    event.  (The 16 B write-back per update and 8 B per spike happen in the
-    apply/finalize kernels and are reported separately.)"""
+    """Bytes the streaming gate kernel must move from HBM: the
+    16-B SynapsePacked record of every visited event (+8 B lastVisited write per
+    event with track_visits).  The pre-spike lookup of lastFired[src] is served
+    by the per-pass 64 KiB LDS filter / L2 bitmap built by k_bitmap, which reads
+    lastFired once per pass (8 B per neuron, k_bitmap's own bytes)."""
+    e = stats["events"]
+    return 16 * e + (8 * e if track_visits else 0)
+
+
+def survey_bytes(stats: dict, track_visits: bool) -> int:
+    """SURVEY.md §8(d) per-event figure for the same work: 24 B per visited event
+    (16 B record + 8 B lastFired[src]) + 8 B lastFired[dst] per pre-gated event."""
     e = stats["events"]
     return 24 * e + (8 * e if track_visits else 0) + 8 * stats["pre_gated"]
 
@@ -148,8 +155,10 @@ def main():
     if rank == 0:
         value = total_events / dt
         avg_gate_ms = gate_ms / max(1, launches)
-        bytes_per_launch = algorithmic_bytes(stats, bool(brain.params.track_visits)) / max(1, launches)
+        track = bool(brain.params.track_visits)
+        bytes_per_launch = algorithmic_bytes(stats, track) / max(1, launches)
         achieved = bytes_per_launch / (avg_gate_ms * 1e-3) / 1e9
+        survey_per_launch = survey_bytes(stats, track) / max(1, launches)
         traffic = load_traffic(args.config) if world == 1 else None
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -157,7 +166,13 @@ def main():
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
             "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4),
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "bytes_formula": "24*E + 8*G1 (SURVEY §8d; E visited, G1 pre-gated)",
+            "bytes_formula": "16*E (SynapsePacked stream; E visited events) -- DESIGN.md §5",
+            "survey_formula_bytes_per_launch": int(survey_per_launch),
+            "survey_formula_achieved": round(survey_per_launch / (avg_gate_ms * 1e-3) / 1e9, 1),
+            "survey_formula": "24*E + 8*G1 (SURVEY §8d; G1 pre-gated) -- counts an 8-B lastFired[src] "
+                              "gather per event that this design answers from LDS/L2",
+            "traffic_source": "profiles/traffic_%s.json (rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE)"
+                              % args.config if traffic else None,
             "pass_ms": round(dt / args.steps * 1e3, 4),
         }
         cpu = None

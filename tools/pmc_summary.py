@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run into committed evidence under profiles/.
+
+* profiles/<tag>_kernel_stats.csv  : rocprofv3 --stats output (whole run)
+* profiles/<tag>_steady_state.txt  : per-kernel medians over the last 30 passes
+* profiles/traffic_<cfg>.json      : k_gate HBM bytes per launch from the PMC
+  passes.  MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
+  FETCH_SIZE reads exactly half the bytes of a wide (16 B/lane) coalesced
+  streaming read, which is what k_gate's record stream is, so the read side is
+  doubled; WRITE_SIZE is used as is.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+import sys
+
+
+def find(d, pat):
+    hits = glob.glob(os.path.join(d, "**", pat), recursive=True)
+    return hits[0] if hits else None
+
+
+def steady(trace_csv, n_last=30):
+    rows = list(csv.DictReader(open(trace_csv)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_bitmap")]
+    per = {}
+    starts = idx[-n_last:]
+    for a in starts:
+        j = a
+        while j < len(rows) and (j == a or not rows[j]["Kernel_Name"].startswith("k_bitmap")):
+            r = rows[j]
+            per.setdefault(r["Kernel_Name"], []).append(
+                (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            j += 1
+    spans = [(int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
+             for a, b in zip(starts[:-1], starts[1:])]
+    return per, spans
+
+
+def pmc_values(d, counter):
+    f = find(d, "*counter_collection*.csv")
+    if not f:
+        return []
+    vals = []
+    for r in csv.DictReader(open(f)):
+        if r.get("Kernel_Name", "").startswith("k_gate") and r.get("Counter_Name") == counter:
+            vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    out, tag, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
+    os.makedirs("profiles", exist_ok=True)
+    stats = find(os.path.join(out, "trace"), "*kernel_stats.csv")
+    trace = find(os.path.join(out, "trace"), "*kernel_trace.csv")
+    if stats:
+        shutil.copy(stats, f"profiles/{tag}_kernel_stats.csv")
+    lines = []
+    if trace:
+        per, spans = steady(trace)
+        lines.append(f"steady state, last {len(spans) + 1} passes (us): median  min  max")
+        for k, v in per.items():
+            v = sorted(v)
+            lines.append(f"{k:14s} {statistics.median(v):9.2f} {v[0]:9.2f} {v[-1]:9.2f}")
+        if spans:
+            lines.append(f"pass span median {statistics.median(spans):.2f} us")
+    # last 10 timed k_gate launches of each PMC pass are steady state
+    fetch = pmc_values(os.path.join(out, "fetch"), "FETCH_SIZE")[-10:]
+    write = pmc_values(os.path.join(out, "write"), "WRITE_SIZE")[-10:]
+    res = {"config": cfg, "tag": tag, "kernel": "k_gate"}
+    if fetch and write:
+        f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+        res.update({
+            "fetch_size_kib_raw": f_kib, "write_size_kib": w_kib,
+            "fetch_bytes_corrected": f_kib * 1024 * 2,
+            "write_bytes": w_kib * 1024,
+            "bytes_per_launch": f_kib * 1024 * 2 + w_kib * 1024,
+            "correction": "FETCH_SIZE x2 (gfx950 wide-stream undercount), KiB -> bytes",
+            "launches_used": min(len(fetch), len(write)),
+        })
+        lines.append(f"k_gate PMC per launch: FETCH_SIZE {f_kib:.0f} KiB (x2 -> {f_kib*2048/1e9:.3f} GB), "
+                     f"WRITE_SIZE {w_kib:.0f} KiB ({w_kib*1024/1e9:.4f} GB)")
+        with open(f"profiles/traffic_{cfg}.json", "w") as f:
+            json.dump(res, f, indent=1)
+    for name in ("bench_trace.json", "bench_fetch.json", "bench_write.json"):
+        p = os.path.join(out, name)
+        if os.path.exists(p):
+            txt = open(p).read().strip().splitlines()
+            if txt:
+                lines.append(f"{name}: {txt[-1][:400]}")
+    with open(f"profiles/{tag}_steady_state.txt", "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()

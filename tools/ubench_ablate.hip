@@ -1,0 +1,232 @@
+// ubench_ablate.hip -- ablation study of the gate kernel structure (not product
+// code).  Data shaped like config 3 in steady state: 150M 16-B records over
+// 5,000,512 neurons, ~15.6k recent source neurons (exact bitmap + 64 KiB
+// folded filter), lastFired such that ~0.2 % of events pass the pre-gate.
+//
+// Variants (template flags) -- each times the same sweep:
+//   STREAM   : loads only (floor)
+//   FILTER   : + LDS filter lookups
+//   CONFIRM  : + L2 bitmap confirm on filter hits
+//   GATHER   : + lastFired[dst] gather on hits
+//   STORE    : + compacted entry stores
+// Prefetch depth PF (1 or 2 iterations ahead), K events per lane.
+// build: hipcc --offload-arch=gfx950 -O3 -o tools/ubench_ablate tools/ubench_ablate.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e = (x);                                                              \
+        if (e != hipSuccess) {                                                           \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+            exit(1);                                                                     \
+        }                                                                                \
+    } while (0)
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int FW = 16384;
+
+__device__ __forceinline__ uint4 ldnt(const uint4* p)
+{
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+enum { F_FILTER = 1, F_CONFIRM = 2, F_GATHER = 4, F_STORE = 8 };
+
+template <int BLOCK, int K, int FLAGS, int PF>
+__global__ __launch_bounds__(BLOCK) void k_var(const uint4* syn, uint64_t events, uint32_t iters,
+                                               const uint32_t* bitmap, const uint32_t* filt,
+                                               const uint64_t* lastF, uint4* out, uint32_t* tot,
+                                               uint64_t now)
+{
+    constexpr int NW = BLOCK / 64;
+    constexpr uint32_t IE = 64 * K;
+    __shared__ uint32_t s_filter[(FLAGS & F_FILTER) ? FW : 1];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
+    const uint64_t itb = (uint64_t)r * iters / NR, ite = (uint64_t)(r + 1) * iters / NR;
+    const uint64_t region = itb * IE;
+    if (FLAGS & F_FILTER)
+        for (int i = tid; i < FW / 4; i += BLOCK)
+            reinterpret_cast<uint4*>(s_filter)[i] = reinterpret_cast<const uint4*>(filt)[i];
+    uint4 b0[K], b1[K];
+    auto issue = [&](uint4* dst, uint64_t it) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) dst[k] = ldnt(syn + it * IE + k * 64 + lane);
+    };
+    if (itb < ite) issue(b0, itb);
+    if (PF == 2 && itb + 1 < ite) issue(b1, itb + 1);
+    __syncthreads();
+    uint32_t acc = 0, g2_run = 0;
+    for (uint64_t it = itb; it < ite; ++it) {
+        uint4 rec[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) rec[k] = b0[k];
+        if (PF == 2) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) b0[k] = b1[k];
+        }
+        uint32_t fm = 0;
+        if (FLAGS & F_FILTER) {
+            uint32_t fw[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) fw[k] = s_filter[(rec[k].x >> 5) & (FW - 1)];
+#pragma unroll
+            for (int k = 0; k < K; ++k) fm |= ((fw[k] >> (rec[k].x & 31u)) & 1u) << k;
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc ^= rec[k].x + rec[k].y + rec[k].z;
+        }
+        uint32_t cw[K];
+        uint64_t ld[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            cw[k] = 0xFFFFFFFFu;
+            ld[k] = 0;
+            if ((fm >> k) & 1u) {
+                if (FLAGS & F_CONFIRM) cw[k] = bitmap[rec[k].x >> 5];
+                if (FLAGS & F_GATHER) ld[k] = lastF[rec[k].y];
+            }
+        }
+        if (PF == 1) {
+            if (it + 1 < ite) issue(b0, it + 1);
+        } else {
+            if (it + 2 < ite) issue(b1, it + 2);
+        }
+        uint32_t g2m = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (((fm >> k) & 1u) && ((cw[k] >> (rec[k].x & 31u)) & 1u) && now - ld[k] > 2) g2m |= 1u << k;
+        if (FLAGS & F_STORE) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint64_t bg = __ballot((g2m >> k) & 1u);
+                if ((g2m >> k) & 1u)
+                    out[region + g2_run + mbcnt64(bg)] =
+                        make_uint4((uint32_t)(it * IE - region) + k * 64 + lane, 0u, rec[k].z, 0u);
+                g2_run += (uint32_t)__popcll(bg);
+            }
+        } else {
+            acc += __popc(g2m);
+        }
+    }
+    if (lane == 0) tot[r] = g2_run;
+    if (acc == 0x9876543u) tot[r] = acc;
+}
+
+__global__ void k_fill(uint4* syn, uint64_t n, uint32_t n_nrn)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        syn[i] = make_uint4(512 + (uint32_t)(((z >> 32) * (n_nrn - 512)) >> 32),
+                            512 + (uint32_t)(((z & 0xffffffffu) * (n_nrn - 512)) >> 32), 0x3e000000u, 0u);
+    }
+}
+
+struct Var {
+    const char* name;
+    void (*launch)(int, const uint4*, uint64_t, uint32_t, const uint32_t*, const uint32_t*,
+                   const uint64_t*, uint4*, uint32_t*, uint64_t);
+    int block, k;
+};
+
+template <int BLOCK, int K, int FLAGS, int PF>
+void launch_var(int grid, const uint4* syn, uint64_t ev, uint32_t iters, const uint32_t* bm,
+                const uint32_t* f, const uint64_t* lf, uint4* out, uint32_t* tot, uint64_t now)
+{
+    hipLaunchKernelGGL((k_var<BLOCK, K, FLAGS, PF>), dim3(grid), dim3(BLOCK), 0, 0, syn, ev, iters, bm, f, lf,
+                       out, tot, now);
+}
+
+#define V(B, K, FL, PF, NAME) Var{NAME, launch_var<B, K, FL, PF>, B, K}
+
+int main()
+{
+    const uint64_t n = 150000128ull;
+    const uint32_t n_nrn = 5000512u;
+    const uint32_t nwords = (n_nrn + 31) / 32;
+    uint4 *syn, *out;
+    uint32_t *bm, *filt, *tot;
+    uint64_t* lastF;
+    CK(hipMalloc(&syn, n * 16));
+    CK(hipMalloc(&out, n * 16));
+    CK(hipMalloc(&bm, nwords * 4 + 64));
+    CK(hipMalloc(&filt, FW * 4));
+    CK(hipMalloc(&tot, 1 << 20));
+    CK(hipMalloc(&lastF, (uint64_t)n_nrn * 8));
+    hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, syn, n, n_nrn);
+    std::vector<uint32_t> h(nwords, 0), f(FW, 0);
+    std::vector<uint64_t> lf(n_nrn, 0);
+    const uint64_t now = 1000;
+    srand(7);
+    for (int i = 0; i < 15600; ++i) {
+        uint32_t s = 512 + (uint32_t)(((uint64_t)rand() * 2654435761ull) % (n_nrn - 512));
+        h[s >> 5] |= 1u << (s & 31);
+        lf[s] = now - 1 - (i % 5);
+    }
+    for (uint32_t w = 0; w < nwords; ++w) f[w & (FW - 1)] |= h[w];
+    int fpop = 0;
+    for (uint32_t w : f) fpop += __builtin_popcount(w);
+    CK(hipMemcpy(bm, h.data(), nwords * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(filt, f.data(), FW * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(lastF, lf.data(), (uint64_t)n_nrn * 8, hipMemcpyHostToDevice));
+    CK(hipDeviceSynchronize());
+    printf("filter density %.4f\n", fpop / (double)(FW * 32));
+
+    std::vector<Var> vars = {
+        V(512, 8, 0, 1, "512x8 stream pf1"),
+        V(512, 8, 0, 2, "512x8 stream pf2"),
+        V(512, 8, F_FILTER, 1, "512x8 +filter pf1"),
+        V(512, 8, F_FILTER, 2, "512x8 +filter pf2"),
+        V(512, 8, F_FILTER | F_CONFIRM, 1, "512x8 +confirm pf1"),
+        V(512, 8, F_FILTER | F_CONFIRM | F_GATHER, 1, "512x8 +gather pf1"),
+        V(512, 8, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 1, "512x8 full pf1"),
+        V(512, 8, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 2, "512x8 full pf2"),
+        V(512, 4, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 1, "512x4 full pf1"),
+        V(512, 4, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 2, "512x4 full pf2"),
+        V(1024, 4, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 2, "1024x4 full pf2"),
+        V(1024, 4, F_FILTER, 2, "1024x4 +filter pf2"),
+        V(512, 4, F_FILTER | F_STORE, 2, "512x4 filter+store pf2"),
+    };
+    int cus = 256;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    std::vector<std::vector<float>> t(vars.size());
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int round = 0; round < 5; ++round) {
+        for (size_t v = 0; v < vars.size(); ++v) {
+            const uint32_t iters = (uint32_t)((n + 64 * vars[v].k - 1) / (64 * vars[v].k));
+            const int grid = cus * 2;
+            vars[v].launch(grid, syn, n, iters, bm, filt, lastF, out, tot, now);
+            CK(hipEventRecord(a));
+            for (int rep = 0; rep < 5; ++rep)
+                vars[v].launch(grid, syn, n, iters, bm, filt, lastF, out, tot, now);
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            CK(hipGetLastError());
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            t[v].push_back(ms / 5);
+        }
+    }
+    for (size_t v = 0; v < vars.size(); ++v) {
+        std::sort(t[v].begin(), t[v].end());
+        printf("%-26s median %.4f ms  min %.4f ms  (%6.1f GB/s stream)\n", vars[v].name, t[v][2], t[v][0],
+               n * 16.0 / (t[v][2] * 1e6));
+    }
+    return 0;
+}
