@@ -54,7 +54,12 @@ class Engine(Protocol):
 
 
 class TorchComm:
-    """torch.distributed communicator (backend nccl = RCCL on ROCm, or gloo)."""
+    """torch.distributed communicator.
+
+    backend nccl (= RCCL on ROCm): the collectives run on device tensors, ordered
+    with the pass kernels through the current stream.  backend gloo (CPU tests,
+    or the single-GPU rehearsal of the multi-rank bench): device tensors are
+    staged through host memory."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -63,15 +68,25 @@ class TorchComm:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.staged = dist.get_backend(group) == "gloo"
+
+    def _run(self, fn, *tensors):
+        if not (self.staged and any(t.is_cuda for t in tensors)):
+            fn(*tensors)
+            return
+        host = [t.cpu() for t in tensors]
+        fn(*host)
+        for t, h in zip(tensors, host):
+            t.copy_(h)
 
     def all_gather(self, out, inp) -> None:
-        self._dist.all_gather_into_tensor(out, inp, group=self.group)
+        self._run(lambda o, i: self._dist.all_gather_into_tensor(o, i, group=self.group), out, inp)
 
     def all_reduce_sum(self, t) -> None:
-        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self.group)
+        self._run(lambda x: self._dist.all_reduce(x, op=self._dist.ReduceOp.SUM, group=self.group), t)
 
     def all_reduce_max(self, t) -> None:
-        self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX, group=self.group)
+        self._run(lambda x: self._dist.all_reduce(x, op=self._dist.ReduceOp.MAX, group=self.group), t)
 
 
 def sharded_pass(engine: Engine, comm, summary, gathered, fired) -> None:

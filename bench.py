@@ -107,19 +107,26 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
+    # one GPU per rank; ABNN_DIST_BACKEND=gloo rehearses the multi-rank path with
+    # ranks sharing the visible GPUs (exchange tensors staged through the host)
+    backend = os.environ.get("ABNN_DIST_BACKEND", "nccl")
+    device = local_rank if backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     if world > 1:
         sb = ShardedBrain(TorchComm(), wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events,
-                          device=local_rank)
+                          device=device)
         brain = sb.brain
         step = sb.step
     else:
-        brain = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, device=local_rank)
+        brain = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, device=device)
         step = brain.encode_traversal
     brain.build_random_graph(1)
     brain.set_auto_stimulus(0, wl.n_input)
@@ -127,7 +134,7 @@ def main():
 
     def sync():
         brain.synchronize()
-        torch.cuda.synchronize(local_rank)
+        torch.cuda.synchronize(device)
         if dist is not None:
             dist.barrier()
 
@@ -143,10 +150,11 @@ def main():
     gate_ms, launches = brain.kernel_time()
     stats = brain.stats()
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tdev = f"cuda:{device}" if backend == "nccl" else "cpu"
+        t = torch.tensor([dt], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        ev = torch.tensor([stats["events"]], dtype=torch.float64, device=f"cuda:{local_rank}")
+        ev = torch.tensor([stats["events"]], dtype=torch.float64, device=tdev)
         dist.all_reduce(ev, op=dist.ReduceOp.SUM)
         total_events = float(ev.item())
     else:
@@ -188,7 +196,8 @@ def main():
             "config": {
                 "workload": f"{wl.name}: {wl.note}", "n_neuron": wl.n_neuron, "n_syn": wl.n_syn,
                 "events_per_pass_per_gpu": wl.events, "visited_events_per_pass_per_gpu": local_events,
-                "parallelism": f"synapse-shard dp{world}" if world > 1 else "single GPU",
+                "parallelism": (f"synapse-shard dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)"))
+                               if world > 1 else "single GPU",
                 "pre_gated_frac": stats["pre_gated"] / max(1, stats["events"]),
                 "spikes_per_pass": stats["fired"] / max(1, stats["passes"]),
             },

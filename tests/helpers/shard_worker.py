@@ -1,0 +1,54 @@
+"""torchrun worker for tests/test_sharded_gpu.py: every rank runs the product's
+ShardedBrain on its shard (GPU), then an unsharded GPU Brain of the whole graph,
+and checks its shard, lastFired, clock and rBar against it bit-for-bit."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+
+    import abnn_amd
+    from abnn_amd.shard import ShardedBrain, TorchComm
+
+    n_syn, events, passes = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    sb = ShardedBrain(TorchComm(), 256, 256, 30_000, n_syn, events, device=0, track_visits=1)
+    sb.brain.build_random_graph(4)
+    sb.brain.set_auto_stimulus(0, 256)
+    for k in range(passes):
+        if k == 6:
+            sb.brain.set_reward(0.125)
+        sb.step(1)
+    torch.cuda.synchronize()
+    sb.sync_visits()
+    ref = abnn_amd.Brain(256, 256, 30_000, n_syn, events, track_visits=1)
+    ref.build_random_graph(4)
+    ref.set_auto_stimulus(0, 256)
+    for k in range(passes):
+        if k == 6:
+            ref.set_reward(0.125)
+        ref.encode_traversal(1)
+    mine = sb.brain.download_synapses()
+    theirs = ref.download_synapses(sb.lo, sb.hi - sb.lo)
+    ok = bool(np.array_equal(mine.view(np.uint32), theirs.view(np.uint32)))
+    ok &= bool(np.array_equal(sb.brain.last_fired(), ref.last_fired()))
+    ok &= bool(np.array_equal(sb.brain.last_visited(), ref.last_visited()))
+    ok &= sb.brain.scalars() == ref.scalars()
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print("SHARDED_OK" if flag.item() == 1 else "SHARDED_MISMATCH", flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
