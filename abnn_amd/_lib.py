@@ -139,6 +139,23 @@ SIGNATURES = [
 _lib = None
 
 
+def _share_hip_runtime_with_torch() -> None:
+    """PyTorch-ROCm wheels bundle their own libamdhip64/libhsa-runtime64.  If
+    this library pulled in /opt/rocm's copy first, a later `import torch` would
+    load a second HIP runtime into the process and fail to see the GPU.  When
+    torch is installed, preload its runtime (by path, without importing torch)
+    so both resolve libamdhip64.so.7 to the same object whatever the import
+    order; without torch the system ROCm runtime is used."""
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    hip = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        C.CDLL(hip, mode=C.RTLD_GLOBAL)
+
+
 def load() -> C.CDLL:
     """Load libabnn_hip.so (built in-tree); raise if it is missing."""
     global _lib
@@ -148,6 +165,7 @@ def load() -> C.CDLL:
         raise ImportError(
             f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback for the traversal engine)")
+    _share_hip_runtime_with_torch()
     lib = C.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)  # AttributeError = the ABI is not exported

@@ -91,7 +91,7 @@ void free_all(abnn_brain* b)
                     b->d.bitmap,    b->d.filter,     b->d.range_tot,     b->d.range_tile0,
                     b->d.tile_cnt,  b->d.tile_pre,   b->d.g2buf,         b->d.apply_partial,
                     b->d.fired,     b->d.summary,    b->d.work,          b->idx_scratch,
-                    b->u64_scratch,  b->d.tile_range};
+                    b->u64_scratch,  b->d.tile_range,  const_cast<uint4*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : b->events) {
@@ -267,16 +267,20 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     else abnn_default_params(&p);
     REQUIRE(p.max_spikes < (1u << 30), "max_spikes too large");
     const uint64_t E = visited_events(*dims);
-    // Gate kernel shape: threads per workgroup x events per thread (ABNN_GATE="512x8").
-    uint32_t gate_block = 512, gate_k = 8;
+    // Gate kernel shape: threads per workgroup x events per lane x LDS filter
+    // KiB (ABNN_GATE="512x8f64"; tuning knob, the default is the measured best).
+    uint32_t gate_block = 512, gate_k = 8, filter_kib = 64;
     if (const char* env = std::getenv("ABNN_GATE")) {
-        unsigned gb = 0, gk = 0;
-        if (std::sscanf(env, "%ux%u", &gb, &gk) == 2) {
+        unsigned gb = 0, gk = 0, fk = 0;
+        const int got = std::sscanf(env, "%ux%uf%u", &gb, &gk, &fk);
+        if (got >= 2) {
             gate_block = gb;
             gate_k = gk;
+            if (got == 3) filter_kib = fk;
         }
     }
-    REQUIRE(gate_shape_supported(gate_block, gate_k), "unsupported ABNN_GATE shape");
+    const uint32_t filter_words = filter_kib * 256;
+    REQUIRE(gate_shape_supported(gate_block, gate_k, filter_words), "unsupported ABNN_GATE shape");
     const uint64_t iter_events = 64ull * gate_k;  // one wave iteration
     const uint64_t iters = (E + iter_events - 1) / iter_events;
     REQUIRE(iters < 0x7FFFFFFFull, "too many events for one handle");
@@ -319,9 +323,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
         cus = 256;
     // one wave of persistent workgroups: as many as are resident (each keeps the
     // 64 KiB filter in LDS, so at most two per CU)
-    int per_cu = gate_blocks_per_cu(gate_block, gate_k, p.track_visits != 0);
+    int per_cu = gate_blocks_per_cu(gate_block, gate_k, filter_words, p.track_visits != 0);
     if (per_cu <= 0) per_cu = 1;
-    if (per_cu > 2) per_cu = 2;
+    if (per_cu > 4) per_cu = 4;
     uint64_t G = std::min<uint64_t>(iters, std::min<uint64_t>((uint64_t)cus * per_cu, kMaxGateBlocks));
     // ranges are per wave; the last workgroup may own fewer than one iteration each
     const uint64_t waves = gate_block / 64;
@@ -330,7 +334,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.gate_blocks = (uint32_t)G;
     d.n_ranges = (uint32_t)(G * waves);
     d.n_bitmap_words = (uint32_t)(2 * ((n_nrn + 63) / 64));
-    d.filter_exact = d.n_bitmap_words <= (uint32_t)kFilterWords ? 1u : 0u;
+    d.filter_words = filter_words;
+    d.filter_exact = d.n_bitmap_words <= filter_words ? 1u : 0u;
     abnn_status s;
     // build_buffers, brain.cpp:52-69: allocate and zero every buffer.
     if ((s = dalloc(&d.syn, dims->n_syn)) != ABNN_OK) return fail(s);
@@ -343,7 +348,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.reward = reinterpret_cast<float*>(sb + 1);
     d.rbar = d.reward + 1;
     if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.filter, kFilterWords)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.filter, kMaxFilterWords)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_tot, d.n_ranges)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_tile0, d.n_ranges)) != ABNN_OK) return fail(s);
     const uint64_t max_tiles = E / kApplyBlock + d.n_ranges + 1;
@@ -351,6 +356,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.tile_range, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.tile_pre, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.g2buf, iters * iter_events)) != ABNN_OK) return fail(s);
+    uint4* dummy = nullptr;
+    if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
+    d.dummy = dummy;
     if ((s = dalloc(&d.apply_partial, kApplyGrid)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.fired, p.max_spikes + 1u)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.summary, ABNN_SUMMARY_WORDS)) != ABNN_OK) return fail(s);

@@ -11,13 +11,14 @@
 namespace abnn {
 
 // Pre-spike filter kept in LDS by every gate workgroup: the exact recent-spike
-// bitmap folded modulo kFilterWords 32-bit words (512 Ki bits = 64 KiB).  When
-// the bitmap itself fits (N_NRN <= 512 Ki) the filter IS the bitmap.
-constexpr int kFilterWords = 16384;
+// bitmap folded modulo filter_words 32-bit words (16384 words = 512 Ki bits =
+// 64 KiB by default).  When the bitmap itself fits, the filter IS the bitmap.
+constexpr int kMaxFilterWords = 16384;
 constexpr int kApplyBlock = 256;   // one tile = 256 consecutive pre-gated events of a range
 constexpr int kApplyGrid = 1024;   // persistent grid of the apply kernel
 constexpr int kScanThreads = 1024; // the range scan is one workgroup
 constexpr int kMaxGateBlocks = 1024;
+constexpr int kDummyRecords = 64 * 16;  // >= 64 lanes x max events per lane
 
 // Per-pass bookkeeping in device memory (one per handle).
 struct alignas(16) PassWork {
@@ -38,13 +39,14 @@ struct DeviceState {
     float* reward;            // [1]
     float* rbar;              // [1]
     uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
-    uint32_t* filter;         // [kFilterWords] folded bitmap
+    uint32_t* filter;         // [filter_words] folded bitmap
     uint4* range_tot;         // [n_ranges] {pre-gated entries, 0, 0, 0}
     uint32_t* range_tile0;    // [n_ranges] first entry tile of each range
     uint32_t* tile_range;     // [max_tiles] range of each tile
     uint2* tile_cnt;          // [max_tiles] {candidates, passed refractory} per tile
     uint32_t* tile_pre;       // [max_tiles] exclusive candidate prefix (capped; = budget: skip)
     uint4* g2buf;             // [iters * iter_events] gated entries, per-range regions
+    const uint4* dummy;       // [kDummyRecords] zero records: target of masked-off stream loads
     uint2* apply_partial;     // [kApplyGrid] {updated, fired} per apply workgroup
     int32_t* fired;           // [max_spikes] internal spike list (world = 1)
     int64_t* summary;         // [ABNN_SUMMARY_WORDS] internal (world = 1)
@@ -54,6 +56,7 @@ struct DeviceState {
     uint64_t events;          // visited events per pass (local)
     uint64_t syn_offset;
     uint32_t n_bitmap_words;  // 2 * ceil(n_nrn / 64)
+    uint32_t filter_words;    // LDS filter size (a power of two, compiled per gate shape)
     uint32_t filter_exact;    // bitmap fits the filter: no global confirmation
     uint32_t gate_blocks;     // persistent gate workgroups G
     uint32_t n_ranges;        // G * waves per workgroup: one contiguous range per wave
@@ -73,9 +76,9 @@ struct KernelParams {
 KernelParams to_kernel_params(const abnn_params& p);
 
 // Gate kernel shapes compiled in (threads per workgroup x events per thread).
-bool gate_shape_supported(uint32_t block, uint32_t k);
+bool gate_shape_supported(uint32_t block, uint32_t k, uint32_t filter_words);
 // Resident gate workgroups per CU for a shape (occupancy API; 0 on failure).
-int gate_blocks_per_cu(uint32_t block, uint32_t k, bool track);
+int gate_blocks_per_cu(uint32_t block, uint32_t k, uint32_t filter_words, bool track);
 
 // Launchers (all asynchronous on `s`).
 hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,

@@ -199,13 +199,13 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
     }
 }
 
-// k_fold: filter[j] = OR over m of bitmap[j + m * kFilterWords].
+// k_fold: filter[j] = OR over m of bitmap[j + m * filter_words].
 __global__ __launch_bounds__(256) void k_fold(DeviceState d)
 {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= (uint32_t)kFilterWords) return;
+    if (j >= d.filter_words) return;
     uint32_t v = 0;
-    for (uint32_t w = j; w < d.n_bitmap_words; w += kFilterWords) v |= d.bitmap[w];
+    for (uint32_t w = j; w < d.n_bitmap_words; w += d.filter_words) v |= d.bitmap[w];
     d.filter[j] = v;
 }
 
@@ -217,14 +217,19 @@ __global__ __launch_bounds__(256) void k_fold(DeviceState d)
 // in steady state) are staged in event order in the wave's LDS slab and
 // written out as whole-wave coalesced stores, so stores rarely sit between the
 // prefetch and its wait (vmcnt retires in issue order, stores included).
-template <int BLOCK, int K, bool kTrack>
+template <int BLOCK, int K, int FW, bool kTrack>
 __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
     constexpr int NW = BLOCK / 64;
     constexpr uint32_t IE = 64 * K;
+#ifdef ABNN_EXP_BIG_STAGE
+    constexpr uint32_t kStage = (80 * 1024 - FW * 4) / NW / 16;  // LDS left beside the filter
+    constexpr uint32_t kFlushAt = kStage - 64;   // one k-step adds at most 64
+#else
     constexpr uint32_t kFlushAt = 32;            // staged entries before a flush
     constexpr uint32_t kStage = kFlushAt + 64;   // one k-step adds at most 64
-    __shared__ uint32_t s_filter[kFilterWords];
+#endif
+    __shared__ uint32_t s_filter[FW];
     __shared__ uint4 s_stage[NW][kStage];
 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -238,31 +243,45 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     {
         const uint4* src = reinterpret_cast<const uint4*>(d.filter);
         uint4* dst = reinterpret_cast<uint4*>(s_filter);
-        for (int i = tid; i < kFilterWords / 4; i += BLOCK) dst[i] = src[i];
+        for (int i = tid; i < FW / 4; i += BLOCK) dst[i] = src[i];
     }
 
+    // Every issue is exactly K loads, straight-line: lanes past the sweep and
+    // the prefetch after a range's last iteration read the small L2-resident
+    // dummy block instead.  A branch that could issue fewer loads makes the
+    // compiler's vmcnt bookkeeping assume none, and the wait for the filter
+    // confirmations below would then also wait for this prefetch.
     uint4 nxt[K];
-    auto issue = [&](uint64_t it) {
+    auto issue = [&](uint64_t it, bool live) {
         const uint64_t base = it * IE;
-        if (base + IE <= d.events) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) nxt[k] = load_stream16(d.syn + base + k * 64 + lane);
-        } else {
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const uint64_t t = base + k * 64 + lane;
-                nxt[k] = t < d.events ? load_stream16(d.syn + t) : make_uint4(0u, 0u, 0u, 0u);
-            }
+        for (int k = 0; k < K; ++k) {
+            const uint64_t t = base + k * 64 + lane;
+            const uint4* p = (live && t < d.events) ? d.syn + t : d.dummy + (k * 64 + lane);
+            nxt[k] = load_stream16(p);
         }
     };
-    if (it_begin < it_end) issue(it_begin);
+    issue(it_begin, it_begin < it_end);
     __syncthreads();
 
     const uint32_t nn = (uint32_t)d.n_nrn;  // N_NRN < 2^32 (checked at create)
     uint32_t pend = 0, flushed = 0;
+#ifdef ABNN_EXP_FAKE_FLUSH
+    uint32_t exp_acc = 0;
+#endif
     auto flush = [&]() {  // wave-uniform: write the staged entries, in order
-        if (lane < pend) d.g2buf[region + flushed + lane] = stage[lane];
-        if (lane + 64 < pend) d.g2buf[region + flushed + 64 + lane] = stage[64 + lane];
+#if defined(ABNN_EXP_FAKE_FLUSH)
+        if (lane < pend) exp_acc ^= stage[lane].x;
+        if (lane + 64 < pend) exp_acc ^= stage[64 + lane].y;
+#elif !defined(ABNN_EXP_NO_FLUSH)
+        // non-temporal: plain stores keep these lines in L2 beside the record
+        // stream and cost ~22 us per pass at config 3 (tools/exp_variants.py)
+        for (uint32_t q = lane; q < pend; q += 64) {
+            const uint4 v = stage[q];
+            __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
+                                        reinterpret_cast<u32x4_t*>(d.g2buf + region + flushed + q));
+        }
+#endif
         flushed += pend;
         pend = 0;
     };
@@ -284,7 +303,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // bounds), no branches.
         uint32_t fw[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) fw[k] = s_filter[(rec[k].x >> 5) & (kFilterWords - 1)];
+        for (int k = 0; k < K; ++k) fw[k] = s_filter[(rec[k].x >> 5) & (FW - 1)];
         uint32_t fm = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -298,27 +317,46 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             cw[k] = 0xFFFFFFFFu;
+#ifndef ABNN_EXP_NO_CONFIRM
             if (!exact && ((fm >> k) & 1u)) cw[k] = d.bitmap[rec[k].x >> 5];
+#endif
         }
-        if (it + 1 < it_end) issue(it + 1);  // next iteration's records in flight
+        issue(it + 1, it + 1 < it_end);  // next iteration's records in flight
+        // keep every prefetch load ahead of the first use of a confirmation
+        // (otherwise the scheduler interleaves them and waits mid-prefetch)
+        __builtin_amdgcn_sched_barrier(0);
 
         if (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 if (((vmask >> k) & 1u) && rec[k].y < nn) d.last_visited[rec[k].y] = now;
         }
+        uint32_t g1m = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            g1m |= ((((fm >> k) & 1u) && ((cw[k] >> (rec[k].x & 31u)) & 1u)) ? 1u : 0u) << k;
+        if (__ballot(g1m != 0) == 0) continue;  // ~half the wave-iterations: nothing to stage
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const bool g1 = ((fm >> k) & 1u) && ((cw[k] >> (rec[k].x & 31u)) & 1u);
+            const bool g1 = (g1m >> k) & 1u;
             const uint64_t b1 = __ballot(g1);
+#ifndef ABNN_EXP_NO_STAGE
             if (g1)
                 stage[pend + mbcnt64(b1)] =
                     make_uint4((uint32_t)(base - region) + k * 64 + lane, rec[k].y, rec[k].z, 0u);
+#endif
             pend += (uint32_t)__popcll(b1);
             if (pend >= kFlushAt) flush();
         }
     }
     flush();
+#ifdef ABNN_EXP_FAKE_FLUSH
+    if (exp_acc == 0x12345677u) d.range_tot[r].w = exp_acc;
+#endif
+#if defined(ABNN_EXP_NO_FLUSH) || defined(ABNN_EXP_FAKE_FLUSH) || defined(ABNN_EXP_NO_STAGE) || \
+    defined(ABNN_EXP_NO_CONFIRM)
+    flushed = 0;  // timing-only builds: nothing downstream may read their entries
+#endif
     if (lane == 0) d.range_tot[r] = make_uint4(flushed, 0u, 0u, 0u);
 }
 
@@ -614,44 +652,58 @@ __global__ __launch_bounds__(256) void k_stamp_list(DeviceState d, const uint32_
 
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
-template <int BLOCK, int K>
+template <int BLOCK, int K, int FW>
 hipError_t launch_gate_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
 {
     if (kp.track_visits)
-        hipLaunchKernelGGL((k_gate<BLOCK, K, true>), dim3(d.gate_blocks), dim3(BLOCK), 0, s, d, kp);
+        hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true>), dim3(d.gate_blocks), dim3(BLOCK), 0, s, d, kp);
     else
-        hipLaunchKernelGGL((k_gate<BLOCK, K, false>), dim3(d.gate_blocks), dim3(BLOCK), 0, s, d, kp);
+        hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false>), dim3(d.gate_blocks), dim3(BLOCK), 0, s, d, kp);
     return hipGetLastError();
 }
 
-}  // namespace
-
-template <int BLOCK, int K>
+template <int BLOCK, int K, int FW>
 int occupancy_shape(bool track)
 {
     int n = 0;
-    hipError_t e = track ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, true>, BLOCK, 0)
-                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, false>, BLOCK, 0);
+    hipError_t e = track ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true>, BLOCK, 0)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false>, BLOCK, 0);
     return e == hipSuccess ? n : 0;
 }
 
-int gate_blocks_per_cu(uint32_t block, uint32_t k, bool track)
+// Compiled gate shapes: threads per workgroup x events per lane x filter words.
+#define ABNN_GATE_SHAPES(X) \
+    X(512, 8, 16384)        \
+    X(512, 4, 16384)        \
+    X(1024, 4, 16384)       \
+    X(1024, 4, 8192)        \
+    X(1024, 8, 8192)        \
+    X(512, 4, 8192)         \
+    X(256, 8, 8192)         \
+    X(256, 16, 16384)
+
+constexpr uint64_t shape_key(uint32_t b, uint32_t k, uint32_t fw) { return ((uint64_t)b << 40) | ((uint64_t)k << 32) | fw; }
+
+}  // namespace
+
+int gate_blocks_per_cu(uint32_t block, uint32_t k, uint32_t fw, bool track)
 {
-    switch (block * 100 + k) {
-        case 25608: return occupancy_shape<256, 8>(track);
-        case 25616: return occupancy_shape<256, 16>(track);
-        case 51204: return occupancy_shape<512, 4>(track);
-        case 51208: return occupancy_shape<512, 8>(track);
-        case 102404: return occupancy_shape<1024, 4>(track);
-        case 102408: return occupancy_shape<1024, 8>(track);
+    switch (shape_key(block, k, fw)) {
+#define X(B, K, F) case shape_key(B, K, F): return occupancy_shape<B, K, F>(track);
+        ABNN_GATE_SHAPES(X)
+#undef X
     }
     return 0;
 }
 
-bool gate_shape_supported(uint32_t block, uint32_t k)
+bool gate_shape_supported(uint32_t block, uint32_t k, uint32_t fw)
 {
-    return (block == 256 && (k == 8 || k == 16)) || (block == 512 && (k == 4 || k == 8)) ||
-           (block == 1024 && (k == 4 || k == 8));
+    switch (shape_key(block, k, fw)) {
+#define X(B, K, F) case shape_key(B, K, F): return true;
+        ABNN_GATE_SHAPES(X)
+#undef X
+    }
+    return false;
 }
 
 hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,
@@ -662,7 +714,7 @@ hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t 
                        stim_first, stim_count);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_fold, dim3(kFilterWords / 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_fold, dim3((d.filter_words + 255) / 256), dim3(256), 0, s, d);
     return hipGetLastError();
 }
 
@@ -678,13 +730,10 @@ hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream
 hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s)
 {
     if (d.gate_blocks == 0) return hipSuccess;
-    switch (d.gate_block * 100 + d.gate_k) {
-        case 25608: return launch_gate_shape<256, 8>(d, kp, s);
-        case 25616: return launch_gate_shape<256, 16>(d, kp, s);
-        case 51204: return launch_gate_shape<512, 4>(d, kp, s);
-        case 51208: return launch_gate_shape<512, 8>(d, kp, s);
-        case 102404: return launch_gate_shape<1024, 4>(d, kp, s);
-        case 102408: return launch_gate_shape<1024, 8>(d, kp, s);
+    switch (shape_key(d.gate_block, d.gate_k, d.filter_words)) {
+#define X(B, K, F) case shape_key(B, K, F): return launch_gate_shape<B, K, F>(d, kp, s);
+        ABNN_GATE_SHAPES(X)
+#undef X
     }
     return hipErrorInvalidValue;
 }
