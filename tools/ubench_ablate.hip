@@ -41,7 +41,7 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-enum { F_FILTER = 1, F_CONFIRM = 2, F_GATHER = 4, F_STORE = 8 };
+enum { F_FILTER = 1, F_CONFIRM = 2, F_GATHER = 4, F_STORE = 8, F_STAGE = 16, F_PLAIN = 32, F_SKIP = 64 };
 
 template <int BLOCK, int K, int FLAGS, int PF>
 __global__ __launch_bounds__(BLOCK) void k_var(const uint4* syn, uint64_t events, uint32_t iters,
@@ -124,6 +124,177 @@ __global__ __launch_bounds__(BLOCK) void k_var(const uint4* syn, uint64_t events
     if (acc == 0x9876543u) tot[r] = acc;
 }
 
+// Production-structure loop: straight-line K-load prefetch (dummy block for
+// masked lanes), LDS filter, L2 confirm before the prefetch, sched barrier,
+// pre-gated events staged in LDS and flushed with nt (or plain) stores.
+template <int BLOCK, int K, int FLAGS>
+__global__ __launch_bounds__(BLOCK) void k_prod(const uint4* syn, uint64_t events, uint32_t iters,
+                                                const uint32_t* bitmap, const uint32_t* filt,
+                                                const uint4* dummy, uint4* out, uint32_t* tot)
+{
+    constexpr int NW = BLOCK / 64;
+    constexpr uint32_t IE = 64 * K;
+    constexpr uint32_t kFlushAt = 32, kStage = 96;
+    __shared__ uint32_t s_filter[FW];
+    __shared__ uint4 s_stage[NW][kStage];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
+    const uint64_t itb = (uint64_t)r * iters / NR, ite = (uint64_t)(r + 1) * iters / NR;
+    const uint64_t region = itb * IE;
+    uint4* stage = s_stage[wid];
+    for (int i = tid; i < FW / 4; i += BLOCK)
+        reinterpret_cast<uint4*>(s_filter)[i] = reinterpret_cast<const uint4*>(filt)[i];
+    uint4 nxt[K];
+    auto issue = [&](uint64_t it, bool live) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t t = it * IE + k * 64 + lane;
+            nxt[k] = ldnt((live && t < events) ? syn + t : dummy + (k * 64 + lane));
+        }
+    };
+    issue(itb, itb < ite);
+    __syncthreads();
+    uint32_t pend = 0, flushed = 0;
+    auto flush = [&]() {
+        for (uint32_t q = lane; q < pend; q += 64) {
+            const uint4 v = stage[q];
+            if (FLAGS & F_PLAIN) out[region + flushed + q] = v;
+            else __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(out + region + flushed + q));
+        }
+        flushed += pend;
+        pend = 0;
+    };
+    for (uint64_t it = itb; it < ite; ++it) {
+        uint4 rec[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) rec[k] = nxt[k];
+        const uint64_t base = it * IE;
+        uint32_t fw[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) fw[k] = s_filter[(rec[k].x >> 5) & (FW - 1)];
+        uint32_t fm = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) fm |= ((fw[k] >> (rec[k].x & 31u)) & 1u) << k;
+        uint32_t cw[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            cw[k] = 0xFFFFFFFFu;
+            if ((fm >> k) & 1u) cw[k] = bitmap[rec[k].x >> 5];
+        }
+        issue(it + 1, it + 1 < ite);
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t g1m = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) g1m |= ((((fm >> k) & 1u) && ((cw[k] >> (rec[k].x & 31u)) & 1u)) ? 1u : 0u) << k;
+        if (FLAGS & F_SKIP) {
+            if (__ballot(g1m != 0) == 0) continue;
+        }
+        if (FLAGS & F_STAGE) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool g1 = (g1m >> k) & 1u;
+                const uint64_t b1 = __ballot(g1);
+                if (g1) stage[pend + mbcnt64(b1)] = make_uint4((uint32_t)(base - region) + k * 64 + lane, rec[k].y, rec[k].z, 0u);
+                pend += (uint32_t)__popcll(b1);
+                if (pend >= kFlushAt) flush();
+            }
+        } else {
+            pend += __popc(g1m);
+        }
+    }
+    if (FLAGS & F_STAGE) flush();
+    if (lane == 0) tot[r] = flushed + pend;
+}
+
+// Software-pipelined production loop: iteration i waits once (record block i
+// and the confirmations of i-1 both landed), issues the prefetch of i+1
+// immediately, stages iteration i-1's pre-gated events, then runs the filter
+// of i and issues its confirmations.
+template <int BLOCK, int K, int FLAGS>
+__global__ __launch_bounds__(BLOCK) void k_pipe(const uint4* syn, uint64_t events, uint32_t iters,
+                                                const uint32_t* bitmap, const uint32_t* filt,
+                                                const uint4* dummy, uint4* out, uint32_t* tot)
+{
+    constexpr int NW = BLOCK / 64;
+    constexpr uint32_t IE = 64 * K;
+    constexpr uint32_t kFlushAt = 32, kStage = 96;
+    __shared__ uint32_t s_filter[FW];
+    __shared__ uint4 s_stage[NW][kStage];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
+    const uint64_t itb = (uint64_t)r * iters / NR, ite = (uint64_t)(r + 1) * iters / NR;
+    const uint64_t region = itb * IE;
+    uint4* stage = s_stage[wid];
+    for (int i = tid; i < FW / 4; i += BLOCK)
+        reinterpret_cast<uint4*>(s_filter)[i] = reinterpret_cast<const uint4*>(filt)[i];
+    uint4 nxt[K];
+    auto issue = [&](uint64_t it, bool live) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t t = it * IE + k * 64 + lane;
+            nxt[k] = ldnt((live && t < events) ? syn + t : dummy + (k * 64 + lane));
+        }
+    };
+    issue(itb, itb < ite);
+    __syncthreads();
+    uint32_t pend = 0, flushed = 0;
+    auto flush = [&]() {
+        for (uint32_t q = lane; q < pend; q += 64) {
+            const uint4 v = stage[q];
+            __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(out + region + flushed + q));
+        }
+        flushed += pend;
+        pend = 0;
+    };
+    // carried from the previous iteration: filter hits, confirmation words, record fields
+    uint32_t pfm = 0, pcw[K], px[K], py[K], pz[K];
+    uint64_t pbase = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) pcw[k] = px[k] = py[k] = pz[k] = 0;
+    for (uint64_t it = itb; it <= ite; ++it) {
+        uint4 rec[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) rec[k] = nxt[k];   // waits: records of it + confirmations of it-1
+        const bool live = it < ite;
+        issue(it + 1, it + 1 < ite);                    // prefetch right away
+        __builtin_amdgcn_sched_barrier(0);
+        // stage iteration it-1
+        uint32_t g1m = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) g1m |= ((((pfm >> k) & 1u) && ((pcw[k] >> (px[k] & 31u)) & 1u)) ? 1u : 0u) << k;
+        if (__ballot(g1m != 0) != 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool g1 = (g1m >> k) & 1u;
+                const uint64_t b1 = __ballot(g1);
+                if (g1) stage[pend + mbcnt64(b1)] = make_uint4((uint32_t)(pbase - region) + k * 64 + lane, py[k], pz[k], 0u);
+                pend += (uint32_t)__popcll(b1);
+                if (pend >= kFlushAt) flush();
+            }
+        }
+        if (!live) break;
+        // filter of it, confirmations issued (consumed next iteration)
+        uint32_t fm = 0;
+        uint32_t fw[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) fw[k] = s_filter[(rec[k].x >> 5) & (FW - 1)];
+#pragma unroll
+        for (int k = 0; k < K; ++k) fm |= ((fw[k] >> (rec[k].x & 31u)) & 1u) << k;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            pcw[k] = 0xFFFFFFFFu;
+            if ((fm >> k) & 1u) pcw[k] = bitmap[rec[k].x >> 5];
+            px[k] = rec[k].x;
+            py[k] = rec[k].y;
+            pz[k] = rec[k].z;
+        }
+        pfm = fm;
+        pbase = it * IE;
+    }
+    flush();
+    if (lane == 0) tot[r] = flushed;
+}
+
 __global__ void k_fill(uint4* syn, uint64_t n, uint32_t n_nrn)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
@@ -134,6 +305,24 @@ __global__ void k_fill(uint4* syn, uint64_t n, uint32_t n_nrn)
         syn[i] = make_uint4(512 + (uint32_t)(((z >> 32) * (n_nrn - 512)) >> 32),
                             512 + (uint32_t)(((z & 0xffffffffu) * (n_nrn - 512)) >> 32), 0x3e000000u, 0u);
     }
+}
+
+template <int BLOCK, int K, int FLAGS>
+void launch_prod(int grid, const uint4* syn, uint64_t ev, uint32_t iters, const uint32_t* bm,
+                 const uint32_t* f, const uint64_t* lf, uint4* out, uint32_t* tot, uint64_t now)
+{
+    (void)lf; (void)now;
+    hipLaunchKernelGGL((k_prod<BLOCK, K, FLAGS>), dim3(grid), dim3(BLOCK), 0, 0, syn, ev, iters, bm, f,
+                       out + ev, out, tot);
+}
+
+template <int BLOCK, int K, int FLAGS>
+void launch_pipe(int grid, const uint4* syn, uint64_t ev, uint32_t iters, const uint32_t* bm,
+                 const uint32_t* f, const uint64_t* lf, uint4* out, uint32_t* tot, uint64_t now)
+{
+    (void)lf; (void)now;
+    hipLaunchKernelGGL((k_pipe<BLOCK, K, FLAGS>), dim3(grid), dim3(BLOCK), 0, 0, syn, ev, iters, bm, f,
+                       out + ev, out, tot);
 }
 
 struct Var {
@@ -152,6 +341,8 @@ void launch_var(int grid, const uint4* syn, uint64_t ev, uint32_t iters, const u
 }
 
 #define V(B, K, FL, PF, NAME) Var{NAME, launch_var<B, K, FL, PF>, B, K}
+#define P(B, K, FL, NAME) Var{NAME, launch_prod<B, K, FL>, B, K}
+#define Q(B, K, FL, NAME) Var{NAME, launch_pipe<B, K, FL>, B, K}
 
 int main()
 {
@@ -162,7 +353,8 @@ int main()
     uint32_t *bm, *filt, *tot;
     uint64_t* lastF;
     CK(hipMalloc(&syn, n * 16));
-    CK(hipMalloc(&out, n * 16));
+    CK(hipMalloc(&out, n * 16 + 65536));
+    CK(hipMemset(out, 0, n * 16 + 65536));
     CK(hipMalloc(&bm, nwords * 4 + 64));
     CK(hipMalloc(&filt, FW * 4));
     CK(hipMalloc(&tot, 1 << 20));
@@ -188,18 +380,14 @@ int main()
 
     std::vector<Var> vars = {
         V(512, 8, 0, 1, "512x8 stream pf1"),
-        V(512, 8, 0, 2, "512x8 stream pf2"),
-        V(512, 8, F_FILTER, 1, "512x8 +filter pf1"),
-        V(512, 8, F_FILTER, 2, "512x8 +filter pf2"),
-        V(512, 8, F_FILTER | F_CONFIRM, 1, "512x8 +confirm pf1"),
-        V(512, 8, F_FILTER | F_CONFIRM | F_GATHER, 1, "512x8 +gather pf1"),
-        V(512, 8, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 1, "512x8 full pf1"),
-        V(512, 8, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 2, "512x8 full pf2"),
-        V(512, 4, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 1, "512x4 full pf1"),
-        V(512, 4, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 2, "512x4 full pf2"),
-        V(1024, 4, F_FILTER | F_CONFIRM | F_GATHER | F_STORE, 2, "1024x4 full pf2"),
-        V(1024, 4, F_FILTER, 2, "1024x4 +filter pf2"),
-        V(512, 4, F_FILTER | F_STORE, 2, "512x4 filter+store pf2"),
+        V(256, 8, 0, 1, "256x8 stream pf1"),
+        P(512, 8, F_STAGE | F_SKIP, "prod 512x8"),
+        P(256, 8, F_STAGE | F_SKIP, "prod 256x8"),
+        P(256, 16, F_STAGE | F_SKIP, "prod 256x16"),
+        Q(256, 8, 0, "pipe 256x8"),
+        Q(256, 16, 0, "pipe 256x16"),
+        Q(256, 4, 0, "pipe 256x4"),
+        Q(256, 8, 0, "pipe 256x8 again"),
     };
     int cus = 256;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
