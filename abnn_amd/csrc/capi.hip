@@ -88,8 +88,8 @@ void free_all(abnn_brain* b)
     if (!b) return;
     (void)hipSetDevice(b->device);
     void* ptrs[] = {b->d.syn,       b->d.last_fired, b->d.last_visited,  b->scalar_block,
-                    b->d.bitmap,    b->d.filter,     b->d.range_tot,     b->d.range_tile0,
-                    b->d.tile_cnt,  b->d.tile_pre,   b->d.g2buf,         b->d.apply_partial,
+                    b->d.bitmap,    b->d.filter,     b->d.range_cnt,     b->d.range_tile0,
+                    b->d.tile_mask, b->d.tile_pre,   b->d.g2buf,         b->d.apply_partial,
                     b->d.fired,     b->d.summary,    b->d.work,          b->idx_scratch,
                     b->u64_scratch,  b->d.tile_range,  const_cast<uint4*>(b->d.dummy)};
     for (void* p : ptrs)
@@ -284,6 +284,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     const uint64_t iter_events = 64ull * gate_k;  // one wave iteration
     const uint64_t iters = (E + iter_events - 1) / iter_events;
     REQUIRE(iters < 0x7FFFFFFFull, "too many events for one handle");
+    REQUIRE(E / kTile + (uint64_t)kMaxRanges < 0xFFFFFFFFull, "too many events for one handle");
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -332,7 +333,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     G = std::min<uint64_t>(G, (iters + waves - 1) / waves);
     if (G == 0 && iters > 0) G = 1;
     d.gate_blocks = (uint32_t)G;
-    d.n_ranges = (uint32_t)(G * waves);
+    d.n_ranges = (uint32_t)(G * waves);  // <= kMaxGateBlocks * 16 = kMaxRanges
     d.n_bitmap_words = (uint32_t)(2 * ((n_nrn + 63) / 64));
     d.filter_words = filter_words;
     d.filter_exact = d.n_bitmap_words <= filter_words ? 1u : 0u;
@@ -349,17 +350,17 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.rbar = d.reward + 1;
     if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.filter, kMaxFilterWords)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.range_tot, d.n_ranges)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.range_cnt, d.n_ranges)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_tile0, d.n_ranges)) != ABNN_OK) return fail(s);
-    const uint64_t max_tiles = E / kApplyBlock + d.n_ranges + 1;
-    if ((s = dalloc(&d.tile_cnt, max_tiles)) != ABNN_OK) return fail(s);
+    const uint64_t max_tiles = E / kTile + d.n_ranges + 1;
+    if ((s = dalloc(&d.tile_mask, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.tile_range, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.tile_pre, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.g2buf, iters * iter_events)) != ABNN_OK) return fail(s);
     uint4* dummy = nullptr;
     if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
     d.dummy = dummy;
-    if ((s = dalloc(&d.apply_partial, kApplyGrid)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.apply_partial, kTileBlocks)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.fired, p.max_spikes + 1u)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.summary, ABNN_SUMMARY_WORDS)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);

@@ -14,10 +14,12 @@ namespace abnn {
 // bitmap folded modulo filter_words 32-bit words (16384 words = 512 Ki bits =
 // 64 KiB by default).  When the bitmap itself fits, the filter IS the bitmap.
 constexpr int kMaxFilterWords = 16384;
-constexpr int kApplyBlock = 256;   // one tile = 256 consecutive pre-gated events of a range
-constexpr int kApplyGrid = 1024;   // persistent grid of the apply kernel
-constexpr int kScanThreads = 1024; // the range scan is one workgroup
+constexpr int kTile = 64;          // one tile = 64 consecutive pre-gated events of a range = one wave
+constexpr int kTileBlocks = 2048;  // grid of the tile kernels (x 4 waves = 8192 waves, all resident)
+constexpr int kScanThreads = 1024; // the range and tile scans are one workgroup each
 constexpr int kMaxGateBlocks = 1024;
+constexpr int kMaxRanges = 16384;
+static_assert(kTileBlocks % kScanThreads == 0, "k_finalize sums the apply partials in whole rounds");  // kMaxGateBlocks x up to 16 waves; staged whole in LDS by k_tiles
 constexpr int kDummyRecords = 64 * 16;  // >= 64 lanes x max events per lane
 
 // Per-pass bookkeeping in device memory (one per handle).
@@ -40,14 +42,14 @@ struct DeviceState {
     float* rbar;              // [1]
     uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
     uint32_t* filter;         // [filter_words] folded bitmap
-    uint4* range_tot;         // [n_ranges] {pre-gated entries, 0, 0, 0}
+    uint32_t* range_cnt;      // [n_ranges] pre-gated entries of each range
     uint32_t* range_tile0;    // [n_ranges] first entry tile of each range
     uint32_t* tile_range;     // [max_tiles] range of each tile
-    uint2* tile_cnt;          // [max_tiles] {candidates, passed refractory} per tile
+    uint4* tile_mask;         // [max_tiles] {passed refractory, spike candidate} lane masks (2 x u64)
     uint32_t* tile_pre;       // [max_tiles] exclusive candidate prefix (capped; = budget: skip)
-    uint4* g2buf;             // [iters * iter_events] gated entries, per-range regions
+    uint4* g2buf;             // [iters * iter_events] gated entries {event - region, dst, w, isi}
     const uint4* dummy;       // [kDummyRecords] zero records: target of masked-off stream loads
-    uint2* apply_partial;     // [kApplyGrid] {updated, fired} per apply workgroup
+    uint2* apply_partial;     // [kTileBlocks] {updated, fired} per apply workgroup
     int32_t* fired;           // [max_spikes] internal spike list (world = 1)
     int64_t* summary;         // [ABNN_SUMMARY_WORDS] internal (world = 1)
     PassWork* work;

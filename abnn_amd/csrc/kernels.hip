@@ -5,9 +5,9 @@
 // each doing one HBM-friendly thing:
 //
 //   k_bitmap   : lastFired (u64, 8 B/neuron, read once) -> exact recent-spike
-//                bitmap, bit i = (now - lastFired[i]) <= WINDOW_PRE; the
+//                bitmap, bit i = (now - lastFired[i]) <= WINDOW_PRE, OR-folded
+//                modulo 512 Ki bits into the 64 KiB pre-spike filter; the
 //                per-pass stimulus stamp is fused here.
-//   k_fold     : bitmap folded modulo 512 Ki bits -> the 64 KiB pre-spike filter.
 //   k_gate     : THE streaming kernel.  Persistent workgroups whose waves each
 //                sweep one contiguous range of events with non-temporal dwordx4 loads of
 //                the 16-B SynapsePacked records (1 KiB per wave-instruction,
@@ -194,19 +194,15 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
             bit = (now - L[q]) <= (uint64_t)kp.window_pre;
         }
         const uint64_t m = __ballot(bit);
-        if (lane == 0 && (wave * 4 + q) * 64 < d.n_nrn)
+        if (lane == 0 && (wave * 4 + q) * 64 < d.n_nrn) {
             reinterpret_cast<uint64_t*>(d.bitmap)[wave * 4 + q] = m;
+            // fold into the LDS filter image: filter[j] |= bitmap[j + m * filter_words]
+            // (zeroed by k_refrac of the previous pass; few words are non-zero)
+            const uint32_t w0 = (uint32_t)(wave * 4 + q) * 2u, fm = d.filter_words - 1u;
+            if ((uint32_t)m) atomicOr(d.filter + (w0 & fm), (uint32_t)m);
+            if ((uint32_t)(m >> 32)) atomicOr(d.filter + ((w0 + 1u) & fm), (uint32_t)(m >> 32));
+        }
     }
-}
-
-// k_fold: filter[j] = OR over m of bitmap[j + m * filter_words].
-__global__ __launch_bounds__(256) void k_fold(DeviceState d)
-{
-    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= d.filter_words) return;
-    uint32_t v = 0;
-    for (uint32_t w = j; w < d.n_bitmap_words; w += d.filter_words) v |= d.bitmap[w];
-    d.filter[j] = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -351,129 +347,171 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     }
     flush();
 #ifdef ABNN_EXP_FAKE_FLUSH
-    if (exp_acc == 0x12345677u) d.range_tot[r].w = exp_acc;
+    if (exp_acc == 0x12345677u) d.tile_pre[r] = exp_acc;
 #endif
 #if defined(ABNN_EXP_NO_FLUSH) || defined(ABNN_EXP_FAKE_FLUSH) || defined(ABNN_EXP_NO_STAGE) || \
     defined(ABNN_EXP_NO_CONFIRM)
     flushed = 0;  // timing-only builds: nothing downstream may read their entries
 #endif
-    if (lane == 0) d.range_tot[r] = make_uint4(flushed, 0u, 0u, 0u);
+    if (lane == 0) d.range_cnt[r] = flushed;
 }
 
 // ---------------------------------------------------------------------------
-// Pre-gated entries are processed as tiles of kApplyBlock consecutive entries
-// of one range; tile order = event order; tile_range[t] names the range.
-// k_tiles: one workgroup: first tile of every range and the tile -> range map.
+// Pre-gated entries are processed as tiles of kTile (= 64 = one wave)
+// consecutive entries of one range; tile order = event order; tile_range[t]
+// names the range.  These kernels move a few MB per pass: they are bound by
+// dependent-load latency, so every loop below keeps all of a thread's loads
+// in flight at once and no tile waits on another.
+//
+// k_tiles: one workgroup: first tile of every range, the tile -> range map and
+// the pre-gated total.  All range counts are staged in LDS first.
 __global__ __launch_bounds__(kScanThreads) void k_tiles(DeviceState d)
 {
-    __shared__ uint64_t s_wave[kScanThreads / 64];
+    constexpr uint32_t kPer = kMaxRanges / kScanThreads;  // ranges per thread
+    constexpr uint32_t kBig = 256;                        // ranges filled by the whole workgroup
+    __shared__ uint32_t s_cnt[kMaxRanges];
+    __shared__ uint64_t s_wave[kScanThreads / 64], s_red[kScanThreads / 64];
+    __shared__ uint32_t s_big[kBig], s_big_t0[kBig], s_nbig;
     const uint32_t tid = threadIdx.x, NR = d.n_ranges;
-    const uint32_t per = (NR + kScanThreads - 1) / kScanThreads;
-    const uint32_t lo = min(NR, tid * per), hi = min(NR, lo + per);
-    uint64_t tiles = 0;
-    for (uint32_t r = lo; r < hi; ++r) tiles += (d.range_tot[r].x + kApplyBlock - 1) / kApplyBlock;
+    if (tid == 0) s_nbig = 0;
+    uint32_t v[kPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+        const uint32_t i = u * kScanThreads + tid;
+        v[u] = i < NR ? d.range_cnt[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) s_cnt[u * kScanThreads + tid] = v[u];
+    __syncthreads();
+    const uint32_t lo = tid * kPer;  // contiguous ranges per thread: scan order
+    uint64_t tiles = 0, g1 = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+        const uint32_t c = s_cnt[lo + u];
+        g1 += c;
+        tiles += (c + kTile - 1) / kTile;
+    }
     uint64_t total;
     uint64_t t0 = block_exclusive_scan(tiles, &total, s_wave);
-    for (uint32_t r = lo; r < hi; ++r) {
+#pragma unroll 1
+    for (uint32_t u = 0; u < kPer && lo + u < NR; ++u) {
+        const uint32_t r = lo + u, nt = (s_cnt[r] + kTile - 1) / kTile;
         d.range_tile0[r] = (uint32_t)t0;
-        const uint32_t nt = (d.range_tot[r].x + kApplyBlock - 1) / kApplyBlock;
-        for (uint32_t q = 0; q < nt; ++q) d.tile_range[t0 + q] = r;
+        uint32_t q = 0;
+        if (nt > 4) {  // long ranges (the dense input block) are filled cooperatively
+            const uint32_t slot = atomicAdd(&s_nbig, 1u);
+            if (slot < kBig) {
+                s_big[slot] = r;
+                s_big_t0[slot] = (uint32_t)t0;
+                q = nt;
+            }
+        }
+        for (; q < nt; ++q) d.tile_range[t0 + q] = r;
         t0 += nt;
     }
-    if (tid == 0) d.work->total_tiles = (uint32_t)total;
+    const uint64_t wg1 = wave_sum(g1);
+    if ((tid & 63) == 0) s_red[tid >> 6] = wg1;
+    __syncthreads();
+    const uint32_t nbig = min(s_nbig, kBig);
+    for (uint32_t b = 0; b < nbig; ++b) {
+        const uint32_t r = s_big[b], tb = s_big_t0[b], nt = (s_cnt[r] + kTile - 1) / kTile;
+        for (uint32_t q = tid; q < nt; q += kScanThreads) d.tile_range[tb + q] = r;
+    }
+    if (tid == 0) {
+        uint64_t tg1 = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) tg1 += s_red[w];
+        d.work->total_tiles = (uint32_t)total;
+        d.work->g1 = tg1;
+    }
 }
 
-// k_refrac: per pre-gated entry, the refractory gate with a real 8-B gather of
-// lastFired[dst] (brain.metal:79-83), the spike-candidate test
-// (brain.metal:91-92) and the homeostasis input isi (brain.metal:116); the
-// tile-local candidate prefix; written back in place.  Entry after this pass:
-// x = event - region | passed-refractory << 31, y = tile-local candidate
-// prefix | candidate << 31, z = w, w = isi.
-__global__ __launch_bounds__(kApplyBlock) void k_refrac(DeviceState d, KernelParams kp)
+__device__ __forceinline__ uint32_t wave_uniform(uint32_t v)
 {
-    __shared__ uint32_t s_c[kApplyBlock / 64], s_g[kApplyBlock / 64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// k_refrac: one wave per tile.  Per pre-gated entry the refractory gate with a
+// real 8-B gather of lastFired[dst] (brain.metal:79-83), the spike-candidate
+// test (brain.metal:91-92) and the homeostasis input isi (brain.metal:116,
+// into the entry's fourth word); per tile the two lane masks.  The gate is
+// done with the filter image, so it is zeroed here for the next k_bitmap.
+__global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
+{
+    const uint32_t lane = threadIdx.x & 63, gtid = blockIdx.x * 256 + threadIdx.x;
+    for (uint32_t i = gtid; i < d.filter_words; i += gridDim.x * 256) d.filter[i] = 0u;
+    const uint32_t wave = wave_uniform(gtid >> 6), nwaves = gridDim.x * 4;
     const uint64_t now = *d.clock;
     const uint32_t T = d.work->total_tiles;
-    for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
+    for (uint32_t tile = wave; tile < T; tile += nwaves) {
         const uint32_t r = d.tile_range[tile];
-        const uint32_t n = d.range_tot[r].x;
-        const uint32_t j = (tile - d.range_tile0[r]) * kApplyBlock + tid;
+        const uint32_t j = (tile - d.range_tile0[r]) * kTile + lane;
         const uint64_t region = range_begin(r, d.iters, d.n_ranges) * d.iter_events;
-        const bool valid = j < n;
-        uint4 e = valid ? d.g2buf[region + j] : make_uint4(0u, 0u, 0u, 0u);
+        const bool valid = j < d.range_cnt[r];
+        const uint4 e = valid ? d.g2buf[region + j] : make_uint4(0u, 0u, 0u, 0u);
         const uint64_t ld = valid ? d.last_fired[e.y] : 0ull;
         const bool g2 = valid && (now - ld) > (uint64_t)kp.refractory;
         const uint64_t tg = d.syn_offset + region + e.x;
         const bool cand = g2 && spike_candidate(kp, __uint_as_float(e.z), tg, now);
-        const uint64_t bc = __ballot(cand), bg = __ballot(g2);
-        if (lane == 0) {
-            s_c[wid] = (uint32_t)__popcll(bc);
-            s_g[wid] = (uint32_t)__popcll(bg);
-        }
-        __syncthreads();
-        uint32_t pre = mbcnt64(bc), tc = 0, tgt = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kApplyBlock / 64; ++w) {
-            pre += w < wid ? s_c[w] : 0u;
-            tc += s_c[w];
-            tgt += s_g[w];
-        }
+        const uint64_t bg = __ballot(g2), bc = __ballot(cand);
         if (g2 && tg == 0) d.work->t0_g2 = 1;
-        if (valid) {
-            e.x |= (g2 ? 1u : 0u) << 31;
-            e.y = pre | ((cand ? 1u : 0u) << 31);
-            e.w = __float_as_uint((float)(now - ld));
-            d.g2buf[region + j] = e;
-        }
-        if (tid == 0) d.tile_cnt[tile] = make_uint2(tc, tgt);
-        __syncthreads();
+        if (valid) reinterpret_cast<uint32_t*>(d.g2buf + region + j)[3] = __float_as_uint((float)(now - ld));
+        if (lane == 0)
+            d.tile_mask[tile] = make_uint4((uint32_t)bg, (uint32_t)(bg >> 32), (uint32_t)bc, (uint32_t)(bc >> 32));
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_scan: ordered spike budget over the tiles (one workgroup, in event order).
+// k_scan: ordered spike budget over the tiles (one workgroup, in event order),
+// in chunks of kScanThreads x kSpt tiles whose counts are staged in LDS.
 __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelParams kp,
                                                        int64_t* summary_out)
 {
-    __shared__ uint64_t s_wave[kScanThreads / 64];
-    __shared__ uint64_t s_red[2][kScanThreads / 64];
+    constexpr uint32_t kSpt = 8, kChunk = kScanThreads * kSpt;
+    __shared__ uint32_t s_c[kChunk];  // candidates | passed-refractory << 16, per tile
+    __shared__ uint64_t s_wave[kScanThreads / 64], s_red[kScanThreads / 64];
     const uint32_t tid = threadIdx.x, T = d.work->total_tiles;
-    const uint32_t per = (T + kScanThreads - 1) / kScanThreads;
-    const uint32_t lo = min(T, tid * per), hi = min(T, lo + per);
     const uint64_t budget = kp.max_spikes;
-
-    uint64_t cand = 0, g2 = 0;
-    for (uint32_t t = lo; t < hi; ++t) {
-        const uint2 v = d.tile_cnt[t];  // {candidates, passed refractory}
-        cand += v.x;
-        g2 += v.y;
+    uint64_t carry = 0, g2 = 0;
+    for (uint32_t base = 0; base < T; base += kChunk) {
+        uint4 m[kSpt];
+#pragma unroll
+        for (uint32_t u = 0; u < kSpt; ++u) {
+            const uint32_t i = base + u * kScanThreads + tid;
+            m[u] = i < T ? d.tile_mask[i] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kSpt; ++u)
+            s_c[u * kScanThreads + tid] = (uint32_t)(__popc(m[u].z) + __popc(m[u].w)) |
+                                          ((uint32_t)(__popc(m[u].x) + __popc(m[u].y)) << 16);
+        __syncthreads();
+        const uint32_t lo = tid * kSpt;
+        uint32_t cv[kSpt];
+        uint64_t cs = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < kSpt; ++u) {
+            cv[u] = s_c[lo + u];
+            cs += cv[u] & 0xFFFFu;
+            g2 += cv[u] >> 16;
+        }
+        uint64_t tot;
+        uint64_t pre = carry + block_exclusive_scan(cs, &tot, s_wave);  // syncs: s_c is free after
+#pragma unroll
+        for (uint32_t u = 0; u < kSpt; ++u) {
+            const uint32_t t = base + lo + u;
+            // a tile is applied iff some event in it passed the refractory gate
+            // while the budget lasted; inactive tiles carry the budget itself
+            if (t < T) d.tile_pre[t] = (uint32_t)((cv[u] >> 16) > 0 && pre < budget ? pre : budget);
+            pre += cv[u] & 0xFFFFu;
+        }
+        carry += tot;
     }
-    uint64_t cand_total;
-    uint64_t pre = block_exclusive_scan(cand, &cand_total, s_wave);
-    for (uint32_t t = lo; t < hi; ++t) {
-        const uint2 v = d.tile_cnt[t];
-        // a tile is applied iff some event in it passed the refractory gate
-        // while the budget lasted; inactive tiles carry the budget itself
-        d.tile_pre[t] = (uint32_t)(v.y > 0 && pre < budget ? pre : budget);
-        pre += v.x;
-    }
-    uint64_t g1 = 0;
-    const uint32_t NR = d.n_ranges, rper = (NR + kScanThreads - 1) / kScanThreads;
-    for (uint32_t r = min(NR, tid * rper); r < min(NR, tid * rper + rper); ++r) g1 += d.range_tot[r].x;
-    const uint64_t wg2 = wave_sum(g2), wg1 = wave_sum(g1);
-    if ((tid & 63) == 0) {
-        s_red[0][tid >> 6] = wg2;
-        s_red[1][tid >> 6] = wg1;
-    }
+    const uint64_t wg2 = wave_sum(g2);
+    if ((tid & 63) == 0) s_red[tid >> 6] = wg2;
     __syncthreads();
     if (tid == 0) {
-        uint64_t tg2 = 0, tg1 = 0;
-        for (int w = 0; w < kScanThreads / 64; ++w) {
-            tg2 += s_red[0][w];
-            tg1 += s_red[1][w];
-        }
-        const uint64_t capped = cand_total < budget ? cand_total : budget;
+        uint64_t tg2 = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) tg2 += s_red[w];
+        const uint64_t capped = carry < budget ? carry : budget;
         const uint32_t t0 = d.work->t0_g2;
         summary_out[0] = (int64_t)capped;
         summary_out[1] = (int64_t)t0;
@@ -481,19 +519,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelPara
         summary_out[3] = (int64_t)tg2;
         d.work->t0_g2 = 0;  // re-armed for the next pass
         d.work->events = d.events;
-        d.work->g1 = tg1;
         d.work->g2 = tg2;
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_apply: weight update of the gated events that still had budget.
-__global__ __launch_bounds__(kApplyBlock) void k_apply(DeviceState d, KernelParams kp,
-                                                       const int64_t* summaries, uint32_t world,
-                                                       uint32_t rank, int32_t* fired)
+// k_apply: weight update of the gated events that still had budget; one wave
+// per tile, tiles past the budget skipped on one load.
+__global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
+                                               const int64_t* summaries, uint32_t world,
+                                               uint32_t rank, int32_t* fired)
 {
-    __shared__ uint32_t s_u[kApplyBlock / 64], s_f[kApplyBlock / 64];
-    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
     const uint64_t budget = kp.max_spikes;
     const float R = *d.reward, rb = *d.rbar;  // pass-start values (C1), brain.metal:105-106
     uint64_t off = 0;
@@ -503,46 +541,50 @@ __global__ __launch_bounds__(kApplyBlock) void k_apply(DeviceState d, KernelPara
 
     const uint32_t T = d.work->total_tiles;
     uint32_t upd = 0, nf = 0;
-    for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
+    for (uint32_t tile = wave; tile < T; tile += nwaves) {
         const uint64_t P = off + d.tile_pre[tile];
         if (P >= budget) continue;
+        const uint4 m = d.tile_mask[tile];
+        const uint64_t bg = m.x | ((uint64_t)m.y << 32), bc = m.z | ((uint64_t)m.w << 32);
+        if (!((bg >> lane) & 1u)) continue;   // no entry, or stopped by the refractory gate
+        const uint64_t pre = P + mbcnt64(bc);  // spike candidates before this event
+        if (pre >= budget) continue;           // budget == 0 at this event: brain.metal:85-88
         const uint32_t r = d.tile_range[tile];
-        const uint32_t j = (tile - d.range_tile0[r]) * kApplyBlock + tid;
-        if (j >= d.range_tot[r].x) continue;
+        const uint32_t j = (tile - d.range_tile0[r]) * kTile + lane;
         const uint64_t region = range_begin(r, d.iters, d.n_ranges) * d.iter_events;
         const uint4 e = d.g2buf[region + j];
-        if (!(e.x >> 31)) continue;   // stopped by the refractory gate
-        const uint64_t pre = P + (e.y & 0x7FFFFFFFu);
-        if (pre >= budget) continue;  // budget == 0 at this event: brain.metal:85-88
-        const bool f = (e.y >> 31) != 0;
-        const uint64_t t = region + (e.x & 0x7FFFFFFFu);
+        const bool f = (bc >> lane) & 1u;
         const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.w));
-        uint32_t* rec = reinterpret_cast<uint32_t*>(d.syn + t);
-        rec[2] = __float_as_uint(w);       // brain.metal:122 (src/dst/pad unchanged)
+        // brain.metal:122.  Non-temporal: a plain 4-B store leaves ~160k
+        // scattered dirty partial lines per pass whose write-back lands in the
+        // middle of the next pass's record stream (+30 us of gate time,
+        // tools/exp_variants.py).
+        __builtin_nontemporal_store(__float_as_uint(w), reinterpret_cast<uint32_t*>(d.syn + region + e.x) + 2);
         ++upd;
         if (f) {
-            fired[pre] = (int32_t)rec[1];  // dst, spike list in budget order
+            fired[pre] = (int32_t)e.y;  // dst, spike list in budget order
             ++nf;
         }
     }
+    // per-workgroup partials (atomics from every wave on one address serialise)
+    __shared__ uint32_t s_u[4], s_f[4];
     const uint32_t wu = wave_sum(upd), wf = wave_sum(nf);
-    if ((tid & 63) == 0) {
-        s_u[tid >> 6] = wu;
-        s_f[tid >> 6] = wf;
+    if (lane == 0) {
+        s_u[threadIdx.x >> 6] = wu;
+        s_f[threadIdx.x >> 6] = wf;
     }
     __syncthreads();
-    if (tid == 0)
-        d.apply_partial[blockIdx.x] =
-            make_uint2(s_u[0] + s_u[1] + s_u[2] + s_u[3], s_f[0] + s_f[1] + s_f[2] + s_f[3]);
+    if (threadIdx.x == 0)
+        d.apply_partial[blockIdx.x] = make_uint2(s_u[0] + s_u[1] + s_u[2] + s_u[3], s_f[0] + s_f[1] + s_f[2] + s_f[3]);
 }
 
 // ---------------------------------------------------------------------------
 // k_finalize: stamps, rBar, clock tick, statistics (one workgroup).
-__global__ __launch_bounds__(256) void k_finalize(DeviceState d, KernelParams kp,
-                                                  const int64_t* summaries, uint32_t world,
-                                                  const int32_t* fired)
+__global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, KernelParams kp,
+                                                           const int64_t* summaries, uint32_t world,
+                                                           const int32_t* fired)
 {
-    __shared__ uint32_t s_u[4], s_f[4];
+    constexpr uint32_t kU = 4;
     const uint32_t tid = threadIdx.x;
     const uint64_t now = *d.clock;
     const uint64_t budget = kp.max_spikes;
@@ -552,16 +594,25 @@ __global__ __launch_bounds__(256) void k_finalize(DeviceState d, KernelParams kp
         events += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 2];
     }
     const uint64_t n_fired = total < budget ? total : budget;
-    for (uint64_t i = tid; i < n_fired; i += 256) {
-        const uint32_t n = (uint32_t)fired[i];
-        if (n < d.n_nrn) d.last_fired[n] = now;  // brain.metal:125-126, deferred
+    for (uint64_t i0 = 0; i0 < n_fired; i0 += kU * kScanThreads) {
+        uint32_t n[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint64_t i = i0 + u * kScanThreads + tid;
+            n[u] = i < n_fired ? (uint32_t)fired[i] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u)
+            if (n[u] < d.n_nrn) d.last_fired[n[u]] = now;  // brain.metal:125-126, deferred
     }
     uint32_t upd = 0, nf = 0;
-    for (uint32_t i = tid; i < (uint32_t)kApplyGrid; i += 256) {
-        const uint2 v = d.apply_partial[i];
+#pragma unroll
+    for (uint32_t u = 0; u < kTileBlocks / kScanThreads; ++u) {
+        const uint2 v = d.apply_partial[u * kScanThreads + tid];
         upd += v.x;
         nf += v.y;
     }
+    __shared__ uint32_t s_u[kScanThreads / 64], s_f[kScanThreads / 64];
     upd = wave_sum(upd);
     nf = wave_sum(nf);
     if ((tid & 63) == 0) {
@@ -570,6 +621,11 @@ __global__ __launch_bounds__(256) void k_finalize(DeviceState d, KernelParams kp
     }
     __syncthreads();
     if (tid == 0) {
+        uint64_t tu = 0, tf = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) {
+            tu += s_u[w];
+            tf += s_f[w];
+        }
         const float R = *d.reward, rb = *d.rbar;
         if (summaries[1] != 0 && budget > 0)
             *d.rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
@@ -579,8 +635,8 @@ __global__ __launch_bounds__(256) void k_finalize(DeviceState d, KernelParams kp
         w->stats.events += w->events;
         w->stats.pre_gated += w->g1;
         w->stats.post_gated += w->g2;
-        w->stats.updated += s_u[0] + s_u[1] + s_u[2] + s_u[3];
-        w->stats.fired += s_f[0] + s_f[1] + s_f[2] + s_f[3];
+        w->stats.updated += tu;
+        w->stats.fired += tf;
     }
 }
 
@@ -712,9 +768,6 @@ hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t 
     if (d.n_nrn == 0) return hipSuccess;
     hipLaunchKernelGGL(k_bitmap, dim3((uint32_t)((d.n_nrn + 1023) / 1024)), dim3(256), 0, s, d, kp,
                        stim_first, stim_count);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_fold, dim3((d.filter_words + 255) / 256), dim3(256), 0, s, d);
     return hipGetLastError();
 }
 
@@ -723,7 +776,7 @@ hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream
     hipLaunchKernelGGL(k_tiles, dim3(1), dim3(kScanThreads), 0, s, d);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_refrac, dim3(kApplyGrid), dim3(kApplyBlock), 0, s, d, kp);
+    hipLaunchKernelGGL(k_refrac, dim3(kTileBlocks), dim3(256), 0, s, d, kp);
     return hipGetLastError();
 }
 
@@ -748,7 +801,7 @@ hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int64_t* su
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
                         uint32_t world, uint32_t rank, int32_t* fired, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_apply, dim3(kApplyGrid), dim3(kApplyBlock), 0, s, d, kp, summaries, world,
+    hipLaunchKernelGGL(k_apply, dim3(kTileBlocks), dim3(256), 0, s, d, kp, summaries, world,
                        rank, fired);
     return hipGetLastError();
 }
@@ -756,7 +809,7 @@ hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int6
 hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
                            uint32_t world, const int32_t* fired, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, s, d, kp, summaries, world, fired);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kScanThreads), 0, s, d, kp, summaries, world, fired);
     return hipGetLastError();
 }
 
