@@ -89,7 +89,7 @@ void free_all(abnn_brain* b)
     (void)hipSetDevice(b->device);
     void* ptrs[] = {b->d.syn,       b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->d.bitmap,    b->d.filter,     b->d.range_cnt,     b->d.range_tile0,
-                    b->d.tile_mask, b->d.tile_pre,   b->d.g2buf,         b->d.apply_partial,
+                    b->d.tile_mask, b->d.tile_pre,   b->d.g1idx,    b->d.g2e,         b->d.apply_partial,
                     b->d.fired,     b->d.summary,    b->d.work,          b->idx_scratch,
                     b->u64_scratch,  b->d.tile_range,  const_cast<uint4*>(b->d.dummy)};
     for (void* p : ptrs)
@@ -339,7 +339,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.filter_exact = d.n_bitmap_words <= filter_words ? 1u : 0u;
     abnn_status s;
     // build_buffers, brain.cpp:52-69: allocate and zero every buffer.
-    if ((s = dalloc(&d.syn, dims->n_syn)) != ABNN_OK) return fail(s);
+    // padded: the gate's last iteration reads up to one iteration past the sweep
+    if ((s = dalloc(&d.syn, dims->n_syn + kDummyRecords)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_fired, n_nrn)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_visited, n_nrn)) != ABNN_OK) return fail(s);
     uint64_t* sb = nullptr;
@@ -356,7 +357,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.tile_mask, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.tile_range, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.tile_pre, max_tiles)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.g2buf, iters * iter_events)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.g1idx, iters * iter_events)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.g2e, max_tiles * kTile)) != ABNN_OK) return fail(s);
     uint4* dummy = nullptr;
     if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
     d.dummy = dummy;

@@ -20,7 +20,8 @@ constexpr int kScanThreads = 1024; // the range and tile scans are one workgroup
 constexpr int kMaxGateBlocks = 1024;
 constexpr int kMaxRanges = 16384;
 static_assert(kTileBlocks % kScanThreads == 0, "k_finalize sums the apply partials in whole rounds");  // kMaxGateBlocks x up to 16 waves; staged whole in LDS by k_tiles
-constexpr int kDummyRecords = 64 * 16;  // >= 64 lanes x max events per lane
+constexpr int kDummyRecords = 64 * 16;  // >= 64 lanes x max events per lane; also the record-buffer padding
+constexpr int kStageEntries = 448;      // per gate wave: 4-B event offsets staged in LDS
 
 // Per-pass bookkeeping in device memory (one per handle).
 struct alignas(16) PassWork {
@@ -34,7 +35,7 @@ struct alignas(16) PassWork {
 
 // Kernel-facing view of a handle's device state.
 struct DeviceState {
-    uint4* syn;               // abnn_synapse[n_syn] viewed as 16-B vectors
+    uint4* syn;               // abnn_synapse[n_syn + kDummyRecords] viewed as 16-B vectors (zero padding)
     uint64_t* last_fired;     // [n_nrn]
     uint64_t* last_visited;   // [n_nrn]
     uint64_t* clock;          // [1]
@@ -47,7 +48,8 @@ struct DeviceState {
     uint32_t* tile_range;     // [max_tiles] range of each tile
     uint4* tile_mask;         // [max_tiles] {passed refractory, spike candidate} lane masks (2 x u64)
     uint32_t* tile_pre;       // [max_tiles] exclusive candidate prefix (capped; = budget: skip)
-    uint4* g2buf;             // [iters * iter_events] gated entries {event - region, dst, w, isi}
+    uint32_t* g1idx;          // [iters * iter_events] pre-gated event offsets (event - region), per-range regions
+    uint4* g2e;               // [max_tiles * kTile] {event - region, dst, w, isi} of the events that passed
     const uint4* dummy;       // [kDummyRecords] zero records: target of masked-off stream loads
     uint2* apply_partial;     // [kTileBlocks] {updated, fired} per apply workgroup
     int32_t* fired;           // [max_spikes] internal spike list (world = 1)

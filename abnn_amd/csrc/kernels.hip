@@ -30,6 +30,8 @@
 //
 // All fp32 arithmetic is compiled with -ffp-contract=off and written operation
 // for operation like the oracle, so weights are bit-identical to the CPU.
+#include <type_traits>
+
 #include "engine.h"
 
 #pragma clang fp contract(off)
@@ -93,6 +95,7 @@ __device__ __forceinline__ float updated_weight(const KernelParams& kp, float w,
 }
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 
 // Streaming 16-B load that should not displace the L2/MALL-resident neuron
 // state (bitmap, lastFired): non-temporal dwordx4.
@@ -106,6 +109,11 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t wave_uniform(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k)
@@ -207,34 +215,35 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
 
 // ---------------------------------------------------------------------------
 // k_gate: the streaming kernel (see file header).  Every wave owns one
-// contiguous range of events.  The hot loop holds only what a 16-B record
-// stream needs: the LDS filter, an L2 bitmap word on a filter hit, and the
-// next iteration's records in flight.  Events that pass the pre-gate (~0.2 %
-// in steady state) are staged in event order in the wave's LDS slab and
-// written out as whole-wave coalesced stores, so stores rarely sit between the
-// prefetch and its wait (vmcnt retires in issue order, stores included).
+// contiguous range of events.  The pre-spike gate reads only the src word of
+// each 16-B record (the same lines stream from HBM; one register per event
+// instead of four), so a wave keeps K events per lane in flight in K VGPRs.
+// Loads use a wave-uniform base: the record buffer is padded by
+// kDummyRecords, so the sweep's last iteration reads past its end instead of
+// masking lanes, and the prefetch after a range's last iteration reads the
+// zero dummy block.  Pre-gated events (~0.2 % in steady state) are staged as
+// 4-B event offsets, kStageEntries per wave, so a wave usually flushes once,
+// at the end of its range (vmcnt retires in issue order, stores included: a
+// store between the prefetch and its wait delays the whole stream).
 template <int BLOCK, int K, int FW, bool kTrack>
 __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
     constexpr int NW = BLOCK / 64;
     constexpr uint32_t IE = 64 * K;
-#ifdef ABNN_EXP_BIG_STAGE
-    constexpr uint32_t kStage = (80 * 1024 - FW * 4) / NW / 16;  // LDS left beside the filter
-    constexpr uint32_t kFlushAt = kStage - 64;   // one k-step adds at most 64
-#else
-    constexpr uint32_t kFlushAt = 32;            // staged entries before a flush
-    constexpr uint32_t kStage = kFlushAt + 64;   // one k-step adds at most 64
-#endif
+    constexpr uint32_t kFlushAt = kStageEntries - 64;  // one k-step adds at most 64
+    static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
     __shared__ uint32_t s_filter[FW];
-    __shared__ uint4 s_stage[NW][kStage];
+    __shared__ uint32_t s_stage[NW][kStageEntries];
+    using Word = typename std::conditional<kTrack, u32x2_t, uint32_t>::type;  // {src[, dst]}
 
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wid = wave_uniform(tid >> 6);
     const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
     const uint64_t it_begin = range_begin(r, d.iters, NR), it_end = range_begin(r + 1, d.iters, NR);
     const uint64_t region = it_begin * IE;
     const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
     const bool exact = d.filter_exact != 0;
-    uint4* stage = s_stage[wid];
+    uint32_t* stage = s_stage[wid];
 
     {
         const uint4* src = reinterpret_cast<const uint4*>(d.filter);
@@ -242,52 +251,40 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         for (int i = tid; i < FW / 4; i += BLOCK) dst[i] = src[i];
     }
 
-    // Every issue is exactly K loads, straight-line: lanes past the sweep and
-    // the prefetch after a range's last iteration read the small L2-resident
-    // dummy block instead.  A branch that could issue fewer loads makes the
-    // compiler's vmcnt bookkeeping assume none, and the wait for the filter
-    // confirmations below would then also wait for this prefetch.
-    uint4 nxt[K];
+    Word nxt[K];
     auto issue = [&](uint64_t it, bool live) {
-        const uint64_t base = it * IE;
+        const uint4* base = live ? d.syn + it * IE : d.dummy;  // wave-uniform
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint64_t t = base + k * 64 + lane;
-            const uint4* p = (live && t < d.events) ? d.syn + t : d.dummy + (k * 64 + lane);
-            nxt[k] = load_stream16(p);
-        }
+        for (int k = 0; k < K; ++k)
+            nxt[k] = __builtin_nontemporal_load(reinterpret_cast<const Word*>(base + k * 64 + lane));
     };
     issue(it_begin, it_begin < it_end);
     __syncthreads();
 
     const uint32_t nn = (uint32_t)d.n_nrn;  // N_NRN < 2^32 (checked at create)
     uint32_t pend = 0, flushed = 0;
-#ifdef ABNN_EXP_FAKE_FLUSH
-    uint32_t exp_acc = 0;
-#endif
-    auto flush = [&]() {  // wave-uniform: write the staged entries, in order
-#if defined(ABNN_EXP_FAKE_FLUSH)
-        if (lane < pend) exp_acc ^= stage[lane].x;
-        if (lane + 64 < pend) exp_acc ^= stage[64 + lane].y;
-#elif !defined(ABNN_EXP_NO_FLUSH)
-        // non-temporal: plain stores keep these lines in L2 beside the record
-        // stream and cost ~22 us per pass at config 3 (tools/exp_variants.py)
-        for (uint32_t q = lane; q < pend; q += 64) {
-            const uint4 v = stage[q];
-            __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
-                                        reinterpret_cast<u32x4_t*>(d.g2buf + region + flushed + q));
-        }
-#endif
+    auto flush = [&]() {  // wave-uniform: write the staged offsets, in order
+        for (uint32_t q = lane; q < pend; q += 64)
+            __builtin_nontemporal_store(stage[q], d.g1idx + region + flushed + q);
         flushed += pend;
         pend = 0;
     };
     for (uint64_t it = it_begin; it < it_end; ++it) {
-        uint4 rec[K];
+        uint32_t src[K];
+        uint32_t dst[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) rec[k] = nxt[k];
+        for (int k = 0; k < K; ++k) {
+            if constexpr (kTrack) {
+                src[k] = nxt[k].x;
+                dst[k] = nxt[k].y;
+            } else {
+                src[k] = nxt[k];
+                dst[k] = 0;
+            }
+        }
         const uint64_t base = it * IE;
-        uint32_t vmask = (1u << K) - 1u;  // events of this lane that exist
-        if (base + IE > d.events) {       // only the sweep's last iteration
+        uint32_t vmask = (K == 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);  // events of this lane that exist
+        if (base + IE > d.events) {  // only the sweep's last iteration
             vmask = 0;
 #pragma unroll
             for (int k = 0; k < K; ++k)
@@ -299,11 +296,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // bounds), no branches.
         uint32_t fw[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) fw[k] = s_filter[(rec[k].x >> 5) & (FW - 1)];
+        for (int k = 0; k < K; ++k) fw[k] = s_filter[(src[k] >> 5) & (FW - 1)];
         uint32_t fm = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const bool hit = ((fw[k] >> (rec[k].x & 31u)) & 1u) && rec[k].x < nn && rec[k].y < nn;
+            const bool hit = ((fw[k] >> (src[k] & 31u)) & 1u) && src[k] < nn;
             fm |= (hit ? 1u : 0u) << k;
         }
         fm &= vmask;
@@ -313,46 +310,34 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             cw[k] = 0xFFFFFFFFu;
-#ifndef ABNN_EXP_NO_CONFIRM
-            if (!exact && ((fm >> k) & 1u)) cw[k] = d.bitmap[rec[k].x >> 5];
-#endif
+            if (!exact && ((fm >> k) & 1u)) cw[k] = d.bitmap[src[k] >> 5];
         }
         issue(it + 1, it + 1 < it_end);  // next iteration's records in flight
         // keep every prefetch load ahead of the first use of a confirmation
         // (otherwise the scheduler interleaves them and waits mid-prefetch)
         __builtin_amdgcn_sched_barrier(0);
 
-        if (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
+        if constexpr (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (((vmask >> k) & 1u) && rec[k].y < nn) d.last_visited[rec[k].y] = now;
+                if (((vmask >> k) & 1u) && dst[k] < nn) d.last_visited[dst[k]] = now;
         }
         uint32_t g1m = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            g1m |= ((((fm >> k) & 1u) && ((cw[k] >> (rec[k].x & 31u)) & 1u)) ? 1u : 0u) << k;
-        if (__ballot(g1m != 0) == 0) continue;  // ~half the wave-iterations: nothing to stage
+            g1m |= ((((fm >> k) & 1u) && ((cw[k] >> (src[k] & 31u)) & 1u)) ? 1u : 0u) << k;
+        if (__ballot(g1m != 0) == 0) continue;  // ~a third of the wave-iterations: nothing to stage
+        const uint32_t rel = (uint32_t)(base - region);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const bool g1 = (g1m >> k) & 1u;
             const uint64_t b1 = __ballot(g1);
-#ifndef ABNN_EXP_NO_STAGE
-            if (g1)
-                stage[pend + mbcnt64(b1)] =
-                    make_uint4((uint32_t)(base - region) + k * 64 + lane, rec[k].y, rec[k].z, 0u);
-#endif
+            if (g1) stage[pend + mbcnt64(b1)] = rel + k * 64 + lane;
             pend += (uint32_t)__popcll(b1);
             if (pend >= kFlushAt) flush();
         }
     }
     flush();
-#ifdef ABNN_EXP_FAKE_FLUSH
-    if (exp_acc == 0x12345677u) d.tile_pre[r] = exp_acc;
-#endif
-#if defined(ABNN_EXP_NO_FLUSH) || defined(ABNN_EXP_FAKE_FLUSH) || defined(ABNN_EXP_NO_STAGE) || \
-    defined(ABNN_EXP_NO_CONFIRM)
-    flushed = 0;  // timing-only builds: nothing downstream may read their entries
-#endif
     if (lane == 0) d.range_cnt[r] = flushed;
 }
 
@@ -425,15 +410,11 @@ __global__ __launch_bounds__(kScanThreads) void k_tiles(DeviceState d)
     }
 }
 
-__device__ __forceinline__ uint32_t wave_uniform(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
-
 // k_refrac: one wave per tile.  Per pre-gated entry the refractory gate with a
 // real 8-B gather of lastFired[dst] (brain.metal:79-83), the spike-candidate
 // test (brain.metal:91-92) and the homeostasis input isi (brain.metal:116,
-// into the entry's fourth word); per tile the two lane masks.  The gate is
+// into the entry's fourth word); per tile the two lane masks and, for the
+// events that passed, the entry {offset, dst, w, isi} at the tile's slot.  The gate is
 // done with the filter image, so it is zeroed here for the next k_bitmap.
 __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
 {
@@ -442,19 +423,23 @@ __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
     const uint32_t wave = wave_uniform(gtid >> 6), nwaves = gridDim.x * 4;
     const uint64_t now = *d.clock;
     const uint32_t T = d.work->total_tiles;
+    const uint32_t nn = (uint32_t)d.n_nrn;
     for (uint32_t tile = wave; tile < T; tile += nwaves) {
         const uint32_t r = d.tile_range[tile];
         const uint32_t j = (tile - d.range_tile0[r]) * kTile + lane;
         const uint64_t region = range_begin(r, d.iters, d.n_ranges) * d.iter_events;
-        const bool valid = j < d.range_cnt[r];
-        const uint4 e = valid ? d.g2buf[region + j] : make_uint4(0u, 0u, 0u, 0u);
-        const uint64_t ld = valid ? d.last_fired[e.y] : 0ull;
+        bool valid = j < d.range_cnt[r];
+        const uint32_t rel = valid ? d.g1idx[region + j] : 0u;
+        // the gate kept only the event offset: dst and w come from the record
+        const uint4 rec = valid ? d.syn[region + rel] : make_uint4(0u, 0u, 0u, 0u);
+        valid = valid && rec.y < nn;
+        const uint64_t ld = valid ? d.last_fired[rec.y] : 0ull;
         const bool g2 = valid && (now - ld) > (uint64_t)kp.refractory;
-        const uint64_t tg = d.syn_offset + region + e.x;
-        const bool cand = g2 && spike_candidate(kp, __uint_as_float(e.z), tg, now);
+        const uint64_t tg = d.syn_offset + region + rel;
+        const bool cand = g2 && spike_candidate(kp, __uint_as_float(rec.z), tg, now);
         const uint64_t bg = __ballot(g2), bc = __ballot(cand);
         if (g2 && tg == 0) d.work->t0_g2 = 1;
-        if (valid) reinterpret_cast<uint32_t*>(d.g2buf + region + j)[3] = __float_as_uint((float)(now - ld));
+        if (g2) d.g2e[(uint64_t)tile * kTile + lane] = make_uint4(rel, rec.y, rec.z, __float_as_uint((float)(now - ld)));
         if (lane == 0)
             d.tile_mask[tile] = make_uint4((uint32_t)bg, (uint32_t)(bg >> 32), (uint32_t)bc, (uint32_t)(bc >> 32));
     }
@@ -550,9 +535,8 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
         const uint64_t pre = P + mbcnt64(bc);  // spike candidates before this event
         if (pre >= budget) continue;           // budget == 0 at this event: brain.metal:85-88
         const uint32_t r = d.tile_range[tile];
-        const uint32_t j = (tile - d.range_tile0[r]) * kTile + lane;
         const uint64_t region = range_begin(r, d.iters, d.n_ranges) * d.iter_events;
-        const uint4 e = d.g2buf[region + j];
+        const uint4 e = d.g2e[(uint64_t)tile * kTile + lane];
         const bool f = (bc >> lane) & 1u;
         const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.w));
         // brain.metal:122.  Non-temporal: a plain 4-B store leaves ~160k
@@ -730,13 +714,14 @@ int occupancy_shape(bool track)
 // Compiled gate shapes: threads per workgroup x events per lane x filter words.
 #define ABNN_GATE_SHAPES(X) \
     X(512, 8, 16384)        \
+    X(512, 16, 16384)       \
     X(512, 4, 16384)        \
-    X(1024, 4, 16384)       \
-    X(1024, 4, 8192)        \
+    X(512, 8, 8192)         \
+    X(512, 16, 8192)        \
     X(1024, 8, 8192)        \
-    X(512, 4, 8192)         \
-    X(256, 8, 8192)         \
-    X(256, 16, 16384)
+    X(1024, 4, 8192)        \
+    X(256, 16, 8192)        \
+    X(256, 8, 8192)
 
 constexpr uint64_t shape_key(uint32_t b, uint32_t k, uint32_t fw) { return ((uint64_t)b << 40) | ((uint64_t)k << 32) | fw; }
 

@@ -1,3 +1,4 @@
+#include <type_traits>
 // ubench_ablate.hip -- ablation study of the gate kernel structure (not product
 // code).  Data shaped like config 3 in steady state: 150M 16-B records over
 // 5,000,512 neurons, ~15.6k recent source neurons (exact bitmap + 64 KiB
@@ -41,7 +42,9 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-enum { F_FILTER = 1, F_CONFIRM = 2, F_GATHER = 4, F_STORE = 8, F_STAGE = 16, F_PLAIN = 32, F_SKIP = 64 };
+enum { F_FILTER = 1, F_CONFIRM = 2, F_GATHER = 4, F_STORE = 8, F_STAGE = 16, F_PLAIN = 32, F_SKIP = 64,
+       F_NOWRITE = 128 /* stage: no LDS write */, F_NOSTORE = 256 /* flush: LDS read, no global store */,
+       F_T4 = 512 /* stage 4-B event offsets, 448 per wave: flush ~once per range */ };
 
 template <int BLOCK, int K, int FLAGS, int PF>
 __global__ __launch_bounds__(BLOCK) void k_var(const uint4* syn, uint64_t events, uint32_t iters,
@@ -134,14 +137,15 @@ __global__ __launch_bounds__(BLOCK) void k_prod(const uint4* syn, uint64_t event
 {
     constexpr int NW = BLOCK / 64;
     constexpr uint32_t IE = 64 * K;
-    constexpr uint32_t kFlushAt = 32, kStage = 96;
+    constexpr uint32_t kFlushAt = (FLAGS & F_T4) ? 384 : 32, kStage = kFlushAt + 64;
+    using Entry = typename std::conditional<(FLAGS & F_T4) != 0, uint32_t, uint4>::type;
     __shared__ uint32_t s_filter[FW];
-    __shared__ uint4 s_stage[NW][kStage];
+    __shared__ Entry s_stage[NW][kStage];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
     const uint64_t itb = (uint64_t)r * iters / NR, ite = (uint64_t)(r + 1) * iters / NR;
     const uint64_t region = itb * IE;
-    uint4* stage = s_stage[wid];
+    Entry* stage = s_stage[wid];
     for (int i = tid; i < FW / 4; i += BLOCK)
         reinterpret_cast<uint4*>(s_filter)[i] = reinterpret_cast<const uint4*>(filt)[i];
     uint4 nxt[K];
@@ -154,11 +158,20 @@ __global__ __launch_bounds__(BLOCK) void k_prod(const uint4* syn, uint64_t event
     };
     issue(itb, itb < ite);
     __syncthreads();
-    uint32_t pend = 0, flushed = 0;
+    uint32_t pend = 0, flushed = 0, sink = 0;
     auto flush = [&]() {
+        if constexpr ((FLAGS & F_T4) != 0) {
+            uint32_t* o = reinterpret_cast<uint32_t*>(out);
+            for (uint32_t q = lane; q < pend; q += 64)
+                __builtin_nontemporal_store(stage[q], o + region + flushed + q);
+            flushed += pend;
+            pend = 0;
+            return;
+        }
         for (uint32_t q = lane; q < pend; q += 64) {
-            const uint4 v = stage[q];
-            if (FLAGS & F_PLAIN) out[region + flushed + q] = v;
+            const uint4 v = reinterpret_cast<const uint4*>(stage)[q];
+            if (FLAGS & F_NOSTORE) sink ^= v.x ^ v.y;
+            else if (FLAGS & F_PLAIN) out[region + flushed + q] = v;
             else __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(out + region + flushed + q));
         }
         flushed += pend;
@@ -194,7 +207,13 @@ __global__ __launch_bounds__(BLOCK) void k_prod(const uint4* syn, uint64_t event
             for (int k = 0; k < K; ++k) {
                 const bool g1 = (g1m >> k) & 1u;
                 const uint64_t b1 = __ballot(g1);
-                if (g1) stage[pend + mbcnt64(b1)] = make_uint4((uint32_t)(base - region) + k * 64 + lane, rec[k].y, rec[k].z, 0u);
+                if constexpr ((FLAGS & F_T4) != 0) {
+                    if (g1) stage[pend + mbcnt64(b1)] = (uint32_t)(base - region) + k * 64 + lane;
+                } else {
+                    if (!(FLAGS & F_NOWRITE) && g1)
+                        reinterpret_cast<uint4*>(stage)[pend + mbcnt64(b1)] =
+                            make_uint4((uint32_t)(base - region) + k * 64 + lane, rec[k].y, rec[k].z, 0u);
+                }
                 pend += (uint32_t)__popcll(b1);
                 if (pend >= kFlushAt) flush();
             }
@@ -204,6 +223,7 @@ __global__ __launch_bounds__(BLOCK) void k_prod(const uint4* syn, uint64_t event
     }
     if (FLAGS & F_STAGE) flush();
     if (lane == 0) tot[r] = flushed + pend;
+    if (sink == 0x9876543u) tot[r] = sink;
 }
 
 // Software-pipelined production loop: iteration i waits once (record block i
@@ -217,9 +237,10 @@ __global__ __launch_bounds__(BLOCK) void k_pipe(const uint4* syn, uint64_t event
 {
     constexpr int NW = BLOCK / 64;
     constexpr uint32_t IE = 64 * K;
-    constexpr uint32_t kFlushAt = 32, kStage = 96;
+    constexpr uint32_t kFlushAt = (FLAGS & F_T4) ? 384 : 32, kStage = kFlushAt + 64;
+    using Entry = typename std::conditional<(FLAGS & F_T4) != 0, uint32_t, uint4>::type;
     __shared__ uint32_t s_filter[FW];
-    __shared__ uint4 s_stage[NW][kStage];
+    __shared__ Entry s_stage[NW][kStage];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
     const uint64_t itb = (uint64_t)r * iters / NR, ite = (uint64_t)(r + 1) * iters / NR;
@@ -295,6 +316,214 @@ __global__ __launch_bounds__(BLOCK) void k_pipe(const uint4* syn, uint64_t event
     if (lane == 0) tot[r] = flushed;
 }
 
+// Pipelined loop with 4-B staged entries (event offset only; dst and w are
+// re-read downstream): iteration i waits once, issues the prefetch of i+1
+// at once, stages i-1 (its confirmations have landed), then filters i and
+// issues its confirmations.  Carried state: confirmation words + bit indices.
+template <int BLOCK, int K, int FLAGS>
+__global__ __launch_bounds__(BLOCK) void k_pipe4(const uint4* syn, uint64_t events, uint32_t iters,
+                                                 const uint32_t* bitmap, const uint32_t* filt,
+                                                 const uint4* dummy, uint4* out, uint32_t* tot)
+{
+    constexpr int NW = BLOCK / 64;
+    constexpr uint32_t IE = 64 * K;
+    constexpr uint32_t kFlushAt = 384, kStage = kFlushAt + 64;
+    __shared__ uint32_t s_filter[FW];
+    __shared__ uint32_t s_stage[NW][kStage];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
+    const uint64_t itb = (uint64_t)r * iters / NR, ite = (uint64_t)(r + 1) * iters / NR;
+    const uint64_t region = itb * IE;
+    uint32_t* stage = s_stage[wid];
+    for (int i = tid; i < FW / 4; i += BLOCK)
+        reinterpret_cast<uint4*>(s_filter)[i] = reinterpret_cast<const uint4*>(filt)[i];
+    uint4 nxt[K];
+    auto issue = [&](uint64_t it, bool live) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t t = it * IE + k * 64 + lane;
+            nxt[k] = ldnt((live && t < events) ? syn + t : dummy + (k * 64 + lane));
+        }
+    };
+    issue(itb, itb < ite);
+    __syncthreads();
+    uint32_t pend = 0, flushed = 0;
+    uint32_t* o = reinterpret_cast<uint32_t*>(out);
+    auto flush = [&]() {
+        for (uint32_t q = lane; q < pend; q += 64)
+            __builtin_nontemporal_store(stage[q], o + region + flushed + q);
+        flushed += pend;
+        pend = 0;
+    };
+    uint32_t pfm = 0, pcw[K], pbit[K];
+    uint32_t prel = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) pcw[k] = pbit[k] = 0;
+    for (uint64_t it = itb; it <= ite; ++it) {
+        uint4 rec[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) rec[k] = nxt[k];
+        const bool live = it < ite;
+        issue(it + 1, it + 1 < ite);
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t g1m = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) g1m |= ((((pfm >> k) & 1u) && ((pcw[k] >> pbit[k]) & 1u)) ? 1u : 0u) << k;
+        if (__ballot(g1m != 0) != 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool g1 = (g1m >> k) & 1u;
+                const uint64_t b1 = __ballot(g1);
+                if (g1) stage[pend + mbcnt64(b1)] = prel + k * 64 + lane;
+                pend += (uint32_t)__popcll(b1);
+                if (pend >= kFlushAt) flush();
+            }
+        }
+        if (!live) break;
+        uint32_t fw[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) fw[k] = s_filter[(rec[k].x >> 5) & (FW - 1)];
+        uint32_t fm = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) fm |= ((fw[k] >> (rec[k].x & 31u)) & 1u) << k;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            pcw[k] = 0u;
+            if ((fm >> k) & 1u) pcw[k] = bitmap[rec[k].x >> 5];
+            pbit[k] = rec[k].x & 31u;
+        }
+        pfm = fm;
+        prel = (uint32_t)(it * IE - region);
+    }
+    flush();
+    if (lane == 0) tot[r] = flushed;
+}
+
+__device__ __forceinline__ uint32_t ldnt32(const uint32_t* p) { return __builtin_nontemporal_load(p); }
+
+// x-only gate loop: each lane loads just the src dword of its records (same
+// lines from HBM, a quarter of the registers), stages 4-B event offsets.
+// Loads use a wave-uniform base (the record buffer is padded, so the last
+// iteration reads past the end instead of masking lanes).
+// PIPE: stage iteration i-1 after issuing the prefetch of i+1.
+template <int BLOCK, int K, int PIPE>
+__global__ __launch_bounds__(BLOCK) void k_x(const uint4* syn, uint64_t events, uint32_t iters,
+                                             const uint32_t* bitmap, const uint32_t* filt,
+                                             const uint4* dummy, uint4* out, uint32_t* tot)
+{
+    constexpr int NW = BLOCK / 64;
+    constexpr uint32_t IE = 64 * K;
+    constexpr uint32_t kStage = 448, kFlushAt = kStage - 64;
+    __shared__ uint32_t s_filter[FW];
+    __shared__ uint32_t s_stage[NW][kStage];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
+    const uint64_t itb = (uint64_t)r * iters / NR, ite = (uint64_t)(r + 1) * iters / NR;
+    const uint64_t region = itb * IE;
+    uint32_t* stage = s_stage[wid];
+    const uint32_t* sx = reinterpret_cast<const uint32_t*>(syn);
+    const uint32_t* dx = reinterpret_cast<const uint32_t*>(dummy);
+    for (int i = tid; i < FW / 4; i += BLOCK)
+        reinterpret_cast<uint4*>(s_filter)[i] = reinterpret_cast<const uint4*>(filt)[i];
+    uint32_t nxt[K];
+    auto issue = [&](uint64_t it, bool live) {
+        const uint32_t* base = live ? sx + 4 * (it * IE) : dx;  // wave-uniform
+#pragma unroll
+        for (int k = 0; k < K; ++k) nxt[k] = ldnt32(base + 4 * (k * 64 + lane));
+    };
+    issue(itb, itb < ite);
+    __syncthreads();
+    uint32_t pend = 0, flushed = 0;
+    uint32_t* o = reinterpret_cast<uint32_t*>(out);
+    auto flush = [&]() {
+        for (uint32_t q = lane; q < pend; q += 64)
+            __builtin_nontemporal_store(stage[q], o + region + flushed + q);
+        flushed += pend;
+        pend = 0;
+    };
+    auto stage_it = [&](uint32_t g1m, uint32_t rel) {
+        if (__ballot(g1m != 0) == 0) return;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const bool g1 = (g1m >> k) & 1u;
+            const uint64_t b1 = __ballot(g1);
+            if (g1) stage[pend + mbcnt64(b1)] = rel + k * 64 + lane;
+            pend += (uint32_t)__popcll(b1);
+            if (pend >= kFlushAt) flush();
+        }
+    };
+    if constexpr (PIPE == 0) {
+        for (uint64_t it = itb; it < ite; ++it) {
+            uint32_t x[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] = nxt[k];
+            uint32_t vmask = 0xFFFFFFFFu;
+            if (it * IE + IE > events) {
+                vmask = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k) vmask |= (it * IE + k * 64 + lane < events ? 1u : 0u) << k;
+            }
+            uint32_t fw[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) fw[k] = s_filter[(x[k] >> 5) & (FW - 1)];
+            uint32_t fm = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) fm |= ((fw[k] >> (x[k] & 31u)) & 1u) << k;
+            fm &= vmask;
+            uint32_t cw[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                cw[k] = 0u;
+                if ((fm >> k) & 1u) cw[k] = bitmap[x[k] >> 5];
+            }
+            issue(it + 1, it + 1 < ite);
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t g1m = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) g1m |= ((cw[k] >> (x[k] & 31u)) & 1u) << k;
+            stage_it(g1m, (uint32_t)(it * IE - region));
+        }
+    } else {
+        uint32_t pcw[K], prel = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) pcw[k] = 0;
+        for (uint64_t it = itb; it <= ite; ++it) {
+            uint32_t x[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] = nxt[k];
+            const bool live = it < ite;
+            issue(it + 1, it + 1 < ite);
+            __builtin_amdgcn_sched_barrier(0);
+            // pcw[k] already holds the confirmed bit (shifted down) of iteration it-1
+            uint32_t g1m = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) g1m |= (pcw[k] & 1u) << k;
+            stage_it(g1m, prel);
+            if (!live) break;
+            uint32_t vmask = 0xFFFFFFFFu;
+            if (it * IE + IE > events) {
+                vmask = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k) vmask |= (it * IE + k * 64 + lane < events ? 1u : 0u) << k;
+            }
+            uint32_t fw[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) fw[k] = s_filter[(x[k] >> 5) & (FW - 1)];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                // the bit position rides in the low 5 bits of x: keep it beside the word
+                const bool hit = ((fw[k] >> (x[k] & 31u)) & 1u) && ((vmask >> k) & 1u);
+                pcw[k] = 0u;
+                if (hit) pcw[k] = bitmap[x[k] >> 5] >> (x[k] & 31u);
+            }
+            prel = (uint32_t)(it * IE - region);
+        }
+    }
+    flush();
+    if (lane == 0) tot[r] = flushed;
+}
+
 __global__ void k_fill(uint4* syn, uint64_t n, uint32_t n_nrn)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
@@ -325,6 +554,24 @@ void launch_pipe(int grid, const uint4* syn, uint64_t ev, uint32_t iters, const 
                        out + ev, out, tot);
 }
 
+template <int BLOCK, int K, int FLAGS>
+void launch_pipe4(int grid, const uint4* syn, uint64_t ev, uint32_t iters, const uint32_t* bm,
+                  const uint32_t* f, const uint64_t* lf, uint4* out, uint32_t* tot, uint64_t now)
+{
+    (void)lf; (void)now;
+    hipLaunchKernelGGL((k_pipe4<BLOCK, K, FLAGS>), dim3(grid), dim3(BLOCK), 0, 0, syn, ev, iters, bm, f,
+                       out + ev, out, tot);
+}
+
+template <int BLOCK, int K, int PIPE>
+void launch_x(int grid, const uint4* syn, uint64_t ev, uint32_t iters, const uint32_t* bm,
+              const uint32_t* f, const uint64_t* lf, uint4* out, uint32_t* tot, uint64_t now)
+{
+    (void)lf; (void)now;
+    hipLaunchKernelGGL((k_x<BLOCK, K, PIPE>), dim3(grid), dim3(BLOCK), 0, 0, syn, ev, iters, bm, f,
+                       out + ev, out, tot);
+}
+
 struct Var {
     const char* name;
     void (*launch)(int, const uint4*, uint64_t, uint32_t, const uint32_t*, const uint32_t*,
@@ -343,6 +590,8 @@ void launch_var(int grid, const uint4* syn, uint64_t ev, uint32_t iters, const u
 #define V(B, K, FL, PF, NAME) Var{NAME, launch_var<B, K, FL, PF>, B, K}
 #define P(B, K, FL, NAME) Var{NAME, launch_prod<B, K, FL>, B, K}
 #define Q(B, K, FL, NAME) Var{NAME, launch_pipe<B, K, FL>, B, K}
+#define Q4(B, K, FL, NAME) Var{NAME, launch_pipe4<B, K, FL>, B, K}
+#define X(B, K, PIPE, NAME) Var{NAME, launch_x<B, K, PIPE>, B, K}
 
 int main()
 {
@@ -352,7 +601,7 @@ int main()
     uint4 *syn, *out;
     uint32_t *bm, *filt, *tot;
     uint64_t* lastF;
-    CK(hipMalloc(&syn, n * 16));
+    CK(hipMalloc(&syn, (n + 4096) * 16));  // padded: the x-only loop reads past the end
     CK(hipMalloc(&out, n * 16 + 65536));
     CK(hipMemset(out, 0, n * 16 + 65536));
     CK(hipMalloc(&bm, nwords * 4 + 64));
@@ -380,14 +629,15 @@ int main()
 
     std::vector<Var> vars = {
         V(512, 8, 0, 1, "512x8 stream pf1"),
-        V(256, 8, 0, 1, "256x8 stream pf1"),
-        P(512, 8, F_STAGE | F_SKIP, "prod 512x8"),
-        P(256, 8, F_STAGE | F_SKIP, "prod 256x8"),
-        P(256, 16, F_STAGE | F_SKIP, "prod 256x16"),
-        Q(256, 8, 0, "pipe 256x8"),
-        Q(256, 16, 0, "pipe 256x16"),
-        Q(256, 4, 0, "pipe 256x4"),
-        Q(256, 8, 0, "pipe 256x8 again"),
+        P(512, 8, F_STAGE | F_SKIP, "prod"),
+        X(512, 8, 0, "x 512x8"),
+        X(512, 16, 0, "x 512x16"),
+        X(512, 8, 1, "x pipe 512x8"),
+        X(512, 16, 1, "x pipe 512x16"),
+        X(1024, 8, 1, "x pipe 1024x8"),
+        X(512, 32, 1, "x pipe 512x32"),
+        V(512, 8, 0, 1, "512x8 stream pf1 again"),
+        P(512, 8, F_STAGE | F_SKIP, "prod again"),
     };
     int cus = 256;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
