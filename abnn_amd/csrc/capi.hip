@@ -88,10 +88,10 @@ void free_all(abnn_brain* b)
     if (!b) return;
     (void)hipSetDevice(b->device);
     void* ptrs[] = {b->d.syn,       b->d.last_fired, b->d.last_visited,  b->scalar_block,
-                    b->d.bitmap,    b->d.filter,     b->d.range_cnt,     b->d.range_tile0,
+                    b->d.bitmap,    b->d.filter,     b->d.range_cnt,     b->d.tile_desc,
                     b->d.tile_mask, b->d.tile_pre,   b->d.g1idx,    b->d.g2e,         b->d.apply_partial,
                     b->d.fired,     b->d.summary,    b->d.work,          b->idx_scratch,
-                    b->u64_scratch,  b->d.tile_range,  const_cast<uint4*>(b->d.dummy)};
+                    b->u64_scratch,  const_cast<uint4*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : b->events) {
@@ -268,8 +268,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     REQUIRE(p.max_spikes < (1u << 30), "max_spikes too large");
     const uint64_t E = visited_events(*dims);
     // Gate kernel shape: threads per workgroup x events per lane x LDS filter
-    // KiB (ABNN_GATE="512x8f64"; tuning knob, the default is the measured best).
-    uint32_t gate_block = 512, gate_k = 8, filter_kib = 64;
+    // KiB (ABNN_GATE="512x8f32"; tuning knob, the default is the measured best).
+    uint32_t gate_block = 512, gate_k = 8, filter_kib = 32;
     if (const char* env = std::getenv("ABNN_GATE")) {
         unsigned gb = 0, gk = 0, fk = 0;
         const int got = std::sscanf(env, "%ux%uf%u", &gb, &gk, &fk);
@@ -352,10 +352,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.filter, kMaxFilterWords)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_cnt, d.n_ranges)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.range_tile0, d.n_ranges)) != ABNN_OK) return fail(s);
     const uint64_t max_tiles = E / kTile + d.n_ranges + 1;
     if ((s = dalloc(&d.tile_mask, max_tiles)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.tile_range, max_tiles)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.tile_desc, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.tile_pre, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.g1idx, iters * iter_events)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.g2e, max_tiles * kTile)) != ABNN_OK) return fail(s);

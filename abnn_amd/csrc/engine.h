@@ -44,8 +44,7 @@ struct DeviceState {
     uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
     uint32_t* filter;         // [filter_words] folded bitmap
     uint32_t* range_cnt;      // [n_ranges] pre-gated entries of each range
-    uint32_t* range_tile0;    // [n_ranges] first entry tile of each range
-    uint32_t* tile_range;     // [max_tiles] range of each tile
+    uint4* tile_desc;         // [max_tiles] {range, first entry in the range, entries, 0}
     uint4* tile_mask;         // [max_tiles] {passed refractory, spike candidate} lane masks (2 x u64)
     uint32_t* tile_pre;       // [max_tiles] exclusive candidate prefix (capped; = budget: skip)
     uint32_t* g1idx;          // [iters * iter_events] pre-gated event offsets (event - region), per-range regions

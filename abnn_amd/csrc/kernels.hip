@@ -214,6 +214,109 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
 }
 
 // ---------------------------------------------------------------------------
+// Pre-gated entries are processed as tiles of kTile (= 64 = one wave)
+// consecutive entries of one range; tile order = event order;
+// tile_desc[t] = {range, first entry of the tile in its range, entries, 0}.
+// These steps move a few MB per pass: they are bound by dependent-load
+// latency, so every loop below keeps all of a thread's loads in flight at
+// once, scans run on DPP over coalesced chunks, and no tile waits on another.
+
+// Inclusive wave scan on DPP (row_shr within 16-lane rows, then the gfx9
+// row broadcasts): six VALU ops, no LDS crossbar round trips.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+    int v = (int)x;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return (uint32_t)v;
+}
+
+__device__ __forceinline__ uint32_t lane63(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+__device__ __forceinline__ uint32_t tiles_of(uint32_t n) { return (n + kTile - 1) / kTile; }
+
+// Tile descriptors and the pre-gated total, by one workgroup of NT threads.
+// Wave w owns a contiguous block of ranges read as
+// coalesced 64-range chunks (at most 16 with NT = kScanThreads); the chunk scans are recomputed in the second sweep
+// rather than kept.  `lds` is scratch of >= 64 + 3 * kBig words.
+template <int NT>
+__device__ void build_tiles(const DeviceState& d, uint32_t* lds)
+{
+    constexpr uint32_t NWv = NT / 64, kCh = kMaxRanges / NT, kBig = 256;
+    uint32_t* s_wt = lds;                                       // [NWv] tiles per wave
+    uint64_t* s_wg1 = reinterpret_cast<uint64_t*>(lds + 16);    // [NWv] entries per wave
+    uint32_t* s_nbig = lds + 48;
+    uint32_t* s_big = lds + 64;                                 // {range, first tile, entries} x kBig
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = wave_uniform(tid >> 6), NR = d.n_ranges;
+    const uint32_t per = ((NR + NWv - 1) / NWv + 63) & ~63u, nch = per / 64;
+    if (tid == 0) *s_nbig = 0;
+    uint32_t cnt[kCh];
+#pragma unroll
+    for (uint32_t c = 0; c < kCh; ++c) {
+        const uint32_t r = w * per + c * 64 + lane;
+        cnt[c] = (c < nch && r < NR) ? d.range_cnt[r] : 0u;
+    }
+    uint32_t run = 0;
+    uint64_t g1 = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kCh; ++c) {
+        run += lane63(wave_incl_scan(tiles_of(cnt[c])));
+        g1 += cnt[c];
+    }
+    g1 = wave_sum(g1);
+    if (lane == 0) {
+        s_wt[w] = run;
+        s_wg1[w] = g1;
+    }
+    __syncthreads();
+    uint32_t off = 0, total = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < NWv; ++v) {
+        off += v < w ? s_wt[v] : 0u;
+        total += s_wt[v];
+    }
+    run = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kCh; ++c) {
+        const uint32_t r = w * per + c * 64 + lane;
+        const uint32_t n = cnt[c], nt = tiles_of(n), x = wave_incl_scan(nt);
+        const uint32_t t0 = off + run + x - nt;
+        run += lane63(x);
+        uint32_t q = 0;
+        if (nt > 4) {  // long ranges (the dense input block) are filled cooperatively
+            const uint32_t slot = atomicAdd(s_nbig, 1u);
+            if (slot < kBig) {
+                s_big[3 * slot] = r;
+                s_big[3 * slot + 1] = t0;
+                s_big[3 * slot + 2] = n;
+                q = nt;
+            }
+        }
+        for (; q < nt; ++q) d.tile_desc[t0 + q] = make_uint4(r, q * kTile, min(n - q * kTile, (uint32_t)kTile), 0u);
+    }
+    __syncthreads();
+    const uint32_t nbig = min(*s_nbig, kBig);
+    for (uint32_t b = 0; b < nbig; ++b) {
+        const uint32_t r = s_big[3 * b], t0 = s_big[3 * b + 1], n = s_big[3 * b + 2], nt = tiles_of(n);
+        for (uint32_t q = tid; q < nt; q += NT)
+            d.tile_desc[t0 + q] = make_uint4(r, q * kTile, min(n - q * kTile, (uint32_t)kTile), 0u);
+    }
+    if (tid == 0) {
+        uint64_t tg1 = 0;
+        for (uint32_t v = 0; v < NWv; ++v) tg1 += s_wg1[v];
+        d.work->total_tiles = total;
+        d.work->g1 = tg1;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_gate: the streaming kernel (see file header).  Every wave owns one
 // contiguous range of events.  The pre-spike gate reads only the src word of
 // each 16-B record (the same lines stream from HBM; one register per event
@@ -341,81 +444,19 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     if (lane == 0) d.range_cnt[r] = flushed;
 }
 
-// ---------------------------------------------------------------------------
-// Pre-gated entries are processed as tiles of kTile (= 64 = one wave)
-// consecutive entries of one range; tile order = event order; tile_range[t]
-// names the range.  These kernels move a few MB per pass: they are bound by
-// dependent-load latency, so every loop below keeps all of a thread's loads
-// in flight at once and no tile waits on another.
-//
-// k_tiles: one workgroup: first tile of every range, the tile -> range map and
-// the pre-gated total.  All range counts are staged in LDS first.
+// k_tiles: one workgroup builds the tile descriptors (build_tiles).
 __global__ __launch_bounds__(kScanThreads) void k_tiles(DeviceState d)
 {
-    constexpr uint32_t kPer = kMaxRanges / kScanThreads;  // ranges per thread
-    constexpr uint32_t kBig = 256;                        // ranges filled by the whole workgroup
-    __shared__ uint32_t s_cnt[kMaxRanges];
-    __shared__ uint64_t s_wave[kScanThreads / 64], s_red[kScanThreads / 64];
-    __shared__ uint32_t s_big[kBig], s_big_t0[kBig], s_nbig;
-    const uint32_t tid = threadIdx.x, NR = d.n_ranges;
-    if (tid == 0) s_nbig = 0;
-    uint32_t v[kPer];
-#pragma unroll
-    for (uint32_t u = 0; u < kPer; ++u) {
-        const uint32_t i = u * kScanThreads + tid;
-        v[u] = i < NR ? d.range_cnt[i] : 0u;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kPer; ++u) s_cnt[u * kScanThreads + tid] = v[u];
-    __syncthreads();
-    const uint32_t lo = tid * kPer;  // contiguous ranges per thread: scan order
-    uint64_t tiles = 0, g1 = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < kPer; ++u) {
-        const uint32_t c = s_cnt[lo + u];
-        g1 += c;
-        tiles += (c + kTile - 1) / kTile;
-    }
-    uint64_t total;
-    uint64_t t0 = block_exclusive_scan(tiles, &total, s_wave);
-#pragma unroll 1
-    for (uint32_t u = 0; u < kPer && lo + u < NR; ++u) {
-        const uint32_t r = lo + u, nt = (s_cnt[r] + kTile - 1) / kTile;
-        d.range_tile0[r] = (uint32_t)t0;
-        uint32_t q = 0;
-        if (nt > 4) {  // long ranges (the dense input block) are filled cooperatively
-            const uint32_t slot = atomicAdd(&s_nbig, 1u);
-            if (slot < kBig) {
-                s_big[slot] = r;
-                s_big_t0[slot] = (uint32_t)t0;
-                q = nt;
-            }
-        }
-        for (; q < nt; ++q) d.tile_range[t0 + q] = r;
-        t0 += nt;
-    }
-    const uint64_t wg1 = wave_sum(g1);
-    if ((tid & 63) == 0) s_red[tid >> 6] = wg1;
-    __syncthreads();
-    const uint32_t nbig = min(s_nbig, kBig);
-    for (uint32_t b = 0; b < nbig; ++b) {
-        const uint32_t r = s_big[b], tb = s_big_t0[b], nt = (s_cnt[r] + kTile - 1) / kTile;
-        for (uint32_t q = tid; q < nt; q += kScanThreads) d.tile_range[tb + q] = r;
-    }
-    if (tid == 0) {
-        uint64_t tg1 = 0;
-        for (int w = 0; w < kScanThreads / 64; ++w) tg1 += s_red[w];
-        d.work->total_tiles = (uint32_t)total;
-        d.work->g1 = tg1;
-    }
+    __shared__ uint32_t s_scratch[64 + 3 * 256];
+    build_tiles<kScanThreads>(d, s_scratch);
 }
 
 // k_refrac: one wave per tile.  Per pre-gated entry the refractory gate with a
 // real 8-B gather of lastFired[dst] (brain.metal:79-83), the spike-candidate
-// test (brain.metal:91-92) and the homeostasis input isi (brain.metal:116,
-// into the entry's fourth word); per tile the two lane masks and, for the
-// events that passed, the entry {offset, dst, w, isi} at the tile's slot.  The gate is
-// done with the filter image, so it is zeroed here for the next k_bitmap.
+// test (brain.metal:91-92) and the homeostasis input isi (brain.metal:116);
+// per tile the two lane masks and, for the events that passed, the entry
+// {offset, dst, w, isi} at the tile's slot.  The gate is done with the filter
+// image, so it is zeroed here for the next k_bitmap.
 __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
 {
     const uint32_t lane = threadIdx.x & 63, gtid = blockIdx.x * 256 + threadIdx.x;
@@ -425,11 +466,10 @@ __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
     const uint32_t T = d.work->total_tiles;
     const uint32_t nn = (uint32_t)d.n_nrn;
     for (uint32_t tile = wave; tile < T; tile += nwaves) {
-        const uint32_t r = d.tile_range[tile];
-        const uint32_t j = (tile - d.range_tile0[r]) * kTile + lane;
-        const uint64_t region = range_begin(r, d.iters, d.n_ranges) * d.iter_events;
-        bool valid = j < d.range_cnt[r];
-        const uint32_t rel = valid ? d.g1idx[region + j] : 0u;
+        const uint4 td = d.tile_desc[tile];
+        const uint64_t region = range_begin(td.x, d.iters, d.n_ranges) * d.iter_events;
+        bool valid = lane < td.z;
+        const uint32_t rel = valid ? d.g1idx[region + td.y + lane] : 0u;
         // the gate kept only the event offset: dst and w come from the record
         const uint4 rec = valid ? d.syn[region + rel] : make_uint4(0u, 0u, 0u, 0u);
         valid = valid && rec.y < nn;
@@ -446,56 +486,64 @@ __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
 }
 
 // ---------------------------------------------------------------------------
-// k_scan: ordered spike budget over the tiles (one workgroup, in event order),
-// in chunks of kScanThreads x kSpt tiles whose counts are staged in LDS.
+// k_scan: ordered spike budget over the tiles (one workgroup, in event order).
+// Up to kSuper tiles per round: wave w scans a contiguous block of 64-tile
+// chunks held in registers; rounds carry the prefix (warm-up passes only).
 __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelParams kp,
                                                        int64_t* summary_out)
 {
-    constexpr uint32_t kSpt = 8, kChunk = kScanThreads * kSpt;
-    __shared__ uint32_t s_c[kChunk];  // candidates | passed-refractory << 16, per tile
-    __shared__ uint64_t s_wave[kScanThreads / 64], s_red[kScanThreads / 64];
-    const uint32_t tid = threadIdx.x, T = d.work->total_tiles;
+    constexpr uint32_t NWv = kScanThreads / 64, kCh = 16, kSuper = NWv * kCh * 64;
+    __shared__ uint32_t s_wt[NWv];
+    __shared__ uint64_t s_red[NWv];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = wave_uniform(tid >> 6);
+    const uint32_t T = d.work->total_tiles;
     const uint64_t budget = kp.max_spikes;
     uint64_t carry = 0, g2 = 0;
-    for (uint32_t base = 0; base < T; base += kChunk) {
-        uint4 m[kSpt];
+    for (uint32_t base = 0; base < T; base += kSuper) {
+        const uint32_t n = min(T - base, kSuper);
+        const uint32_t per = ((n + NWv - 1) / NWv + 63) & ~63u, nch = per / 64;
+        uint32_t cg[kCh];  // candidates | passed-refractory << 16, per tile
 #pragma unroll
-        for (uint32_t u = 0; u < kSpt; ++u) {
-            const uint32_t i = base + u * kScanThreads + tid;
-            m[u] = i < T ? d.tile_mask[i] : make_uint4(0u, 0u, 0u, 0u);
+        for (uint32_t c = 0; c < kCh; ++c) {
+            const uint32_t i = w * per + c * 64 + lane;
+            const uint4 m = (c < nch && i < n) ? d.tile_mask[base + i] : make_uint4(0u, 0u, 0u, 0u);
+            cg[c] = (uint32_t)(__popc(m.z) + __popc(m.w)) | ((uint32_t)(__popc(m.x) + __popc(m.y)) << 16);
         }
+        uint32_t excl[kCh], run = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < kSpt; ++u)
-            s_c[u * kScanThreads + tid] = (uint32_t)(__popc(m[u].z) + __popc(m[u].w)) |
-                                          ((uint32_t)(__popc(m[u].x) + __popc(m[u].y)) << 16);
+        for (uint32_t c = 0; c < kCh; ++c) {
+            const uint32_t x = cg[c] & 0xFFFFu, inc = wave_incl_scan(x);
+            excl[c] = run + inc - x;
+            run += lane63(inc);
+            g2 += cg[c] >> 16;
+        }
+        if (lane == 0) s_wt[w] = run;
         __syncthreads();
-        const uint32_t lo = tid * kSpt;
-        uint32_t cv[kSpt];
-        uint64_t cs = 0;
+        uint64_t off = carry, tot = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < kSpt; ++u) {
-            cv[u] = s_c[lo + u];
-            cs += cv[u] & 0xFFFFu;
-            g2 += cv[u] >> 16;
+        for (uint32_t v = 0; v < NWv; ++v) {
+            off += v < w ? s_wt[v] : 0u;
+            tot += s_wt[v];
         }
-        uint64_t tot;
-        uint64_t pre = carry + block_exclusive_scan(cs, &tot, s_wave);  // syncs: s_c is free after
 #pragma unroll
-        for (uint32_t u = 0; u < kSpt; ++u) {
-            const uint32_t t = base + lo + u;
-            // a tile is applied iff some event in it passed the refractory gate
-            // while the budget lasted; inactive tiles carry the budget itself
-            if (t < T) d.tile_pre[t] = (uint32_t)((cv[u] >> 16) > 0 && pre < budget ? pre : budget);
-            pre += cv[u] & 0xFFFFu;
+        for (uint32_t c = 0; c < kCh; ++c) {
+            const uint32_t i = w * per + c * 64 + lane;
+            if (c < nch && i < n) {
+                const uint64_t pre = off + excl[c];
+                // a tile is applied iff some event in it passed the refractory
+                // gate while the budget lasted; inactive tiles carry the budget
+                d.tile_pre[base + i] = (uint32_t)((cg[c] >> 16) > 0 && pre < budget ? pre : budget);
+            }
         }
         carry += tot;
+        __syncthreads();  // s_wt is rewritten by the next round
     }
     const uint64_t wg2 = wave_sum(g2);
-    if ((tid & 63) == 0) s_red[tid >> 6] = wg2;
+    if (lane == 0) s_red[w] = wg2;
     __syncthreads();
     if (tid == 0) {
         uint64_t tg2 = 0;
-        for (int w = 0; w < kScanThreads / 64; ++w) tg2 += s_red[w];
+        for (uint32_t v = 0; v < NWv; ++v) tg2 += s_red[v];
         const uint64_t capped = carry < budget ? carry : budget;
         const uint32_t t0 = d.work->t0_g2;
         summary_out[0] = (int64_t)capped;
@@ -534,8 +582,7 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
         if (!((bg >> lane) & 1u)) continue;   // no entry, or stopped by the refractory gate
         const uint64_t pre = P + mbcnt64(bc);  // spike candidates before this event
         if (pre >= budget) continue;           // budget == 0 at this event: brain.metal:85-88
-        const uint32_t r = d.tile_range[tile];
-        const uint64_t region = range_begin(r, d.iters, d.n_ranges) * d.iter_events;
+        const uint64_t region = range_begin(d.tile_desc[tile].x, d.iters, d.n_ranges) * d.iter_events;
         const uint4 e = d.g2e[(uint64_t)tile * kTile + lane];
         const bool f = (bc >> lane) & 1u;
         const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.w));
@@ -767,7 +814,7 @@ hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream
 
 hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s)
 {
-    if (d.gate_blocks == 0) return hipSuccess;
+    if (d.gate_blocks == 0) return hipSuccess;  // no events: n_ranges = 0, k_tiles writes no tiles
     switch (shape_key(d.gate_block, d.gate_k, d.filter_words)) {
 #define X(B, K, F) case shape_key(B, K, F): return launch_gate_shape<B, K, F>(d, kp, s);
         ABNN_GATE_SHAPES(X)
