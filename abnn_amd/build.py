@@ -24,6 +24,10 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
 CPP_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "brain_cpp_test.cpp")
 CPP_TEST_BIN = os.path.join(ROOT, "tests", "cpp", "brain_cpp_test")
+ENGINE_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "engine_test.cpp")
+ENGINE_TEST_BIN = os.path.join(ROOT, "tests", "cpp", "engine_test")
+ENGINE_HOST_SRC = os.path.join(ROOT, "tests", "cpp", "engine_host_test.cpp")
+ENGINE_HOST_BIN = os.path.join(ROOT, "tests", "cpp", "engine_host_test")
 
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
@@ -73,10 +77,38 @@ def build_cpp_example(force: bool = False) -> str | None:
     return CPP_TEST_BIN
 
 
+def build_engine_tests(force: bool = False) -> tuple[str | None, str | None]:
+    """Test programs of the learning driver (include/abnn/engine.hpp): the
+    CPU-only known-answer program, and the GPU-vs-oracle driver run (links the
+    oracle's C restatement -- test infrastructure, like the program itself)."""
+    inc = os.path.join(ROOT, "include")
+    hdrs = [os.path.join(inc, "abnn", "engine.hpp"), os.path.join(inc, "abnn", "brain.hpp")]
+    host = None
+    if os.path.exists(ENGINE_HOST_SRC):
+        if force or _stale(ENGINE_HOST_BIN, [ENGINE_HOST_SRC, *hdrs]):
+            _run(["g++", "-O2", "-std=c++17", "-Wall", "-ffp-contract=off", "-I", inc,
+                  "-o", ENGINE_HOST_BIN, ENGINE_HOST_SRC])
+        host = ENGINE_HOST_BIN
+    gpu = None
+    if os.path.exists(ENGINE_TEST_SRC):
+        osrc = os.path.join(ORACLE_DIR, "c1_oracle.c")
+        deps = [ENGINE_TEST_SRC, os.path.join(ROOT, "tests", "cpp", "oracle_brain.hpp"), osrc, LIB, *hdrs]
+        if force or _stale(ENGINE_TEST_BIN, deps):
+            obj = ENGINE_TEST_BIN + ".oracle.o"
+            _run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-pthread", "-c", "-o", obj, osrc])
+            _run(["g++", "-O2", "-std=c++17", "-Wall", "-ffp-contract=off", "-pthread", "-I", inc,
+                  "-o", ENGINE_TEST_BIN, ENGINE_TEST_SRC, obj, "-L", PKG, "-labnn_hip",
+                  f"-Wl,-rpath,{PKG}", "-Wl,-rpath,$ORIGIN/../../abnn_amd"])
+            os.remove(obj)
+        gpu = ENGINE_TEST_BIN
+    return host, gpu
+
+
 def build_all(force: bool = False) -> None:
     build_hip(force)
     build_oracle(force)
     build_cpp_example(force)
+    build_engine_tests(force)
 
 
 if __name__ == "__main__":

@@ -154,10 +154,11 @@ public:
         check(abnn_get_scalars(h_, &s), "abnn_get_scalars");
         return s;
     }
-    std::vector<uint64_t> last_fired() const
+    std::vector<uint64_t> last_fired() const { return last_fired(0, n_neuron()); }
+    std::vector<uint64_t> last_fired(uint64_t first, uint64_t n) const
     {
-        std::vector<uint64_t> v(n_neuron());
-        check(abnn_get_last_fired(h_, 0, v.data(), v.size()), "abnn_get_last_fired");
+        std::vector<uint64_t> v(n);
+        check(abnn_get_last_fired(h_, first, v.data(), n), "abnn_get_last_fired");
         return v;
     }
     uint64_t checksum() const
