@@ -51,13 +51,18 @@ class Params(C.Structure):
         ("tau_pre", C.c_uint32),
         ("renorm_thresh", C.c_uint64),
         ("track_visits", C.c_uint32),
-        ("reserved0", C.c_uint32),
+        ("mode", C.c_uint32),
         ("seed", C.c_uint64),
     ]
 
 
 class Scalars(C.Structure):
-    _fields_ = [("clock", C.c_uint64), ("reward", C.c_float), ("rbar", C.c_float)]
+    _fields_ = [("clock", C.c_uint64), ("reward", C.c_float), ("rbar", C.c_float),
+                ("pass_index", C.c_uint64)]
+
+
+MODE_SWEEP, MODE_RANDOM = 0, 1  # abnn_params.mode (include/abnn/abnn.h)
+ABI_VERSION = 2
 
 
 class Stats(C.Structure):
@@ -171,7 +176,7 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)  # AttributeError = the ABI is not exported
         fn.restype = res
         fn.argtypes = args
-    if lib.abnn_abi_version() != 1:
+    if lib.abnn_abi_version() != ABI_VERSION:
         raise ImportError("libabnn_hip.so ABI version mismatch")
     _lib = lib
     return lib

@@ -21,8 +21,11 @@ from ._lib import Dims, Params, Scalars, State, Stats, call
 SYN_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("w", "<f4"), ("pad", "<f4")])
 
 
-def visited_events(events_per_pass: int, n_syn: int) -> int:
-    """min(roundup(EVENTS,256), nSyn) -- brain.cpp:116-118 with brain.metal:60-61."""
+def visited_events(events_per_pass: int, n_syn: int, mode: int = 0) -> int:
+    """Sweep: min(roundup(EVENTS,256), nSyn) -- brain.cpp:116-118 with
+    brain.metal:60-61.  Random mode: exactly EVENTS picks (README §4)."""
+    if mode == _lib.MODE_RANDOM:
+        return int(events_per_pass) if int(n_syn) else 0
     grid = (int(events_per_pass) + 255) // 256 * 256
     return min(grid, int(n_syn))
 
@@ -101,7 +104,7 @@ class Brain:
         return self._params
 
     def visited_events(self) -> int:
-        return visited_events(self._dims.events_per_pass, self._dims.n_syn)
+        return visited_events(self._dims.events_per_pass, self._dims.n_syn, self._params.mode)
 
     def state_ptrs(self) -> dict:
         s = State()
@@ -156,10 +159,13 @@ class Brain:
     def scalars(self) -> dict:
         s = Scalars()
         call("abnn_get_scalars", self._h, C.byref(s))
-        return {"clock": int(s.clock), "reward": float(s.reward), "rbar": float(s.rbar)}
+        return {"clock": int(s.clock), "reward": float(s.reward), "rbar": float(s.rbar),
+                "pass_index": int(s.pass_index)}
 
-    def set_scalars(self, clock: int, reward: float, rbar: float) -> None:
-        s = Scalars(clock, reward, rbar)
+    def set_scalars(self, clock: int, reward: float, rbar: float, pass_index: Optional[int] = None) -> None:
+        if pass_index is None:
+            pass_index = self.scalars()["pass_index"]
+        s = Scalars(clock, reward, rbar, pass_index)
         call("abnn_set_scalars", self._h, C.byref(s))
 
     def set_reward(self, r: float) -> None:

@@ -36,8 +36,9 @@ void set_err(const std::string& m) { g_err = m; }
         }                                                                              \
     } while (0)
 
-uint64_t visited_events(const abnn_dims& d)
+uint64_t visited_events(const abnn_dims& d, uint32_t mode)
 {
+    if (mode == ABNN_MODE_RANDOM) return d.n_syn ? d.events_per_pass : 0;  // README §4: EVENTS picks
     uint64_t grid = (d.events_per_pass + 255u) / 256u * 256u;  // brain.cpp:116-118
     return grid < d.n_syn ? grid : d.n_syn;                     // brain.metal:61
 }
@@ -90,6 +91,7 @@ void free_all(abnn_brain* b)
     void* ptrs[] = {b->d.syn,       b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->d.bitmap,    b->d.filter,     b->d.range_cnt,     b->d.tile_desc,
                     b->d.tile_mask, b->d.tile_pre,   b->d.g1idx,    b->d.g2e,         b->d.apply_partial,
+                    b->d.claim,
                     b->d.fired,     b->d.summary,    b->d.work,          b->idx_scratch,
                     b->u64_scratch,  const_cast<uint4*>(b->d.dummy)};
     for (void* p : ptrs)
@@ -266,7 +268,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (params) p = *params;
     else abnn_default_params(&p);
     REQUIRE(p.max_spikes < (1u << 30), "max_spikes too large");
-    const uint64_t E = visited_events(*dims);
+    REQUIRE(p.mode == ABNN_MODE_SWEEP || p.mode == ABNN_MODE_RANDOM, "unknown mode");
+    const uint64_t E = visited_events(*dims, p.mode);
+    REQUIRE(p.mode != ABNN_MODE_RANDOM || E < 0xFFFFFFFFull, "random mode: events per pass must fit u32");
     // Gate kernel shape: threads per workgroup x events per lane x LDS filter
     // KiB (ABNN_GATE="512x8f32"; tuning knob, the default is the measured best).
     uint32_t gate_block = 512, gate_k = 8, filter_kib = 32;
@@ -315,6 +319,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.n_nrn = n_nrn;
     d.events = E;
     d.syn_offset = dims->syn_offset;
+    d.seed = p.seed;
+    d.mode = p.mode;
     d.gate_block = gate_block;
     d.gate_k = gate_k;
     d.iter_events = (uint32_t)iter_events;
@@ -324,7 +330,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
         cus = 256;
     // one wave of persistent workgroups: as many as are resident (each keeps the
     // 64 KiB filter in LDS, so at most two per CU)
-    int per_cu = gate_blocks_per_cu(gate_block, gate_k, filter_words, p.track_visits != 0);
+    int per_cu = gate_blocks_per_cu(gate_block, gate_k, filter_words, p.track_visits != 0,
+                                    p.mode == ABNN_MODE_RANDOM);
     if (per_cu <= 0) per_cu = 1;
     if (per_cu > 4) per_cu = 4;
     uint64_t G = std::min<uint64_t>(iters, std::min<uint64_t>((uint64_t)cus * per_cu, kMaxGateBlocks));
@@ -344,11 +351,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.last_fired, n_nrn)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_visited, n_nrn)) != ABNN_OK) return fail(s);
     uint64_t* sb = nullptr;
-    if ((s = dalloc(&sb, 2)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&sb, 3)) != ABNN_OK) return fail(s);  // {clock, reward|rbar, pass_index}
     b->scalar_block = sb;
     d.clock = sb;
     d.reward = reinterpret_cast<float*>(sb + 1);
     d.rbar = d.reward + 1;
+    d.pass_index = sb + 2;
     if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.filter, kMaxFilterWords)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_cnt, d.n_ranges)) != ABNN_OK) return fail(s);
@@ -362,6 +370,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
     d.dummy = dummy;
     if ((s = dalloc(&d.apply_partial, kTileBlocks)) != ABNN_OK) return fail(s);
+    if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, dims->n_syn)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.fired, p.max_spikes + 1u)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.summary, ABNN_SUMMARY_WORDS)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
@@ -503,11 +512,12 @@ abnn_status abnn_get_scalars(abnn_brain* b, abnn_scalars* out)
 {
     REQUIRE(b && out, "null argument");
     ST_TRY(sync_all(b));
-    uint64_t blk[2];
+    uint64_t blk[3];
     HIP_TRY(hipMemcpy(blk, b->scalar_block, sizeof(blk), hipMemcpyDeviceToHost));
     out->clock = blk[0];
     std::memcpy(&out->reward, reinterpret_cast<char*>(blk) + 8, 4);
     std::memcpy(&out->rbar, reinterpret_cast<char*>(blk) + 12, 4);
+    out->pass_index = blk[2];
     return ABNN_OK;
 }
 
@@ -515,10 +525,11 @@ abnn_status abnn_set_scalars(abnn_brain* b, const abnn_scalars* in)
 {
     REQUIRE(b && in, "null argument");
     ST_TRY(sync_all(b));
-    uint64_t blk[2];
+    uint64_t blk[3];
     blk[0] = in->clock;
     std::memcpy(reinterpret_cast<char*>(blk) + 8, &in->reward, 4);
     std::memcpy(reinterpret_cast<char*>(blk) + 12, &in->rbar, 4);
+    blk[2] = in->pass_index;
     HIP_TRY(hipMemcpy(b->scalar_block, blk, sizeof(blk), hipMemcpyHostToDevice));
     b->clock_host = in->clock;
     return ABNN_OK;

@@ -39,6 +39,7 @@ struct DeviceState {
     uint64_t* last_fired;     // [n_nrn]
     uint64_t* last_visited;   // [n_nrn]
     uint64_t* clock;          // [1]
+    uint64_t* pass_index;     // [1] passes run (keys the random-mode picks)
     float* reward;            // [1]
     float* rbar;              // [1]
     uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
@@ -51,6 +52,7 @@ struct DeviceState {
     uint4* g2e;               // [max_tiles * kTile] {event - region, dst, w, isi} of the events that passed
     const uint4* dummy;       // [kDummyRecords] zero records: target of masked-off stream loads
     uint2* apply_partial;     // [kTileBlocks] {updated, fired} per apply workgroup
+    uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     int32_t* fired;           // [max_spikes] internal spike list (world = 1)
     int64_t* summary;         // [ABNN_SUMMARY_WORDS] internal (world = 1)
     PassWork* work;
@@ -58,6 +60,8 @@ struct DeviceState {
     uint64_t n_nrn;
     uint64_t events;          // visited events per pass (local)
     uint64_t syn_offset;
+    uint64_t seed;            // random-mode pick key (abnn_params.seed)
+    uint32_t mode;            // ABNN_MODE_SWEEP / ABNN_MODE_RANDOM
     uint32_t n_bitmap_words;  // 2 * ceil(n_nrn / 64)
     uint32_t filter_words;    // LDS filter size (a power of two, compiled per gate shape)
     uint32_t filter_exact;    // bitmap fits the filter: no global confirmation
@@ -81,7 +85,7 @@ KernelParams to_kernel_params(const abnn_params& p);
 // Gate kernel shapes compiled in (threads per workgroup x events per thread).
 bool gate_shape_supported(uint32_t block, uint32_t k, uint32_t filter_words);
 // Resident gate workgroups per CU for a shape (occupancy API; 0 on failure).
-int gate_blocks_per_cu(uint32_t block, uint32_t k, uint32_t filter_words, bool track);
+int gate_blocks_per_cu(uint32_t block, uint32_t k, uint32_t filter_words, bool track, bool random);
 
 // Launchers (all asynchronous on `s`).
 hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,

@@ -124,6 +124,35 @@ __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k)
     return z ^ (z >> 31);
 }
 
+// Random-edge mode pick (include/abnn/abnn.h): Philox4x32-10 of
+// {t, pass} under key seed ^ shard offset, then Lemire multiply-shift onto
+// [0, n_syn).  Only the first two output words are used.
+__device__ __forceinline__ uint64_t pick_record(uint64_t seed, uint64_t stream, uint64_t pass,
+                                                uint64_t t, uint64_t n_syn)
+{
+    uint32_t x0 = (uint32_t)t, x1 = (uint32_t)(t >> 32), x2 = (uint32_t)pass, x3 = (uint32_t)(pass >> 32);
+    const uint64_t k = seed ^ stream;
+    uint32_t k0 = (uint32_t)k, k1 = (uint32_t)(k >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, x0), lo0 = 0xD2511F53u * x0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, x2), lo1 = 0xCD9E8D57u * x2;
+        x0 = hi1 ^ x1 ^ k0;
+        x1 = lo1;
+        x2 = hi0 ^ x3 ^ k1;
+        x3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return __umul64hi(((uint64_t)x1 << 32) | x0, n_syn);
+}
+
+// Record visited by local event t: itself (sweep, brain.metal:70) or its pick.
+__device__ __forceinline__ uint64_t rec_index(const DeviceState& d, uint64_t t, uint64_t pass)
+{
+    return d.mode == ABNN_MODE_RANDOM ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : t;
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z)
 {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -328,7 +357,7 @@ __device__ void build_tiles(const DeviceState& d, uint32_t* lds)
 // 4-B event offsets, kStageEntries per wave, so a wave usually flushes once,
 // at the end of its range (vmcnt retires in issue order, stores included: a
 // store between the prefetch and its wait delays the whole stream).
-template <int BLOCK, int K, int FW, bool kTrack>
+template <int BLOCK, int K, int FW, bool kTrack, bool kRandom>
 __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
     constexpr int NW = BLOCK / 64;
@@ -355,11 +384,23 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     }
 
     Word nxt[K];
+    const uint64_t pass = kRandom ? *d.pass_index : 0;
     auto issue = [&](uint64_t it, bool live) {
-        const uint4* base = live ? d.syn + it * IE : d.dummy;  // wave-uniform
+        if constexpr (kRandom) {  // random-edge mode: a per-lane random record per event
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            nxt[k] = __builtin_nontemporal_load(reinterpret_cast<const Word*>(base + k * 64 + lane));
+            for (int k = 0; k < K; ++k) {
+                const uint64_t t = it * IE + k * 64 + lane;
+                const uint4* p = (live && t < d.events)
+                                     ? d.syn + pick_record(d.seed, d.syn_offset, pass, t, d.n_syn)
+                                     : d.dummy + (k * 64 + lane);
+                nxt[k] = __builtin_nontemporal_load(reinterpret_cast<const Word*>(p));
+            }
+        } else {
+            const uint4* base = live ? d.syn + it * IE : d.dummy;  // wave-uniform
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                nxt[k] = __builtin_nontemporal_load(reinterpret_cast<const Word*>(base + k * 64 + lane));
+        }
     };
     issue(it_begin, it_begin < it_end);
     __syncthreads();
@@ -465,13 +506,14 @@ __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
     const uint64_t now = *d.clock;
     const uint32_t T = d.work->total_tiles;
     const uint32_t nn = (uint32_t)d.n_nrn;
+    const uint64_t pass = *d.pass_index;
     for (uint32_t tile = wave; tile < T; tile += nwaves) {
         const uint4 td = d.tile_desc[tile];
         const uint64_t region = range_begin(td.x, d.iters, d.n_ranges) * d.iter_events;
         bool valid = lane < td.z;
         const uint32_t rel = valid ? d.g1idx[region + td.y + lane] : 0u;
         // the gate kept only the event offset: dst and w come from the record
-        const uint4 rec = valid ? d.syn[region + rel] : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 rec = valid ? d.syn[rec_index(d, region + rel, pass)] : make_uint4(0u, 0u, 0u, 0u);
         valid = valid && rec.y < nn;
         const uint64_t ld = valid ? d.last_fired[rec.y] : 0ull;
         const bool g2 = valid && (now - ld) > (uint64_t)kp.refractory;
@@ -557,6 +599,32 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelPara
 }
 
 // ---------------------------------------------------------------------------
+// k_claim (random mode): every event that will reach the update raises its
+// record's claim to its event index + 1, so k_apply lets only the highest
+// store (the last writer in event order).  Same tile walk as k_apply.
+__global__ __launch_bounds__(256) void k_claim(DeviceState d, KernelParams kp, const int64_t* summaries,
+                                               uint32_t rank)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
+    const uint64_t budget = kp.max_spikes, pass = *d.pass_index;
+    uint64_t off = 0;
+    for (uint32_t q = 0; q < rank; ++q) off += (uint64_t)summaries[q * ABNN_SUMMARY_WORDS + 0];
+    off = off < budget ? off : budget;
+    const uint32_t T = d.work->total_tiles;
+    for (uint32_t tile = wave; tile < T; tile += nwaves) {
+        const uint64_t P = off + d.tile_pre[tile];
+        if (P >= budget) continue;
+        const uint4 m = d.tile_mask[tile];
+        const uint64_t bg = m.x | ((uint64_t)m.y << 32), bc = m.z | ((uint64_t)m.w << 32);
+        if (!((bg >> lane) & 1u) || P + mbcnt64(bc) >= budget) continue;
+        const uint64_t region = range_begin(d.tile_desc[tile].x, d.iters, d.n_ranges) * d.iter_events;
+        const uint64_t t = region + d.g2e[(uint64_t)tile * kTile + lane].x;
+        atomicMax(d.claim + rec_index(d, t, pass), (uint32_t)(t + 1));
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_apply: weight update of the gated events that still had budget; one wave
 // per tile, tiles past the budget skipped on one load.
 __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
@@ -573,6 +641,8 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
     off = off < budget ? off : budget;
 
     const uint32_t T = d.work->total_tiles;
+    const uint64_t pass = *d.pass_index;
+    const bool random = d.mode == ABNN_MODE_RANDOM;
     uint32_t upd = 0, nf = 0;
     for (uint32_t tile = wave; tile < T; tile += nwaves) {
         const uint64_t P = off + d.tile_pre[tile];
@@ -586,11 +656,16 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
         const uint4 e = d.g2e[(uint64_t)tile * kTile + lane];
         const bool f = (bc >> lane) & 1u;
         const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.w));
+        const uint64_t t = region + e.x, ri = rec_index(d, t, pass);
+        // random mode: of the events that updated one synapse this pass, the
+        // highest (k_claim) stores its weight; every one of them still counts
+        const bool store = !random || d.claim[ri] == (uint32_t)(t + 1);
+        if (random && store) d.claim[ri] = 0u;  // re-armed for the next pass
         // brain.metal:122.  Non-temporal: a plain 4-B store leaves ~160k
         // scattered dirty partial lines per pass whose write-back lands in the
         // middle of the next pass's record stream (+30 us of gate time,
         // tools/exp_variants.py).
-        __builtin_nontemporal_store(__float_as_uint(w), reinterpret_cast<uint32_t*>(d.syn + region + e.x) + 2);
+        if (store) __builtin_nontemporal_store(__float_as_uint(w), reinterpret_cast<uint32_t*>(d.syn + ri) + 2);
         ++upd;
         if (f) {
             fired[pre] = (int32_t)e.y;  // dst, spike list in budget order
@@ -661,6 +736,7 @@ __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, Kernel
         if (summaries[1] != 0 && budget > 0)
             *d.rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
         if (events > 0) *d.clock = now + kp.clock_inc; // brain.metal:129
+        *d.pass_index += 1;
         PassWork* w = d.work;
         w->stats.passes += 1;
         w->stats.events += w->events;
@@ -742,19 +818,29 @@ inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 template <int BLOCK, int K, int FW>
 hipError_t launch_gate_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
 {
-    if (kp.track_visits)
-        hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true>), dim3(d.gate_blocks), dim3(BLOCK), 0, s, d, kp);
-    else
-        hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false>), dim3(d.gate_blocks), dim3(BLOCK), 0, s, d, kp);
+    const dim3 g(d.gate_blocks), b(BLOCK);
+    const bool random = d.mode == ABNN_MODE_RANDOM;
+    if (kp.track_visits) {
+        if (random) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true, true>), g, b, 0, s, d, kp);
+        else hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true, false>), g, b, 0, s, d, kp);
+    } else {
+        if (random) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, true>), g, b, 0, s, d, kp);
+        else hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false>), g, b, 0, s, d, kp);
+    }
     return hipGetLastError();
 }
 
 template <int BLOCK, int K, int FW>
-int occupancy_shape(bool track)
+int occupancy_shape(bool track, bool random)
 {
     int n = 0;
-    hipError_t e = track ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true>, BLOCK, 0)
-                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false>, BLOCK, 0);
+    hipError_t e;
+    if (track)
+        e = random ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, true>, BLOCK, 0)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, false>, BLOCK, 0);
+    else
+        e = random ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, true>, BLOCK, 0)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, false>, BLOCK, 0);
     return e == hipSuccess ? n : 0;
 }
 
@@ -774,10 +860,10 @@ constexpr uint64_t shape_key(uint32_t b, uint32_t k, uint32_t fw) { return ((uin
 
 }  // namespace
 
-int gate_blocks_per_cu(uint32_t block, uint32_t k, uint32_t fw, bool track)
+int gate_blocks_per_cu(uint32_t block, uint32_t k, uint32_t fw, bool track, bool random)
 {
     switch (shape_key(block, k, fw)) {
-#define X(B, K, F) case shape_key(B, K, F): return occupancy_shape<B, K, F>(track);
+#define X(B, K, F) case shape_key(B, K, F): return occupancy_shape<B, K, F>(track, random);
         ABNN_GATE_SHAPES(X)
 #undef X
     }
@@ -833,6 +919,11 @@ hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int64_t* su
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
                         uint32_t world, uint32_t rank, int32_t* fired, hipStream_t s)
 {
+    if (d.mode == ABNN_MODE_RANDOM) {
+        hipLaunchKernelGGL(k_claim, dim3(kTileBlocks), dim3(256), 0, s, d, kp, summaries, rank);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_apply, dim3(kTileBlocks), dim3(256), 0, s, d, kp, summaries, world,
                        rank, fired);
     return hipGetLastError();

@@ -38,9 +38,10 @@ def shard_ranges(n_syn_global: int, world: int) -> list[tuple[int, int]]:
     return out
 
 
-def global_events(n_syn_global: int, events_per_pass: int, world: int) -> int:
-    """Visited events per pass over all shards (each shard sweeps its own range)."""
-    return sum(visited_events(events_per_pass, hi - lo) for lo, hi in shard_ranges(n_syn_global, world))
+def global_events(n_syn_global: int, events_per_pass: int, world: int, mode: int = 0) -> int:
+    """Visited events per pass over all shards (each shard sweeps, or picks
+    within, its own range)."""
+    return sum(visited_events(events_per_pass, hi - lo, mode) for lo, hi in shard_ranges(n_syn_global, world))
 
 
 class Engine(Protocol):
@@ -125,7 +126,8 @@ class ShardedBrain:
         lo, hi = shard_ranges(n_syn_global, self.world)[self.rank]
         self.lo, self.hi = lo, hi
         self.n_syn_global = n_syn_global
-        self.global_events = global_events(n_syn_global, events_per_pass, self.world)
+        self.global_events = global_events(n_syn_global, events_per_pass, self.world,
+                                           int(param_overrides.get("mode", 0)))
         self.brain = Brain(n_input, n_output, n_hidden, hi - lo, events_per_pass, device=device,
                            syn_offset=lo, global_events=self.global_events, **param_overrides)
         dev = torch.device("cuda", device)

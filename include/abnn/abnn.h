@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ABNN_ABI_VERSION 1
+#define ABNN_ABI_VERSION 2
 
 typedef enum abnn_status {
     ABNN_OK = 0,
@@ -70,7 +70,8 @@ typedef struct abnn_dims {
     uint64_t events_per_pass;    /* EVENTS_PER_PASS (constants.h:11); visited
                                     events per pass are
                                     min(roundup(events,256), n_syn) (brain.cpp:117,
-                                    brain.metal:61)                            */
+                                    brain.metal:61) in sweep mode and exactly
+                                    events_per_pass in random mode              */
     uint64_t syn_offset;         /* global id of local synapse 0 (sharding; 0)   */
     uint64_t global_events;      /* sum over shards of visited events per pass;
                                     0 = this handle alone (used for the clock
@@ -99,15 +100,39 @@ typedef struct abnn_params {
     uint32_t track_visits;   /* 0: lastVisited untouched (reference code,
                                 brain.metal:44); 1: lastVisited[dst] = now for
                                 every visited event (README §4)        */
-    uint32_t reserved0;
-    uint64_t seed;           /* seed of the handle's host RNG (inject_inputs) */
+    uint32_t mode;           /* ABNN_MODE_SWEEP (the reference code: event t
+                                visits synapse t) or ABNN_MODE_RANDOM (README
+                                §4, SURVEY §8(a) A14: event t visits a uniform
+                                random synapse, below)                 */
+    uint64_t seed;           /* seed of the handle's host RNG (inject_inputs)
+                                and of the random-mode picks           */
 } abnn_params;
 
-/* Scalar state (brain.cpp:57-60): clock, reward, running-average reward. */
+/* Random-edge mode (README §4 "pick a random synapse"; no reference code, so
+ * the build defines it):
+ *   E = events_per_pass events per pass; event t (local index) visits record
+ *   e(t) = mulhi64(x, n_syn), x = (out[1] << 32) | out[0] of
+ *   Philox4x32-10(counter = {t_lo, t_hi, pass_lo, pass_hi},
+ *                 key = {seed_lo ^ off_lo, seed_hi ^ off_hi}),
+ *   pass = abnn_scalars.pass_index, off = abnn_dims.syn_offset (a shard picks
+ *   within its own records, with its own stream).
+ *   Gates, budget, candidate test (rand01((u32)(syn_offset + t) ^ now)) and
+ *   stamps follow schedule C1 with t as the event id.  Every event reads the
+ *   pass-start record; when several events that reached the update picked
+ *   the same synapse, the weight stored is the one computed by the highest
+ *   event index (a legal serialisation of the racy kernel: all reads before
+ *   all writes, writes in event order).                                      */
+#define ABNN_MODE_SWEEP 0u
+#define ABNN_MODE_RANDOM 1u
+
+/* Scalar state (brain.cpp:57-60): clock, reward, running-average reward,
+ * plus the pass counter that keys the random-mode picks. */
 typedef struct abnn_scalars {
     uint64_t clock;          /* u64 (u32 in brain.cpp:57; identical < 2^32) */
     float reward;
     float rbar;
+    uint64_t pass_index;     /* passes run by this handle (+1 per pass; not
+                                reset by renormalisation or reset_stats)    */
 } abnn_scalars;
 
 /* Cumulative per-handle pass statistics (for the roofline byte count). */

@@ -71,12 +71,43 @@ static inline float clampf(float x, float lo, float hi)
     return m < hi ? m : hi;
 }
 
-/* Visited events per pass: the grid is roundup(EVENTS,256) threads and every
- * tid >= nSyn returns at once (BR:116-118, MSL:60-61). */
-uint64_t oracle_visited_events(const abnn_dims* d)
+/* Visited events per pass.  Sweep: the grid is roundup(EVENTS,256) threads
+ * and every tid >= nSyn returns at once (BR:116-118, MSL:60-61).  Random
+ * mode (README §4): exactly EVENTS picks. */
+uint64_t oracle_visited_events(const abnn_dims* d, uint32_t mode)
 {
+    if (mode == ABNN_MODE_RANDOM) return d->n_syn ? d->events_per_pass : 0;
     uint64_t grid = (d->events_per_pass + 255u) / 256u * 256u;
     return grid < d->n_syn ? grid : d->n_syn;
+}
+
+/* Philox4x32-10: ten rounds of two 32x32->64 multiplies; the key is bumped
+ * by the Weyl constants between rounds. */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4])
+{
+    uint32_t x0 = ctr[0], x1 = ctr[1], x2 = ctr[2], x3 = ctr[3], k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * x0, p1 = (uint64_t)0xCD9E8D57u * x2;
+        const uint32_t y0 = (uint32_t)(p1 >> 32) ^ x1 ^ k0, y1 = (uint32_t)p1;
+        const uint32_t y2 = (uint32_t)(p0 >> 32) ^ x3 ^ k1, y3 = (uint32_t)p0;
+        x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = x0; out[1] = x1; out[2] = x2; out[3] = x3;
+}
+
+/* Random-mode record of local event t: Lemire multiply-shift of a 64-bit
+ * Philox draw onto [0, n_syn). */
+uint64_t oracle_pick(uint64_t seed, uint64_t stream, uint64_t pass, uint64_t t, uint64_t n_syn)
+{
+    const uint64_t k = seed ^ stream;
+    const uint32_t c[4] = {(uint32_t)t, (uint32_t)(t >> 32), (uint32_t)pass, (uint32_t)(pass >> 32)};
+    const uint32_t key[2] = {(uint32_t)k, (uint32_t)(k >> 32)};
+    uint32_t o[4];
+    oracle_philox4x32_10(c, key, o);
+    const uint64_t x = ((uint64_t)o[1] << 32) | o[0];
+    return (uint64_t)(((unsigned __int128)x * n_syn) >> 64);
 }
 
 /* Synthetic graph, recipe of build_random_graph (ENG:31-53) with a portable
@@ -211,6 +242,15 @@ static inline int spike_candidate(const abnn_params* p, float w, uint64_t t_glob
     return prob > oracle_rand01((uint32_t)t_global ^ (uint32_t)now);  /* MSL:92 */
 }
 
+/* Record visited by local event t (sweep: t itself). */
+static inline uint64_t rec_index(const oracle_state* s, uint64_t t)
+{
+    if (s->p.mode != ABNN_MODE_RANDOM) return t;
+    return oracle_pick(s->p.seed, s->dims.syn_offset, s->pass_index, t, s->dims.n_syn);
+}
+
+static uint64_t events_of(const oracle_state* s) { return oracle_visited_events(&s->dims, s->p.mode); }
+
 /* Pass start: auto-stimulus (the bench's "all inputs fire") and the host's
  * renormalisation decision, taken on the pass-start clock (BR:127-128). */
 static int pass_begin(oracle_state* s)
@@ -237,6 +277,7 @@ static void pass_end(oracle_state* s, const uint32_t* fired, uint64_t n_fired,
         s->clock = 0;
     }
     s->stats.passes += 1;
+    s->pass_index += 1;
 }
 
 /* ---- the oracle of record: literal serial C1 loop ------------------------ */
@@ -245,16 +286,23 @@ void oracle_pass_serial(oracle_state* s)
     const abnn_params* p = &s->p;
     int renorm = pass_begin(s);
     const uint64_t now = s->clock;                 /* per-TG clock cache, MSL:63-68 */
-    const uint64_t E = oracle_visited_events(&s->dims);
+    const uint64_t E = events_of(s);
     const uint64_t* L = s->last_fired;             /* pass-start snapshot (C1)       */
     const float R = s->reward, rb = s->rbar;        /* MSL:105-106                    */
     uint32_t budget = p->max_spikes;               /* reset per pass, BR:90          */
     uint32_t* fired = (uint32_t*)malloc(sizeof(uint32_t) * (p->max_spikes + 1u));
     uint64_t n_fired = 0;
     int t0_updated = 0;
+    const int random = p->mode == ABNN_MODE_RANDOM;
+    /* random mode: weights are written after the sweep, in event order, so
+     * every event reads the pass-start record and the last writer wins */
+    uint64_t* pend_e = NULL;
+    float* pend_w = NULL;
+    uint64_t n_pend = 0, cap_pend = 0;
 
     for (uint64_t t = 0; t < E; ++t) {
-        abnn_synapse sy = s->syn[t];               /* MSL:70 */
+        const uint64_t e = rec_index(s, t);
+        abnn_synapse sy = s->syn[e];               /* MSL:70 */
         uint64_t tg = s->dims.syn_offset + t;
         if (now - L[sy.src] > p->window_pre) continue;          /* MSL:73-77 */
         s->stats.pre_gated++;
@@ -267,11 +315,25 @@ void oracle_pass_serial(oracle_state* s)
         if (f) budget -= 1;                                     /* MSL:95-98 (C1: never loses) */
         if (tg == 0) t0_updated = 1;                            /* MSL:110-113 */
         float isi = (float)(now - ld);                          /* MSL:116 */
-        s->syn[t].w = updated_weight(p, sy.w, f, R, rb, isi);   /* MSL:101-122 */
+        float w = updated_weight(p, sy.w, f, R, rb, isi);       /* MSL:101-121 */
+        if (!random) {
+            s->syn[t].w = w;                                    /* MSL:122 */
+        } else {
+            if (n_pend == cap_pend) {
+                cap_pend = cap_pend ? 2 * cap_pend : 1024;
+                pend_e = (uint64_t*)realloc(pend_e, cap_pend * sizeof(uint64_t));
+                pend_w = (float*)realloc(pend_w, cap_pend * sizeof(float));
+            }
+            pend_e[n_pend] = e;
+            pend_w[n_pend++] = w;
+        }
         if (f) fired[n_fired++] = sy.dst;                       /* MSL:125-126 (deferred) */
     }
+    for (uint64_t i = 0; i < n_pend; ++i) s->syn[pend_e[i]].w = pend_w[i];
+    free(pend_e);
+    free(pend_w);
     if (p->track_visits)
-        for (uint64_t t = 0; t < E; ++t) s->last_visited[s->syn[t].dst] = now;
+        for (uint64_t t = 0; t < E; ++t) s->last_visited[s->syn[rec_index(s, t)].dst] = now;
     s->stats.events += E;
     s->stats.fired += n_fired;
     pass_end(s, fired, n_fired, t0_updated,
@@ -317,7 +379,7 @@ static void gate_range(const oracle_state* s, uint64_t t0, uint64_t t1, g2vec* o
     const uint64_t* L = s->last_fired;
     memset(c, 0, sizeof(*c));
     for (uint64_t t = t0; t < t1; ++t) {
-        abnn_synapse sy = s->syn[t];
+        abnn_synapse sy = s->syn[rec_index(s, t)];
         if (now - L[sy.src] > p->window_pre) continue;
         c->g1++;
         uint64_t ld = L[sy.dst];
@@ -331,7 +393,7 @@ static void gate_range(const oracle_state* s, uint64_t t0, uint64_t t1, g2vec* o
         e.isi = (float)(now - ld);
         e.pre = (uint32_t)c->cand;
         e.cand = (uint32_t)spike_candidate(p, sy.w, tg, now);
-        e.pad = 0;
+        e.w = sy.w;
         c->cand += e.cand;
         g2_push(out, &e);
     }
@@ -348,8 +410,8 @@ static uint64_t apply_range(oracle_state* s, const oracle_g2* g, uint64_t n, uin
     for (uint64_t j = 0; j < n; ++j) {
         uint64_t pre = off + g[j].pre;
         if (pre >= p->max_spikes) break; /* entries are in order: the rest are inactive */
-        abnn_synapse* sy = &s->syn[g[j].t];
-        sy->w = updated_weight(p, sy->w, (int)g[j].cand, R, rb, g[j].isi);
+        abnn_synapse* sy = &s->syn[rec_index(s, g[j].t)];
+        sy->w = updated_weight(p, g[j].w, (int)g[j].cand, R, rb, g[j].isi);  /* pass-start w */
         nu++;
         if (g[j].cand) { fired[pre] = (int32_t)sy->dst; nf++; }
     }
@@ -361,7 +423,7 @@ int64_t oracle_shard_gate(oracle_state* s, oracle_g2* out, uint64_t cap,
                           int64_t summary[ABNN_SUMMARY_WORDS])
 {
     (void)pass_begin(s); /* stimulus; the renorm decision is re-taken in commit */
-    uint64_t E = oracle_visited_events(&s->dims);
+    uint64_t E = events_of(s);
     g2vec g = {out, 0, cap, 0, 0};
     gate_counts c;
     gate_range(s, 0, E, &g, &c);
@@ -394,8 +456,8 @@ void oracle_shard_apply(oracle_state* s, const oracle_g2* g2, int64_t n_g2,
     s->stats.updated += nu;
     s->stats.fired += nf;
     if (s->p.track_visits) {
-        uint64_t E = oracle_visited_events(&s->dims);
-        for (uint64_t t = 0; t < E; ++t) s->last_visited[s->syn[t].dst] = s->clock;
+        uint64_t E = events_of(s);
+        for (uint64_t t = 0; t < E; ++t) s->last_visited[s->syn[rec_index(s, t)].dst] = s->clock;
     }
 }
 
@@ -420,6 +482,7 @@ void oracle_shard_commit(oracle_state* s, const int64_t* summaries, uint32_t wor
         s->clock = 0;
     }
     s->stats.passes += 1;
+    s->pass_index += 1;
 }
 
 /* ---- threaded pass: nthreads contiguous virtual shards ------------------- */
@@ -449,7 +512,7 @@ void oracle_pass_threaded(oracle_state* s, int nthreads)
     if (nthreads > 256) nthreads = 256;
     const abnn_params* p = &s->p;
     int renorm = pass_begin(s);
-    uint64_t E = oracle_visited_events(&s->dims);
+    uint64_t E = events_of(s);
     thr_job* jobs = (thr_job*)calloc((size_t)nthreads, sizeof(thr_job));
     pthread_t th[256];
     uint64_t per = (E + (uint64_t)nthreads - 1) / (uint64_t)nthreads;
@@ -469,12 +532,15 @@ void oracle_pass_threaded(oracle_state* s, int nthreads)
                 off += jobs[k].c.cand;
             }
         }
+        /* random mode: shards may pick the same synapse, so the writes go in
+         * event order (shard order) on one thread; the gate phase is parallel */
+        const int serial = nthreads == 1 || (phase == 1 && p->mode == ABNN_MODE_RANDOM);
         for (int k = 0; k < nthreads; ++k) {
             jobs[k].phase = phase;
-            if (nthreads == 1) thr_worker(&jobs[k]);
+            if (serial) thr_worker(&jobs[k]);
             else pthread_create(&th[k], NULL, thr_worker, &jobs[k]);
         }
-        if (nthreads > 1)
+        if (!serial)
             for (int k = 0; k < nthreads; ++k) pthread_join(th[k], NULL);
     }
     uint64_t total = 0, nf = 0;
@@ -491,7 +557,7 @@ void oracle_pass_threaded(oracle_state* s, int nthreads)
     uint64_t n_fired = total < p->max_spikes ? total : p->max_spikes;
     (void)nf;
     if (p->track_visits)
-        for (uint64_t t = 0; t < E; ++t) s->last_visited[s->syn[t].dst] = s->clock;
+        for (uint64_t t = 0; t < E; ++t) s->last_visited[s->syn[rec_index(s, t)].dst] = s->clock;
     s->stats.events += E;
     s->stats.fired += n_fired;
     uint32_t* fu = (uint32_t*)fired;

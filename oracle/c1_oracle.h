@@ -36,6 +36,7 @@ typedef struct oracle_state {
     uint64_t rng;               /* host RNG state (inject_inputs)          */
     uint64_t stim_first, stim_count;
     abnn_stats stats;
+    uint64_t pass_index;        /* passes run (keys the random-mode picks)   */
 } oracle_state;
 
 /* One G2 entry (event that passed both gates) of a shard, in event order. */
@@ -44,13 +45,17 @@ typedef struct oracle_g2 {
     float isi;                  /* (float)(now - lastFired[dst])           */
     uint32_t pre;               /* local exclusive count of spike candidates */
     uint32_t cand;              /* 1 if p > rand01                         */
-    uint32_t pad;
+    float w;                    /* pass-start weight of the visited record */
 } oracle_g2;
 
 void oracle_default_params(abnn_params* p);
 float oracle_rand01(uint32_t s);
 uint64_t oracle_splitmix64_at(uint64_t seed, uint64_t k);
-uint64_t oracle_visited_events(const abnn_dims* d);
+uint64_t oracle_visited_events(const abnn_dims* d, uint32_t mode);
+/* Philox4x32-10 (Salmon et al., SC'11; the Random123 constants) and the
+ * random-mode pick of abnn.h: record visited by local event t. */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+uint64_t oracle_pick(uint64_t seed, uint64_t stream, uint64_t pass, uint64_t t, uint64_t n_syn);
 void oracle_gen_synapse(uint64_t i, uint32_t n_in, uint32_t n_out, uint64_t n_nrn,
                         uint64_t seed, abnn_synapse* out);
 void oracle_gen_synapses(abnn_synapse* out, uint64_t first_global, uint64_t n,

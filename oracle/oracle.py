@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
 SYN_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("w", "<f4"), ("pad", "<f4")])
-G2_DTYPE = np.dtype([("t", "<u8"), ("isi", "<f4"), ("pre", "<u4"), ("cand", "<u4"), ("pad", "<u4")])
+G2_DTYPE = np.dtype([("t", "<u8"), ("isi", "<f4"), ("pre", "<u4"), ("cand", "<u4"), ("w", "<f4")])
 SUMMARY_WORDS = 4
 
 
@@ -34,7 +34,7 @@ class Params(C.Structure):
                 ("a_ltd", C.c_float), ("w_min", C.c_float), ("w_max", C.c_float),
                 ("max_spikes", C.c_uint32), ("tick_ns", C.c_uint32), ("tau_vis", C.c_uint32),
                 ("tau_pre", C.c_uint32), ("renorm_thresh", C.c_uint64),
-                ("track_visits", C.c_uint32), ("reserved0", C.c_uint32), ("seed", C.c_uint64)]
+                ("track_visits", C.c_uint32), ("mode", C.c_uint32), ("seed", C.c_uint64)]
 
 
 class Stats(C.Structure):
@@ -46,7 +46,8 @@ class State(C.Structure):
     _fields_ = [("dims", Dims), ("p", Params), ("n_nrn", C.c_uint64), ("syn", C.c_void_p),
                 ("last_fired", C.c_void_p), ("last_visited", C.c_void_p), ("clock", C.c_uint64),
                 ("reward", C.c_float), ("rbar", C.c_float), ("rng", C.c_uint64),
-                ("stim_first", C.c_uint64), ("stim_count", C.c_uint64), ("stats", Stats)]
+                ("stim_first", C.c_uint64), ("stim_count", C.c_uint64), ("stats", Stats),
+                ("pass_index", C.c_uint64)]
 
 
 _lib = None
@@ -66,7 +67,9 @@ def load() -> C.CDLL:
             "oracle_default_params": (None, [C.POINTER(Params)]),
             "oracle_rand01": (C.c_float, [u32]),
             "oracle_splitmix64_at": (u64, [u64, u64]),
-            "oracle_visited_events": (u64, [C.POINTER(Dims)]),
+            "oracle_visited_events": (u64, [C.POINTER(Dims), u32]),
+            "oracle_philox4x32_10": (None, [vp, vp, vp]),
+            "oracle_pick": (u64, [u64, u64, u64, u64, u64]),
             "oracle_gen_synapses": (None, [vp, u64, u64, u32, u32, u64, u64, C.c_int]),
             "oracle_checksum_synapses": (u64, [vp, u64, u64]),
             "oracle_inject_inputs": (None, [C.POINTER(State), vp, u32, C.c_float]),
@@ -111,9 +114,21 @@ def checksum(syn: np.ndarray, first_global: int = 0) -> int:
     return int(load().oracle_checksum_synapses(syn.ctypes.data, syn.shape[0], first_global))
 
 
-def visited_events(events: int, n_syn: int) -> int:
+def visited_events(events: int, n_syn: int, mode: int = 0) -> int:
     d = Dims(0, 0, 0, n_syn, events, 0, 0)
-    return int(load().oracle_visited_events(C.byref(d)))
+    return int(load().oracle_visited_events(C.byref(d), mode))
+
+
+def philox4x32_10(ctr, key) -> list[int]:
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    load().oracle_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def pick(seed: int, stream: int, pass_index: int, t: int, n_syn: int) -> int:
+    return int(load().oracle_pick(seed, stream, pass_index, t, n_syn))
 
 
 class OracleBrain:
@@ -157,10 +172,13 @@ class OracleBrain:
         return checksum(self.syn, int(self.s.dims.syn_offset))
 
     def scalars(self) -> dict:
-        return {"clock": int(self.s.clock), "reward": float(self.s.reward), "rbar": float(self.s.rbar)}
+        return {"clock": int(self.s.clock), "reward": float(self.s.reward), "rbar": float(self.s.rbar),
+                "pass_index": int(self.s.pass_index)}
 
-    def set_scalars(self, clock: int, reward: float, rbar: float) -> None:
+    def set_scalars(self, clock: int, reward: float, rbar: float, pass_index: Optional[int] = None) -> None:
         self.s.clock, self.s.reward, self.s.rbar = clock, reward, rbar
+        if pass_index is not None:
+            self.s.pass_index = pass_index
 
     def set_reward(self, r: float) -> None:
         self.s.reward = r
@@ -195,7 +213,7 @@ class OracleBrain:
 
     # shard phases --------------------------------------------------------------------------
     def shard_gate(self, summary: np.ndarray) -> np.ndarray:
-        ev = visited_events(int(self.s.dims.events_per_pass), int(self.s.dims.n_syn))
+        ev = visited_events(int(self.s.dims.events_per_pass), int(self.s.dims.n_syn), int(self.p.mode))
         buf = np.zeros(max(1, ev), dtype=G2_DTYPE)
         n = self._lib.oracle_shard_gate(C.byref(self.s), buf.ctypes.data, buf.shape[0],
                                         summary.ctypes.data)

@@ -48,6 +48,27 @@ class Cell:
             self.v, self.pending = self.pending, None
 
 
+M32 = 0xFFFFFFFF
+
+
+def philox4x32_10(ctr, key):
+    """Philox4x32-10 (Salmon et al., SC'11), written independently of the C oracle."""
+    x0, x1, x2, x3 = ctr
+    k0, k1 = key
+    for _ in range(10):
+        p0, p1 = 0xD2511F53 * x0, 0xCD9E8D57 * x2
+        x0, x1, x2, x3 = ((p1 >> 32) ^ x1 ^ k0) & M32, p1 & M32, ((p0 >> 32) ^ x3 ^ k1) & M32, p0 & M32
+        k0, k1 = (k0 + 0x9E3779B9) & M32, (k1 + 0xBB67AE85) & M32
+    return x0, x1, x2, x3
+
+
+def pick(seed, stream, pass_index, t, n_syn):
+    """Random-mode record of event t (include/abnn/abnn.h)."""
+    k = seed ^ stream
+    o = philox4x32_10((t & M32, t >> 32, pass_index & M32, pass_index >> 32), (k & M32, k >> 32))
+    return (((o[1] << 32) | o[0]) * n_syn) >> 64
+
+
 class MetalEmu:
     """State of one Brain: synapse list, lastFired cells, scalars."""
 
@@ -63,12 +84,18 @@ class MetalEmu:
         self.events = int(events)
         self.p = params
         self.stim = (0, 0)
+        self.pass_index = 0
 
     def kernel(self):
-        """One dispatch of monte_carlo_traversal over roundup(EVENTS,256) threads."""
+        """One dispatch of monte_carlo_traversal over roundup(EVENTS,256) threads
+        (sweep), or EVENTS threads each visiting a random record (random mode:
+        every thread reads the pass-start record; stores land in tid order)."""
         p = self.p
         n_syn = len(self.src)
-        grid = (self.events + 255) // 256 * 256
+        random = p.get("mode", 0) == 1
+        grid = self.events if random else (self.events + 255) // 256 * 256
+        w0 = list(self.w)
+        rec = [pick(p["seed"], 0, self.pass_index, t, n_syn) for t in range(grid)] if random and n_syn else None
         lastF = [Cell(v) for v in self.lastF]
         clock = Cell(self.clock)
         rbar = Cell(self.rbar)
@@ -76,21 +103,24 @@ class MetalEmu:
         now_tg = clock.load()      # every TG caches the same pass-start value under C1
         ticked = False
         for tid in range(grid):
-            if tid >= n_syn:
+            if not random and tid >= n_syn:
                 break                               # brain.metal:61
+            if random and n_syn == 0:
+                break
+            e = rec[tid] if random else tid
             now = now_tg
-            lp = lastF[self.src[tid]].load()
+            lp = lastF[self.src[e]].load()
             if (now - lp) & U64 > p["window_pre"]:
                 ticked |= tid == 0
                 continue
-            ld = lastF[self.dst[tid]].load()
+            ld = lastF[self.dst[e]].load()
             if (now - ld) & U64 <= p["refractory"]:
                 ticked |= tid == 0
                 continue
             if budget == 0:
                 ticked |= tid == 0
                 continue
-            w = self.w[tid]
+            w = w0[e]
             prob = metal_clamp(F(w * w) * F(p["base_scale"]), F(0.0), F(1.0))
             fired = prob > rand01((tid & U32) ^ (now & U32))
             if fired:
@@ -107,9 +137,9 @@ class MetalEmu:
             isi = F((now - ld) & U64)
             est = F(F(1e6) / isi) if isi > F(0.0) else F(0.0)
             dW = F(dW + F(F(F(p["eta_home"]) * F(F(p["target_rate_hz"]) - est)) * w))
-            self.w[tid] = metal_clamp(F(w + dW), F(p["w_min"]), F(p["w_max"]))
+            self.w[e] = metal_clamp(F(w + dW), F(p["w_min"]), F(p["w_max"]))
             if fired:
-                lastF[self.dst[tid]].store(now)
+                lastF[self.dst[e]].store(now)
             ticked |= tid == 0
         for c in lastF:
             c.commit()
@@ -119,8 +149,9 @@ class MetalEmu:
         if ticked:
             self.clock = (now_tg + p["clock_inc"]) & U64
         if p.get("track_visits"):
-            for tid in range(min(grid, n_syn)):
-                self.lastV[self.dst[tid]] = now_tg
+            for tid in range(grid if random else min(grid, n_syn)):
+                self.lastV[self.dst[rec[tid] if random else tid]] = now_tg
+        self.pass_index += 1
 
     def one_pass(self):
         """run_one_pass minus the host driver: stimulus, kernel, renorm (brain.cpp:87-141)."""

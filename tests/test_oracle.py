@@ -66,6 +66,7 @@ def _emu_from(ob: O.OracleBrain, events):
     for k in p:
         p[k] = getattr(ob.p, k)
     p["track_visits"] = ob.p.track_visits
+    p["mode"], p["seed"] = ob.p.mode, ob.p.seed
     e = MetalEmu(ob.syn["src"], ob.syn["dst"], ob.syn["w"], ob.n_neuron(), events, p)
     return e
 
@@ -210,3 +211,92 @@ def test_inject_and_read_outputs():
     ob.s.clock = 8
     out = ob.read_outputs()
     assert out[5] and not out[6] and out.sum() == 1
+
+
+# ---- random-edge mode (README §4; build-defined contract in include/abnn/abnn.h) ----
+
+def test_philox_known_answers():
+    """The published Philox4x32-10 known-answer vectors (Random123 kat_vectors)."""
+    from py_reference import philox4x32_10 as py_philox
+
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+           ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+           ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+            (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1))]
+    for ctr, key, want in kat:
+        assert tuple(O.philox4x32_10(ctr, key)) == want
+        assert tuple(py_philox(ctr, key)) == want
+
+
+def test_pick_in_range_and_uniform():
+    from py_reference import pick as py_pick
+
+    n = 1000
+    picks = np.array([O.pick(7, 0, 3, t, n) for t in range(20_000)])
+    assert picks.min() >= 0 and picks.max() < n
+    counts = np.bincount(picks, minlength=n)
+    assert counts.min() > 0 and abs(counts.mean() - 20.0) < 1e-9 and counts.std() < 7.0
+    for t in (0, 1, 123456, 2**32 + 5):
+        for stream, pidx, nn in ((0, 0, 10), (99, 2**33, 4_000_000_000), (5, 1, 1)):
+            assert O.pick(11, stream, pidx, t, nn) == py_pick(11, stream, pidx, t, nn)
+
+
+def _random_brain(n_hidden=488, n_syn=2_000, events=12_000, **kw):
+    ob = O.OracleBrain(256, 256, n_hidden, n_syn, events, mode=1, seed=9, **kw)
+    ob.build_random_graph(seed=5)
+    ob.set_auto_stimulus(0, 256)
+    return ob
+
+
+@pytest.mark.parametrize("case", ["dense", "hidden", "visits"])
+def test_random_mode_oracle_matches_python_restatement(case):
+    # n_syn << events: ~6 visits per synapse per pass, so colliding updates are common
+    kw = {"n_hidden": 3000, "n_syn": 30_000, "events": 9_000} if case == "hidden" else {}
+    if case == "visits":
+        kw["track_visits"] = 1
+    ob = _random_brain(**kw)
+    emu = _emu_from(ob, ob.s.dims.events_per_pass)
+    emu.p["mode"], emu.p["seed"] = 1, 9
+    emu.stim = (0, 256)
+    for k in range(8):
+        if k == 4:
+            ob.set_reward(0.6)
+            emu.reward = np.float32(0.6)
+        ob.pass_serial()
+        emu.one_pass()
+        _compare(ob, emu)
+    assert ob.scalars()["pass_index"] == 8 and ob.stats()["events"] == 8 * ob.s.dims.events_per_pass
+    if case == "visits":
+        assert np.array_equal(ob.last_visited, np.array(emu.lastV, dtype=np.uint64))
+
+
+def test_random_mode_collisions_happen():
+    ob = _random_brain()
+    E, n = int(ob.s.dims.events_per_pass), int(ob.s.dims.n_syn)
+    picks = [O.pick(9, 0, 0, t, n) for t in range(E)]
+    assert len(set(picks)) < E  # the collision rule is exercised
+
+
+@pytest.mark.parametrize("nthreads", [1, 3, 8])
+def test_random_mode_threaded_equals_serial(nthreads):
+    a, b = _random_brain(), _random_brain()
+    for _ in range(7):
+        a.pass_serial()
+        b.pass_threaded(nthreads=nthreads)
+    assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32))
+    assert np.array_equal(a.last_fired, b.last_fired)
+    assert a.scalars() == b.scalars() and a.stats() == b.stats()
+
+
+def test_random_mode_shard_phases_world1_equal_serial():
+    a, b = _random_brain(), _random_brain()
+    for _ in range(6):
+        a.pass_serial()
+        summ = np.zeros(4, dtype=np.int64)
+        b.shard_gate(summ)
+        fired = np.zeros(2560, dtype=np.int32)
+        b.shard_apply(summ, 1, 0, fired)
+        b.shard_commit(summ, 1, fired)
+    assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32))
+    assert np.array_equal(a.last_fired, b.last_fired)
+    assert a.scalars() == b.scalars()
