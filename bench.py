@@ -42,6 +42,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-passes", type=int, default=3)
+    ap.add_argument("--mode", choices=["sweep", "random"], default="sweep",
+                    help="sweep: event t visits synapse t (the reference kernel); random: "
+                         "README §4 random-edge picks (include/abnn/abnn.h)")
+    ap.add_argument("--events", type=int, default=0,
+                    help="override EVENTS_PER_PASS (e.g. = N_SYN for the config-3 full sweep)")
     return ap.parse_args()
 
 
@@ -73,14 +78,23 @@ def load_traffic(config: str):
         return None
 
 
-def cpu_baseline(wl, threads: int, timed_passes: int) -> dict:
-    """The threaded C oracle ("port") on the host cores, same workload.  The sweep
-    only ever touches the first E synapses, so the sample holds exactly those and
-    produces the identical pass results; 6 untimed passes reach the steady state."""
+def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int) -> dict:
+    """The threaded C oracle ("port") on the host cores.  Sweep: the pass only
+    ever touches the first E synapses, so the sample holds exactly those and
+    produces the identical pass results.  Random mode: picks span the whole
+    graph, so the sample is a graph of at most 150M synapses (bounded host
+    memory and generation time) with the same neurons and events.  6 untimed
+    passes reach the steady state."""
     from oracle import oracle as O
 
-    E = O.visited_events(wl.events, wl.n_syn)
-    ob = O.OracleBrain(wl.n_input, wl.n_output, wl.n_hidden, E, wl.events)
+    if mode == 1:
+        n_syn = min(wl.n_syn, 150_000_000)
+        E = O.visited_events(events, n_syn, 1)
+        what = f"{n_syn:,}-synapse random graph ({wl.name} recipe), {E:,} random picks per pass"
+    else:
+        n_syn = E = O.visited_events(events, wl.n_syn)
+        what = f"first {E:,} synapses of the {wl.name} graph (all the sweep touches)"
+    ob = O.OracleBrain(wl.n_input, wl.n_output, wl.n_hidden, n_syn, events, mode=mode)
     ob.build_random_graph(1, nthreads=threads)
     ob.set_auto_stimulus(0, wl.n_input)
     ob.pass_threaded(6, nthreads=threads)
@@ -88,8 +102,7 @@ def cpu_baseline(wl, threads: int, timed_passes: int) -> dict:
     ob.pass_threaded(timed_passes, nthreads=threads)
     dt = time.perf_counter() - t0
     return {"value": timed_passes * E / dt, "unit": "events/s", "cores": threads, "kind": "port",
-            "sample": f"first {E:,} synapses of the {wl.name} graph (all the sweep touches), "
-                      f"{wl.n_neuron:,} neurons, 6 untimed + {timed_passes} timed passes, "
+            "sample": f"{what}, {wl.n_neuron:,} neurons, 6 untimed + {timed_passes} timed passes, "
                       f"oracle_pass_threaded with {threads} threads"}
 
 
@@ -101,6 +114,8 @@ def main():
     from abnn_amd.shard import ShardedBrain, TorchComm
 
     wl = CONFIGS[args.config]
+    mode = 1 if args.mode == "random" else 0
+    events = args.events or wl.events
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -121,12 +136,12 @@ def main():
             dist.init_process_group(backend)
 
     if world > 1:
-        sb = ShardedBrain(TorchComm(), wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events,
-                          device=device)
+        sb = ShardedBrain(TorchComm(), wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, events,
+                          device=device, mode=mode)
         brain = sb.brain
         step = sb.step
     else:
-        brain = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, device=device)
+        brain = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, events, device=device, mode=mode)
         step = brain.encode_traversal
     brain.build_random_graph(1)
     brain.set_auto_stimulus(0, wl.n_input)
@@ -167,14 +182,17 @@ def main():
         bytes_per_launch = algorithmic_bytes(stats, track) / max(1, launches)
         achieved = bytes_per_launch / (avg_gate_ms * 1e-3) / 1e9
         survey_per_launch = survey_bytes(stats, track) / max(1, launches)
-        traffic = load_traffic(args.config) if world == 1 else None
+        default_run = mode == 0 and events == wl.events
+        traffic = load_traffic(args.config) if world == 1 and default_run else None
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
             "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4),
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "bytes_formula": "16*E (SynapsePacked stream; E visited events) -- DESIGN.md §5",
+            "bytes_formula": ("16*E (SynapsePacked stream; E visited events) -- DESIGN.md §5" if mode == 0 else
+                              "16*E (one random SynapsePacked record per pick; HBM moves >= 64 B per "
+                              "random access) -- DESIGN.md §5"),
             "survey_formula_bytes_per_launch": int(survey_per_launch),
             "survey_formula_achieved": round(survey_per_launch / (avg_gate_ms * 1e-3) / 1e9, 1),
             "survey_formula": "24*E + 8*G1 (SURVEY §8d; G1 pre-gated) -- counts an 8-B lastFired[src] "
@@ -186,7 +204,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-            cpu = cpu_baseline(wl, threads, args.cpu_passes)
+            cpu = cpu_baseline(wl, events, mode, threads, args.cpu_passes)
         out = {
             "metric": "traversal events/sec at 1B synapses, 5M neurons; achieved HBM GB/s",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
@@ -195,7 +213,8 @@ def main():
             "data": "synthetic (build_random_graph recipe, portable RNG, generated on GPU)",
             "config": {
                 "workload": f"{wl.name}: {wl.note}", "n_neuron": wl.n_neuron, "n_syn": wl.n_syn,
-                "events_per_pass_per_gpu": wl.events, "visited_events_per_pass_per_gpu": local_events,
+                "events_per_pass_per_gpu": events, "visited_events_per_pass_per_gpu": local_events,
+                "mode": args.mode,
                 "parallelism": (f"synapse-shard dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)"))
                                if world > 1 else "single GPU",
                 "pre_gated_frac": stats["pre_gated"] / max(1, stats["events"]),
