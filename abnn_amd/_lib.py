@@ -26,6 +26,7 @@ class Dims(C.Structure):
         ("events_per_pass", C.c_uint64),
         ("syn_offset", C.c_uint64),
         ("global_events", C.c_uint64),
+        ("syn_capacity", C.c_uint64),
     ]
 
 
@@ -53,6 +54,10 @@ class Params(C.Structure):
         ("track_visits", C.c_uint32),
         ("mode", C.c_uint32),
         ("seed", C.c_uint64),
+        ("w_prune", C.c_float),
+        ("p_new", C.c_float),
+        ("w_init", C.c_float),
+        ("compact_every", C.c_uint32),
     ]
 
 
@@ -73,6 +78,8 @@ class Stats(C.Structure):
         ("post_gated", C.c_uint64),
         ("updated", C.c_uint64),
         ("fired", C.c_uint64),
+        ("pruned", C.c_uint64),
+        ("grown", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

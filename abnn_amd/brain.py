@@ -47,14 +47,15 @@ class Brain:
 
     def __init__(self, n_input: int, n_output: int, n_hidden: int, n_syn: int,
                  events_per_pass: int, *, params: Optional[Params] = None, device: int = 0,
-                 syn_offset: int = 0, global_events: int = 0, **param_overrides):
+                 syn_offset: int = 0, global_events: int = 0, syn_capacity: int = 0,
+                 **param_overrides):
         self._lib = _lib.load()
         if params is None:
             params = _lib.default_params(**param_overrides)
         elif param_overrides:
             raise TypeError("pass either params= or keyword overrides, not both")
         self._dims = Dims(n_input, n_output, n_hidden, n_syn, events_per_pass, syn_offset,
-                          global_events)
+                          global_events, syn_capacity)
         self._params = params
         h = C.c_void_p()
         call("abnn_brain_create", C.byref(self._dims), C.byref(params), int(device), C.byref(h))
@@ -93,18 +94,21 @@ class Brain:
         return int(self._lib.abnn_n_neuron(self._h))
 
     def n_syn(self) -> int:
-        return int(self._dims.n_syn)
+        """Current record count (structural updates change it)."""
+        return int(self.dims.n_syn)
 
     @property
     def dims(self) -> Dims:
-        return self._dims
+        d = Dims()
+        call("abnn_get_dims", self._h, C.byref(d))
+        return d
 
     @property
     def params(self) -> Params:
         return self._params
 
     def visited_events(self) -> int:
-        return visited_events(self._dims.events_per_pass, self._dims.n_syn, self._params.mode)
+        return visited_events(self._dims.events_per_pass, self.n_syn(), self._params.mode)
 
     def state_ptrs(self) -> dict:
         s = State()

@@ -68,6 +68,8 @@ struct abnn_brain {
     uint32_t* idx_scratch = nullptr;
     uint64_t idx_cap = 0;
     uint64_t* u64_scratch = nullptr;
+    int cus = 256, per_cu = 1;     // gate partition inputs (configure)
+    uint64_t pass_host = 0;        // mirror of pass_index (structural-update schedule)
 };
 
 namespace {
@@ -91,7 +93,7 @@ void free_all(abnn_brain* b)
     void* ptrs[] = {b->d.syn,       b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->d.bitmap,    b->d.filter,     b->d.range_cnt,     b->d.tile_desc,
                     b->d.tile_mask, b->d.tile_pre,   b->d.g1idx,    b->d.g2e,         b->d.apply_partial,
-                    b->d.claim,
+                    b->d.claim,     b->d.g2src,      b->d.grown,
                     b->d.fired,     b->d.summary,    b->d.work,          b->idx_scratch,
                     b->u64_scratch,  const_cast<uint4*>(b->d.dummy)};
     for (void* p : ptrs)
@@ -174,6 +176,88 @@ abnn_status time_begin(abnn_brain* b, hipStream_t s, EventPair** out)
     return ABNN_OK;
 }
 
+// Sweep partition for the current record count: visited events, wave
+// iterations and the persistent gate grid (one range per wave).  Run at
+// creation and after every structural update.
+void configure(abnn_brain* b)
+{
+    DeviceState& d = b->d;
+    d.n_syn = b->dims.n_syn;
+    d.events = visited_events(b->dims, b->params.mode);
+    const uint64_t iters = (d.events + d.iter_events - 1) / d.iter_events;
+    d.iters = (uint32_t)iters;
+    uint64_t G = std::min<uint64_t>(iters, std::min<uint64_t>((uint64_t)b->cus * b->per_cu, kMaxGateBlocks));
+    // ranges are per wave; the last workgroup may own fewer than one iteration each
+    const uint64_t waves = d.gate_block / 64;
+    G = std::min<uint64_t>(G, (iters + waves - 1) / waves);
+    if (G == 0 && iters > 0) G = 1;
+    d.gate_blocks = (uint32_t)G;
+    d.n_ranges = (uint32_t)(G * waves);  // <= kMaxGateBlocks * 16 = kMaxRanges
+}
+
+// README §5 structural update (contract in abnn.h): stable removal of the
+// tombstones into a fresh buffer, then the grown records in (pass, slot)
+// order while capacity lasts.  Synchronous; runs between passes.
+abnn_status structural_update(abnn_brain* b)
+{
+    DeviceState& d = b->d;
+    const uint64_t n = b->dims.n_syn, cap = b->dims.syn_capacity;
+    ST_TRY(sync_all(b));
+    const uint64_t nb = (n + kCompactChunk - 1) / kCompactChunk;
+    uint32_t* counts = nullptr;
+    uint64_t* offsets = nullptr;
+    uint4* dst = nullptr;
+    ST_TRY(dalloc(&counts, nb));
+    ST_TRY(dalloc(&offsets, nb));
+    abnn_status st = dalloc(&dst, cap + kDummyRecords);  // zeroed: padding stays zero
+    if (st != ABNN_OK) {
+        (void)hipFree(counts);
+        (void)hipFree(offsets);
+        return st;
+    }
+    std::vector<uint32_t> hc(nb);
+    std::vector<uint64_t> ho(nb);
+    hipError_t e = launch_count_live(d.syn, n, counts, nullptr);
+    if (e == hipSuccess && nb) e = hipMemcpy(hc.data(), counts, nb * 4, hipMemcpyDeviceToHost);
+    uint64_t live = 0;
+    for (uint64_t i = 0; i < nb; ++i) {
+        ho[i] = live;
+        live += hc[i];
+    }
+    if (e == hipSuccess && nb) e = hipMemcpy(offsets, ho.data(), nb * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_compact(d.syn, n, offsets, dst, nullptr);
+    uint64_t added = 0;
+    if (e == hipSuccess && d.grown) {
+        const uint64_t slots = (uint64_t)b->params.compact_every * b->params.max_spikes;
+        std::vector<uint4> g(slots);
+        e = hipMemcpy(g.data(), d.grown, slots * sizeof(uint4), hipMemcpyDeviceToHost);
+        std::vector<uint4> app;
+        for (uint64_t j = 0; e == hipSuccess && j < slots && live + app.size() < cap; ++j)
+            if (g[j].w == 1u) app.push_back(make_uint4(g[j].x, g[j].y, g[j].z, 0u));
+        if (e == hipSuccess && !app.empty())
+            e = hipMemcpy(dst + live, app.data(), app.size() * sizeof(uint4), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemset(d.grown, 0, slots * sizeof(uint4));
+        added = app.size();
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    (void)hipFree(counts);
+    (void)hipFree(offsets);
+    if (e != hipSuccess) {
+        (void)hipFree(dst);
+        set_err(std::string("structural update: ") + hipGetErrorString(e));
+        return ABNN_ERR_HIP;
+    }
+    (void)hipFree(d.syn);
+    d.syn = dst;
+    b->dims.n_syn = live + added;
+    uint64_t grown = 0;
+    HIP_TRY(hipMemcpy(&grown, &d.work->stats.grown, 8, hipMemcpyDeviceToHost));
+    grown += added;
+    HIP_TRY(hipMemcpy(&d.work->stats.grown, &grown, 8, hipMemcpyHostToDevice));
+    configure(b);
+    return ABNN_OK;
+}
+
 // bitmap + streaming gate + chunk scan: the first half of every pass.
 abnn_status run_gate(abnn_brain* b, int64_t* summary_out, hipStream_t s)
 {
@@ -196,6 +280,9 @@ abnn_status run_commit(abnn_brain* b, const int64_t* summaries, uint32_t world,
         HIP_TRY(launch_renorm(b->d, b->clock_host, s));
         b->clock_host = 0;
     }
+    b->pass_host += 1;
+    const uint32_t ce = b->params.compact_every;
+    if (ce != 0 && b->pass_host % ce == 0) ST_TRY(structural_update(b));  // README §5
     return ABNN_OK;
 }
 
@@ -269,8 +356,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     else abnn_default_params(&p);
     REQUIRE(p.max_spikes < (1u << 30), "max_spikes too large");
     REQUIRE(p.mode == ABNN_MODE_SWEEP || p.mode == ABNN_MODE_RANDOM, "unknown mode");
-    const uint64_t E = visited_events(*dims, p.mode);
+    const uint64_t cap = std::max<uint64_t>(dims->syn_capacity, dims->n_syn);  // 0 = creation size
+    abnn_dims dmax = *dims;
+    dmax.n_syn = cap;
+    const uint64_t E = visited_events(dmax, p.mode);  // the most events a pass can visit
     REQUIRE(p.mode != ABNN_MODE_RANDOM || E < 0xFFFFFFFFull, "random mode: events per pass must fit u32");
+    const bool genesis = p.p_new > 0.0f && p.compact_every > 0;
     // Gate kernel shape: threads per workgroup x events per lane x LDS filter
     // KiB (ABNN_GATE="512x8f32"; tuning knob, the default is the measured best).
     uint32_t gate_block = 512, gate_k = 8, filter_kib = 32;
@@ -300,6 +391,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     abnn_brain* b = new (std::nothrow) abnn_brain();
     if (!b) return ABNN_ERR_OOM;
     b->dims = *dims;
+    b->dims.syn_capacity = cap;
     b->params = p;
     b->kp = to_kernel_params(p);
     b->device = device;
@@ -315,16 +407,14 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
         return fail(ABNN_ERR_HIP);
     }
     DeviceState& d = b->d;
-    d.n_syn = dims->n_syn;
     d.n_nrn = n_nrn;
-    d.events = E;
+    d.n_input = dims->n_input;
     d.syn_offset = dims->syn_offset;
     d.seed = p.seed;
     d.mode = p.mode;
     d.gate_block = gate_block;
     d.gate_k = gate_k;
     d.iter_events = (uint32_t)iter_events;
-    d.iters = (uint32_t)iters;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
@@ -334,20 +424,17 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
                                     p.mode == ABNN_MODE_RANDOM);
     if (per_cu <= 0) per_cu = 1;
     if (per_cu > 4) per_cu = 4;
-    uint64_t G = std::min<uint64_t>(iters, std::min<uint64_t>((uint64_t)cus * per_cu, kMaxGateBlocks));
-    // ranges are per wave; the last workgroup may own fewer than one iteration each
-    const uint64_t waves = gate_block / 64;
-    G = std::min<uint64_t>(G, (iters + waves - 1) / waves);
-    if (G == 0 && iters > 0) G = 1;
-    d.gate_blocks = (uint32_t)G;
-    d.n_ranges = (uint32_t)(G * waves);  // <= kMaxGateBlocks * 16 = kMaxRanges
+    b->cus = cus;
+    b->per_cu = per_cu;
+    configure(b);  // sweep partition for the creation size
+    const uint64_t max_ranges = (uint64_t)std::min<int>(kMaxGateBlocks, cus * per_cu) * (gate_block / 64);
     d.n_bitmap_words = (uint32_t)(2 * ((n_nrn + 63) / 64));
     d.filter_words = filter_words;
     d.filter_exact = d.n_bitmap_words <= filter_words ? 1u : 0u;
     abnn_status s;
     // build_buffers, brain.cpp:52-69: allocate and zero every buffer.
     // padded: the gate's last iteration reads up to one iteration past the sweep
-    if ((s = dalloc(&d.syn, dims->n_syn + kDummyRecords)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.syn, cap + kDummyRecords)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_fired, n_nrn)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_visited, n_nrn)) != ABNN_OK) return fail(s);
     uint64_t* sb = nullptr;
@@ -359,8 +446,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.pass_index = sb + 2;
     if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.filter, kMaxFilterWords)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.range_cnt, d.n_ranges)) != ABNN_OK) return fail(s);
-    const uint64_t max_tiles = E / kTile + d.n_ranges + 1;
+    if ((s = dalloc(&d.range_cnt, max_ranges)) != ABNN_OK) return fail(s);
+    const uint64_t max_tiles = E / kTile + max_ranges + 1;
     if ((s = dalloc(&d.tile_mask, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.tile_desc, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.tile_pre, max_tiles)) != ABNN_OK) return fail(s);
@@ -370,7 +457,11 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
     d.dummy = dummy;
     if ((s = dalloc(&d.apply_partial, kTileBlocks)) != ABNN_OK) return fail(s);
-    if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, dims->n_syn)) != ABNN_OK) return fail(s);
+    if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, cap)) != ABNN_OK) return fail(s);
+    if (genesis) {
+        if ((s = dalloc(&d.g2src, max_tiles * kTile)) != ABNN_OK) return fail(s);
+        if ((s = dalloc(&d.grown, (uint64_t)p.compact_every * p.max_spikes)) != ABNN_OK) return fail(s);
+    }
     if ((s = dalloc(&d.fired, p.max_spikes + 1u)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.summary, ABNN_SUMMARY_WORDS)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
@@ -532,6 +623,7 @@ abnn_status abnn_set_scalars(abnn_brain* b, const abnn_scalars* in)
     blk[2] = in->pass_index;
     HIP_TRY(hipMemcpy(b->scalar_block, blk, sizeof(blk), hipMemcpyHostToDevice));
     b->clock_host = in->clock;
+    b->pass_host = in->pass_index;
     return ABNN_OK;
 }
 

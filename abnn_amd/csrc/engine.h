@@ -51,13 +51,16 @@ struct DeviceState {
     uint32_t* g1idx;          // [iters * iter_events] pre-gated event offsets (event - region), per-range regions
     uint4* g2e;               // [max_tiles * kTile] {event - region, dst, w, isi} of the events that passed
     const uint4* dummy;       // [kDummyRecords] zero records: target of masked-off stream loads
-    uint2* apply_partial;     // [kTileBlocks] {updated, fired} per apply workgroup
+    uint4* apply_partial;     // [kTileBlocks] {updated, fired, pruned, 0} per apply workgroup
+    uint32_t* g2src;          // genesis on: [max tiles * kTile] src of the visited record
+    uint4* grown;             // genesis on: [compact_every * max_spikes] grown records (w = 1: used)
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     int32_t* fired;           // [max_spikes] internal spike list (world = 1)
     int64_t* summary;         // [ABNN_SUMMARY_WORDS] internal (world = 1)
     PassWork* work;
     uint64_t n_syn;           // local records
     uint64_t n_nrn;
+    uint32_t n_input;
     uint64_t events;          // visited events per pass (local)
     uint64_t syn_offset;
     uint64_t seed;            // random-mode pick key (abnn_params.seed)
@@ -78,7 +81,12 @@ struct KernelParams {
     float a_ltp, a_ltd, w_min, w_max;
     uint32_t refractory, window_pre, clock_inc, max_spikes;
     uint32_t track_visits;
+    float w_prune, p_new, w_init;  // structural plasticity (README §5)
+    uint32_t compact_every;
 };
+
+constexpr int kCompactThreads = 1024;  // structural update: 4 consecutive records per thread
+constexpr int kCompactChunk = 4 * kCompactThreads;
 
 KernelParams to_kernel_params(const abnn_params& p);
 
@@ -99,6 +107,10 @@ hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int6
 hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
                            uint32_t world, const int32_t* fired, hipStream_t s);
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);
+// Structural update: live records per kCompactChunk block, then a stable
+// compaction into `dst` at the given per-block offsets.
+hipError_t launch_count_live(const uint4* syn, uint64_t n, uint32_t* counts, hipStream_t s);
+hipError_t launch_compact(const uint4* syn, uint64_t n, const uint64_t* offsets, uint4* dst, hipStream_t s);
 hipError_t launch_generate(const DeviceState& d, uint32_t n_in, uint32_t n_out, uint64_t seed,
                            hipStream_t s);
 hipError_t launch_checksum(const DeviceState& d, uint64_t* out_dev, hipStream_t s);

@@ -55,6 +55,10 @@ KernelParams to_kernel_params(const abnn_params& p)
     k.clock_inc = p.clock_inc;
     k.max_spikes = p.max_spikes;
     k.track_visits = p.track_visits;
+    k.w_prune = p.w_prune;
+    k.p_new = p.p_new;
+    k.w_init = p.w_init;
+    k.compact_every = p.compact_every;
     return k;
 }
 
@@ -522,6 +526,7 @@ __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
         const uint64_t bg = __ballot(g2), bc = __ballot(cand);
         if (g2 && tg == 0) d.work->t0_g2 = 1;
         if (g2) d.g2e[(uint64_t)tile * kTile + lane] = make_uint4(rel, rec.y, rec.z, __float_as_uint((float)(now - ld)));
+        if (g2 && d.g2src) d.g2src[(uint64_t)tile * kTile + lane] = rec.x;  // synaptogenesis keeps src
         if (lane == 0)
             d.tile_mask[tile] = make_uint4((uint32_t)bg, (uint32_t)(bg >> 32), (uint32_t)bc, (uint32_t)(bc >> 32));
     }
@@ -643,7 +648,8 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
     const uint32_t T = d.work->total_tiles;
     const uint64_t pass = *d.pass_index;
     const bool random = d.mode == ABNN_MODE_RANDOM;
-    uint32_t upd = 0, nf = 0;
+    const bool prune = kp.w_prune > 0.0f, genesis = d.grown != nullptr && kp.p_new > 0.0f;
+    uint32_t upd = 0, nf = 0, npr = 0;
     for (uint32_t tile = wave; tile < T; tile += nwaves) {
         const uint64_t P = off + d.tile_pre[tile];
         if (P >= budget) continue;
@@ -665,23 +671,41 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
         // scattered dirty partial lines per pass whose write-back lands in the
         // middle of the next pass's record stream (+30 us of gate time,
         // tools/exp_variants.py).
-        if (store) __builtin_nontemporal_store(__float_as_uint(w), reinterpret_cast<uint32_t*>(d.syn + ri) + 2);
+        if (store && prune && w < kp.w_prune) {  // README §5: the synapse is removed
+            __builtin_nontemporal_store(u32x4_t{0xFFFFFFFFu, 0xFFFFFFFFu, __float_as_uint(w), 0u},
+                                        reinterpret_cast<u32x4_t*>(d.syn + ri));
+            ++npr;
+        } else if (store) {
+            __builtin_nontemporal_store(__float_as_uint(w), reinterpret_cast<uint32_t*>(d.syn + ri) + 2);
+        }
         ++upd;
         if (f) {
             fired[pre] = (int32_t)e.y;  // dst, spike list in budget order
             ++nf;
+            if (genesis) {  // README §5 synaptogenesis: slot `pre` of this pass
+                const uint64_t x = splitmix64_at(d.seed ^ ABNN_GENESIS_KEY, (pass << 32) | pre);
+                if (unit24(x) < kp.p_new) {
+                    const uint64_t span = d.n_nrn - d.n_input;
+                    d.grown[(pass % kp.compact_every) * kp.max_spikes + pre] =
+                        make_uint4(d.g2src[(uint64_t)tile * kTile + lane],
+                                   d.n_input + (uint32_t)(((x & 0xFFFFFFFFull) * span) >> 32),
+                                   __float_as_uint(kp.w_init), 1u);
+                }
+            }
         }
     }
     // per-workgroup partials (atomics from every wave on one address serialise)
-    __shared__ uint32_t s_u[4], s_f[4];
-    const uint32_t wu = wave_sum(upd), wf = wave_sum(nf);
+    __shared__ uint32_t s_u[4], s_f[4], s_p[4];
+    const uint32_t wu = wave_sum(upd), wf = wave_sum(nf), wp = wave_sum(npr);
     if (lane == 0) {
         s_u[threadIdx.x >> 6] = wu;
         s_f[threadIdx.x >> 6] = wf;
+        s_p[threadIdx.x >> 6] = wp;
     }
     __syncthreads();
     if (threadIdx.x == 0)
-        d.apply_partial[blockIdx.x] = make_uint2(s_u[0] + s_u[1] + s_u[2] + s_u[3], s_f[0] + s_f[1] + s_f[2] + s_f[3]);
+        d.apply_partial[blockIdx.x] = make_uint4(s_u[0] + s_u[1] + s_u[2] + s_u[3], s_f[0] + s_f[1] + s_f[2] + s_f[3],
+                                                 s_p[0] + s_p[1] + s_p[2] + s_p[3], 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -711,26 +735,30 @@ __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, Kernel
         for (uint32_t u = 0; u < kU; ++u)
             if (n[u] < d.n_nrn) d.last_fired[n[u]] = now;  // brain.metal:125-126, deferred
     }
-    uint32_t upd = 0, nf = 0;
+    uint32_t upd = 0, nf = 0, npr = 0;
 #pragma unroll
     for (uint32_t u = 0; u < kTileBlocks / kScanThreads; ++u) {
-        const uint2 v = d.apply_partial[u * kScanThreads + tid];
+        const uint4 v = d.apply_partial[u * kScanThreads + tid];
         upd += v.x;
         nf += v.y;
+        npr += v.z;
     }
-    __shared__ uint32_t s_u[kScanThreads / 64], s_f[kScanThreads / 64];
+    __shared__ uint32_t s_u[kScanThreads / 64], s_f[kScanThreads / 64], s_p[kScanThreads / 64];
     upd = wave_sum(upd);
     nf = wave_sum(nf);
+    npr = wave_sum(npr);
     if ((tid & 63) == 0) {
         s_u[tid >> 6] = upd;
         s_f[tid >> 6] = nf;
+        s_p[tid >> 6] = npr;
     }
     __syncthreads();
     if (tid == 0) {
-        uint64_t tu = 0, tf = 0;
+        uint64_t tu = 0, tf = 0, tp = 0;
         for (int w = 0; w < kScanThreads / 64; ++w) {
             tu += s_u[w];
             tf += s_f[w];
+            tp += s_p[w];
         }
         const float R = *d.reward, rb = *d.rbar;
         if (summaries[1] != 0 && budget > 0)
@@ -744,6 +772,7 @@ __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, Kernel
         w->stats.post_gated += w->g2;
         w->stats.updated += tu;
         w->stats.fired += tf;
+        w->stats.pruned += tp;
     }
 }
 
@@ -754,6 +783,47 @@ __global__ __launch_bounds__(256) void k_renorm(DeviceState d, uint64_t base)
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < d.n_nrn) d.last_fired[i] -= base;
     if (i == 0) *d.clock = 0;
+}
+
+// ---------------------------------------------------------------------------
+// Structural update (README §5): stable removal of the tombstones.  Each
+// thread owns kCompactChunk / kCompactThreads consecutive records.
+__global__ __launch_bounds__(kCompactThreads) void k_count_live(const uint4* syn, uint64_t n, uint32_t* counts)
+{
+    __shared__ uint32_t s_c[kCompactThreads / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kCompactChunk + (uint64_t)threadIdx.x * 4;
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (base + j < n && syn[base + j].x != 0xFFFFFFFFu) ++c;
+    c = wave_sum(c);
+    if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kCompactThreads / 64; ++w) t += s_c[w];
+        counts[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kCompactThreads) void k_compact(const uint4* syn, uint64_t n, const uint64_t* offsets,
+                                                             uint4* dst)
+{
+    static_assert(kCompactThreads == kScanThreads, "block_exclusive_scan is sized for kScanThreads");
+    __shared__ uint64_t s_wave[kCompactThreads / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kCompactChunk + (uint64_t)threadIdx.x * 4;
+    uint4 r[4];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        r[j] = base + j < n ? syn[base + j] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+        c += r[j].x != 0xFFFFFFFFu ? 1u : 0u;
+    }
+    uint64_t total;
+    uint64_t o = offsets[blockIdx.x] + block_exclusive_scan(c, &total, s_wave);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (r[j].x != 0xFFFFFFFFu) dst[o++] = r[j];
 }
 
 // ---------------------------------------------------------------------------
@@ -940,6 +1010,22 @@ hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s)
 {
     hipLaunchKernelGGL(k_renorm, dim3(blocks_for(d.n_nrn > 0 ? d.n_nrn : 1)), dim3(256), 0, s, d,
                        base);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_live(const uint4* syn, uint64_t n, uint32_t* counts, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_count_live, dim3((uint32_t)((n + kCompactChunk - 1) / kCompactChunk)),
+                       dim3(kCompactThreads), 0, s, syn, n, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const uint4* syn, uint64_t n, const uint64_t* offsets, uint4* dst, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_compact, dim3((uint32_t)((n + kCompactChunk - 1) / kCompactChunk)),
+                       dim3(kCompactThreads), 0, s, syn, n, offsets, dst);
     return hipGetLastError();
 }
 

@@ -76,6 +76,8 @@ typedef struct abnn_dims {
     uint64_t global_events;      /* sum over shards of visited events per pass;
                                     0 = this handle alone (used for the clock
                                     tick rule, brain.metal:61,129)             */
+    uint64_t syn_capacity;       /* records this handle may grow to by
+                                    synaptogenesis; 0 = n_syn (no growth)     */
 } abnn_dims;
 
 /* Every knob of the path with the reference default (abnn_default_params). */
@@ -106,7 +108,31 @@ typedef struct abnn_params {
                                 random synapse, below)                 */
     uint64_t seed;           /* seed of the handle's host RNG (inject_inputs)
                                 and of the random-mode picks           */
+    /* structural plasticity (README §5; build-defined, below) */
+    float w_prune;           /* 0: off; updated weight < w_prune removes the synapse */
+    float p_new;             /* 0: off; probability that a spike grows a synapse     */
+    float w_init;            /* weight of a grown synapse                            */
+    uint32_t compact_every;  /* structural update after every N-th pass; 0 = never   */
 } abnn_params;
+
+/* Structural plasticity (README §5 "Plasticity & Rewiring"; no reference code,
+ * so the build defines it; the CPU oracle restates it):
+ *   pruning: an event that reached the weight update and whose stored weight
+ *     (random mode: the winning store) is < w_prune removes its synapse: the
+ *     record becomes the tombstone {src = dst = 0xFFFFFFFF, w, 0}, which never
+ *     passes the pre-spike gate but still counts as a visited event;
+ *   synaptogenesis: the spike in global budget slot k of pass p grows a
+ *     synapse iff unit24(x) < p_new, x = splitmix64_at(seed ^ ABNN_GENESIS_KEY,
+ *     (p << 32) | k) (the generator's SplitMix64, unit24 = top 24 bits / 2^24):
+ *     record {src of the firing synapse, n_input + ((x & 0xFFFFFFFF) *
+ *     (N_NRN - n_input) >> 32), w_init, 0};
+ *   structural update, after every pass whose ticked pass_index is a multiple
+ *     of compact_every: tombstones are removed by a stable compaction, then
+ *     the synapses grown since the previous update are appended in (pass,
+ *     slot) order while n_syn < syn_capacity.  n_syn, the visited events and
+ *     the borrowed synapse pointer (abnn_state_ptrs) change here.  Sweep-mode
+ *     event ids stay syn_offset + local index (syn_offset is fixed). */
+#define ABNN_GENESIS_KEY 0xA24BAED4963EE407ull
 
 /* Random-edge mode (README §4 "pick a random synapse"; no reference code, so
  * the build defines it):
@@ -143,6 +169,8 @@ typedef struct abnn_stats {
     uint64_t post_gated;     /* passed the refractory gate (brain.metal:79-83)   */
     uint64_t updated;        /* G2: reached the weight update (budget > 0)       */
     uint64_t fired;          /* F: spikes emitted (lastFired stamps)             */
+    uint64_t pruned;         /* synapses removed (tombstoned)                    */
+    uint64_t grown;          /* synapses appended by structural updates          */
 } abnn_stats;
 
 /* Borrowed device pointers (brain.h:54-58 buffer getters). */

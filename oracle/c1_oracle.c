@@ -242,6 +242,104 @@ static inline int spike_candidate(const abnn_params* p, float w, uint64_t t_glob
     return prob > oracle_rand01((uint32_t)t_global ^ (uint32_t)now);  /* MSL:92 */
 }
 
+/* ---- structural plasticity (README §5; contract in abnn.h) --------------- */
+static const uint32_t kTomb = 0xFFFFFFFFu;
+
+/* Store an updated weight, or remove the synapse if it fell below w_prune;
+ * returns 1 if it was removed. */
+static int store_weight(oracle_state* s, uint64_t e, float w)
+{
+    if (s->p.w_prune > 0.0f && w < s->p.w_prune) {
+        s->syn[e].src = kTomb;
+        s->syn[e].dst = kTomb;
+        s->syn[e].w = w;
+        s->syn[e].pad = 0.0f;
+        return 1;
+    }
+    s->syn[e].w = w;
+    return 0;
+}
+
+/* The spike in global budget slot k may grow a synapse from `src`. */
+static void genesis(oracle_state* s, uint64_t k, uint32_t src)
+{
+    const abnn_params* p = &s->p;
+    if (!(p->p_new > 0.0f) || p->compact_every == 0 || !s->grown) return;
+    const uint64_t x = oracle_splitmix64_at(p->seed ^ ABNN_GENESIS_KEY, (s->pass_index << 32) | k);
+    if (!((float)(x >> 40) * (1.0f / 16777216.0f) < p->p_new)) return;
+    const uint64_t lo = s->dims.n_input, span = s->n_nrn - lo;
+    abnn_synapse* g = &s->grown[(s->pass_index % p->compact_every) * p->max_spikes + k];
+    g->src = src;
+    g->dst = (uint32_t)(lo + (((x & 0xFFFFFFFFu) * span) >> 32));
+    g->w = p->w_init;
+    uint32_t one = 1u;
+    memcpy(&g->pad, &one, 4);
+}
+
+/* After every compact_every-th pass: stable compaction of the tombstones,
+ * then the grown synapses in (pass, slot) order while capacity lasts. */
+static void structural_update(oracle_state* s)
+{
+    const abnn_params* p = &s->p;
+    if (p->compact_every == 0 || s->pass_index % p->compact_every != 0) return;
+    uint64_t n = 0;
+    for (uint64_t i = 0; i < s->dims.n_syn; ++i)
+        if (s->syn[i].src != kTomb) s->syn[n++] = s->syn[i];
+    const uint64_t slots = (uint64_t)p->compact_every * p->max_spikes;
+    for (uint64_t j = 0; s->grown && j < slots; ++j) {
+        uint32_t flag;
+        memcpy(&flag, &s->grown[j].pad, 4);
+        if (flag == 1u && n < s->dims.syn_capacity) {
+            s->syn[n] = s->grown[j];
+            s->syn[n].pad = 0.0f;
+            n++;
+            s->stats.grown++;
+        }
+        memset(&s->grown[j], 0, sizeof(abnn_synapse));
+    }
+    s->dims.n_syn = n;
+}
+
+/* Random mode: weight stores collected in event order, resolved per record
+ * (the highest event wins) at the end of the pass. */
+typedef struct pend_w {
+    uint64_t e, order;
+    float w;
+} pend_w;
+typedef struct pend_list {
+    pend_w* v;
+    uint64_t n, cap;
+} pend_list;
+
+static void pend_push(pend_list* l, uint64_t e, float w)
+{
+    if (l->n == l->cap) {
+        l->cap = l->cap ? 2 * l->cap : 1024;
+        l->v = (pend_w*)realloc(l->v, l->cap * sizeof(pend_w));
+    }
+    l->v[l->n].e = e;
+    l->v[l->n].order = l->n;
+    l->v[l->n].w = w;
+    l->n++;
+}
+
+static int pend_cmp(const void* a, const void* b)
+{
+    const pend_w *x = (const pend_w*)a, *y = (const pend_w*)b;
+    if (x->e != y->e) return x->e < y->e ? -1 : 1;
+    return x->order < y->order ? -1 : (x->order > y->order);
+}
+
+static void pend_resolve(oracle_state* s, pend_list* l)
+{
+    qsort(l->v, l->n, sizeof(pend_w), pend_cmp);
+    for (uint64_t i = 0; i < l->n; ++i)
+        if (i + 1 == l->n || l->v[i + 1].e != l->v[i].e) s->stats.pruned += store_weight(s, l->v[i].e, l->v[i].w);
+    free(l->v);
+    l->v = NULL;
+    l->n = l->cap = 0;
+}
+
 /* Record visited by local event t (sweep: t itself). */
 static inline uint64_t rec_index(const oracle_state* s, uint64_t t)
 {
@@ -278,6 +376,7 @@ static void pass_end(oracle_state* s, const uint32_t* fired, uint64_t n_fired,
     }
     s->stats.passes += 1;
     s->pass_index += 1;
+    structural_update(s);
 }
 
 /* ---- the oracle of record: literal serial C1 loop ------------------------ */
@@ -294,16 +393,16 @@ void oracle_pass_serial(oracle_state* s)
     uint64_t n_fired = 0;
     int t0_updated = 0;
     const int random = p->mode == ABNN_MODE_RANDOM;
-    /* random mode: weights are written after the sweep, in event order, so
-     * every event reads the pass-start record and the last writer wins */
-    uint64_t* pend_e = NULL;
-    float* pend_w = NULL;
-    uint64_t n_pend = 0, cap_pend = 0;
+    /* random mode: weights are written after the sweep, so every event reads
+     * the pass-start record; of several stores to one record the last wins */
+    pend_list pend = {NULL, 0, 0};
 
     for (uint64_t t = 0; t < E; ++t) {
         const uint64_t e = rec_index(s, t);
         abnn_synapse sy = s->syn[e];               /* MSL:70 */
         uint64_t tg = s->dims.syn_offset + t;
+        if (p->track_visits && sy.dst < s->n_nrn) s->last_visited[sy.dst] = now;  /* README §4 */
+        if (sy.src >= s->n_nrn) continue;                       /* removed synapse (README §5) */
         if (now - L[sy.src] > p->window_pre) continue;          /* MSL:73-77 */
         s->stats.pre_gated++;
         uint64_t ld = L[sy.dst];                                /* MSL:79 */
@@ -316,24 +415,14 @@ void oracle_pass_serial(oracle_state* s)
         if (tg == 0) t0_updated = 1;                            /* MSL:110-113 */
         float isi = (float)(now - ld);                          /* MSL:116 */
         float w = updated_weight(p, sy.w, f, R, rb, isi);       /* MSL:101-121 */
-        if (!random) {
-            s->syn[t].w = w;                                    /* MSL:122 */
-        } else {
-            if (n_pend == cap_pend) {
-                cap_pend = cap_pend ? 2 * cap_pend : 1024;
-                pend_e = (uint64_t*)realloc(pend_e, cap_pend * sizeof(uint64_t));
-                pend_w = (float*)realloc(pend_w, cap_pend * sizeof(float));
-            }
-            pend_e[n_pend] = e;
-            pend_w[n_pend++] = w;
+        if (!random) s->stats.pruned += store_weight(s, t, w);  /* MSL:122 (+ pruning) */
+        else pend_push(&pend, e, w);
+        if (f) {
+            genesis(s, n_fired, sy.src);                        /* README §5 */
+            fired[n_fired++] = sy.dst;                          /* MSL:125-126 (deferred) */
         }
-        if (f) fired[n_fired++] = sy.dst;                       /* MSL:125-126 (deferred) */
     }
-    for (uint64_t i = 0; i < n_pend; ++i) s->syn[pend_e[i]].w = pend_w[i];
-    free(pend_e);
-    free(pend_w);
-    if (p->track_visits)
-        for (uint64_t t = 0; t < E; ++t) s->last_visited[s->syn[rec_index(s, t)].dst] = now;
+    pend_resolve(s, &pend);
     s->stats.events += E;
     s->stats.fired += n_fired;
     pass_end(s, fired, n_fired, t0_updated,
@@ -380,6 +469,10 @@ static void gate_range(const oracle_state* s, uint64_t t0, uint64_t t1, g2vec* o
     memset(c, 0, sizeof(*c));
     for (uint64_t t = t0; t < t1; ++t) {
         abnn_synapse sy = s->syn[rec_index(s, t)];
+        /* lastVisited is never read by a decision: written as visited, with
+         * the same value `now` from every thread */
+        if (p->track_visits && sy.dst < s->n_nrn) s->last_visited[sy.dst] = now;
+        if (sy.src >= s->n_nrn) continue;  /* removed synapse */
         if (now - L[sy.src] > p->window_pre) continue;
         c->g1++;
         uint64_t ld = L[sy.dst];
@@ -402,7 +495,7 @@ static void gate_range(const oracle_state* s, uint64_t t0, uint64_t t1, g2vec* o
 /* Apply stored entries with global budget offset `off` (exclusive count of
  * candidates in all earlier shards, capped); returns spikes emitted. */
 static uint64_t apply_range(oracle_state* s, const oracle_g2* g, uint64_t n, uint64_t off,
-                            int32_t* fired, uint64_t* updated)
+                            int32_t* fired, uint64_t* updated, pend_list* pend, uint64_t* pruned)
 {
     const abnn_params* p = &s->p;
     const float R = s->reward, rb = s->rbar;
@@ -410,10 +503,17 @@ static uint64_t apply_range(oracle_state* s, const oracle_g2* g, uint64_t n, uin
     for (uint64_t j = 0; j < n; ++j) {
         uint64_t pre = off + g[j].pre;
         if (pre >= p->max_spikes) break; /* entries are in order: the rest are inactive */
-        abnn_synapse* sy = &s->syn[rec_index(s, g[j].t)];
-        sy->w = updated_weight(p, g[j].w, (int)g[j].cand, R, rb, g[j].isi);  /* pass-start w */
+        const uint64_t e = rec_index(s, g[j].t);
+        const abnn_synapse sy = s->syn[e];  /* pass-start src/dst (stores below) */
+        const float w = updated_weight(p, g[j].w, (int)g[j].cand, R, rb, g[j].isi);  /* pass-start w */
+        if (pend) pend_push(pend, e, w);
+        else *pruned += (uint64_t)store_weight(s, e, w);
         nu++;
-        if (g[j].cand) { fired[pre] = (int32_t)sy->dst; nf++; }
+        if (g[j].cand) {
+            genesis(s, pre, sy.src);
+            fired[pre] = (int32_t)sy.dst;
+            nf++;
+        }
     }
     *updated = nu;
     return nf;
@@ -452,13 +552,14 @@ void oracle_shard_apply(oracle_state* s, const oracle_g2* g2, int64_t n_g2,
     memset(fired, 0, sizeof(int32_t) * s->p.max_spikes);
     uint64_t off = shard_offset(summaries, rank, s->p.max_spikes);
     uint64_t nu = 0;
-    uint64_t nf = apply_range(s, g2, (uint64_t)n_g2, off, fired, &nu);
+    pend_list pend = {NULL, 0, 0};
+    const int random = s->p.mode == ABNN_MODE_RANDOM;
+    uint64_t np = 0;
+    uint64_t nf = apply_range(s, g2, (uint64_t)n_g2, off, fired, &nu, random ? &pend : NULL, &np);
+    if (random) pend_resolve(s, &pend);
+    s->stats.pruned += np;
     s->stats.updated += nu;
     s->stats.fired += nf;
-    if (s->p.track_visits) {
-        uint64_t E = events_of(s);
-        for (uint64_t t = 0; t < E; ++t) s->last_visited[s->syn[rec_index(s, t)].dst] = s->clock;
-    }
 }
 
 void oracle_shard_commit(oracle_state* s, const int64_t* summaries, uint32_t world,
@@ -483,6 +584,7 @@ void oracle_shard_commit(oracle_state* s, const int64_t* summaries, uint32_t wor
     }
     s->stats.passes += 1;
     s->pass_index += 1;
+    structural_update(s);
 }
 
 /* ---- threaded pass: nthreads contiguous virtual shards ------------------- */
@@ -492,8 +594,9 @@ typedef struct thr_job {
     g2vec g;
     gate_counts c;
     int32_t* fired;
-    uint64_t nf, nu;
+    uint64_t nf, nu, np;
     int phase;
+    pend_list* pend;  /* random mode: shared, the apply phase runs serially */
 } thr_job;
 
 static void* thr_worker(void* arg)
@@ -502,7 +605,7 @@ static void* thr_worker(void* arg)
     if (j->phase == 0)
         gate_range(j->s, j->t0, j->t1, &j->g, &j->c);
     else
-        j->nf = apply_range(j->s, j->g.v, j->g.n, j->off, j->fired, &j->nu);
+        j->nf = apply_range(j->s, j->g.v, j->g.n, j->off, j->fired, &j->nu, j->pend, &j->np);
     return NULL;
 }
 
@@ -517,7 +620,9 @@ void oracle_pass_threaded(oracle_state* s, int nthreads)
     pthread_t th[256];
     uint64_t per = (E + (uint64_t)nthreads - 1) / (uint64_t)nthreads;
     int32_t* fired = (int32_t*)calloc(p->max_spikes + 1u, sizeof(int32_t));
+    pend_list pend = {NULL, 0, 0};
     for (int k = 0; k < nthreads; ++k) {
+        jobs[k].pend = p->mode == ABNN_MODE_RANDOM ? &pend : NULL;
         jobs[k].s = s;
         jobs[k].t0 = per * (uint64_t)k < E ? per * (uint64_t)k : E;
         jobs[k].t1 = jobs[k].t0 + per < E ? jobs[k].t0 + per : E;
@@ -543,12 +648,14 @@ void oracle_pass_threaded(oracle_state* s, int nthreads)
         if (!serial)
             for (int k = 0; k < nthreads; ++k) pthread_join(th[k], NULL);
     }
+    pend_resolve(s, &pend);
     uint64_t total = 0, nf = 0;
     int t0 = 0;
     for (int k = 0; k < nthreads; ++k) {
         s->stats.pre_gated += jobs[k].c.g1;
         s->stats.post_gated += jobs[k].c.g2;
         s->stats.updated += jobs[k].nu;
+        s->stats.pruned += jobs[k].np;
         total += jobs[k].c.cand;
         nf += jobs[k].nf;
         t0 |= jobs[k].c.t0;
@@ -556,8 +663,6 @@ void oracle_pass_threaded(oracle_state* s, int nthreads)
     }
     uint64_t n_fired = total < p->max_spikes ? total : p->max_spikes;
     (void)nf;
-    if (p->track_visits)
-        for (uint64_t t = 0; t < E; ++t) s->last_visited[s->syn[rec_index(s, t)].dst] = s->clock;
     s->stats.events += E;
     s->stats.fired += n_fired;
     uint32_t* fu = (uint32_t*)fired;

@@ -37,6 +37,9 @@ typedef struct oracle_state {
     uint64_t stim_first, stim_count;
     abnn_stats stats;
     uint64_t pass_index;        /* passes run (keys the random-mode picks)   */
+    abnn_synapse* grown;        /* structural plasticity: compact_every *
+                                   max_spikes slots, zeroed by the caller;
+                                   a grown synapse has pad bits = 1          */
 } oracle_state;
 
 /* One G2 entry (event that passed both gates) of a shard, in event order. */

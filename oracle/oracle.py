@@ -23,7 +23,8 @@ SUMMARY_WORDS = 4
 class Dims(C.Structure):
     _fields_ = [("n_input", C.c_uint32), ("n_output", C.c_uint32), ("n_hidden", C.c_uint64),
                 ("n_syn", C.c_uint64), ("events_per_pass", C.c_uint64),
-                ("syn_offset", C.c_uint64), ("global_events", C.c_uint64)]
+                ("syn_offset", C.c_uint64), ("global_events", C.c_uint64),
+                ("syn_capacity", C.c_uint64)]
 
 
 class Params(C.Structure):
@@ -34,12 +35,15 @@ class Params(C.Structure):
                 ("a_ltd", C.c_float), ("w_min", C.c_float), ("w_max", C.c_float),
                 ("max_spikes", C.c_uint32), ("tick_ns", C.c_uint32), ("tau_vis", C.c_uint32),
                 ("tau_pre", C.c_uint32), ("renorm_thresh", C.c_uint64),
-                ("track_visits", C.c_uint32), ("mode", C.c_uint32), ("seed", C.c_uint64)]
+                ("track_visits", C.c_uint32), ("mode", C.c_uint32), ("seed", C.c_uint64),
+                ("w_prune", C.c_float), ("p_new", C.c_float), ("w_init", C.c_float),
+                ("compact_every", C.c_uint32)]
 
 
 class Stats(C.Structure):
     _fields_ = [("passes", C.c_uint64), ("events", C.c_uint64), ("pre_gated", C.c_uint64),
-                ("post_gated", C.c_uint64), ("updated", C.c_uint64), ("fired", C.c_uint64)]
+                ("post_gated", C.c_uint64), ("updated", C.c_uint64), ("fired", C.c_uint64),
+                ("pruned", C.c_uint64), ("grown", C.c_uint64)]
 
 
 class State(C.Structure):
@@ -47,7 +51,7 @@ class State(C.Structure):
                 ("last_fired", C.c_void_p), ("last_visited", C.c_void_p), ("clock", C.c_uint64),
                 ("reward", C.c_float), ("rbar", C.c_float), ("rng", C.c_uint64),
                 ("stim_first", C.c_uint64), ("stim_count", C.c_uint64), ("stats", Stats),
-                ("pass_index", C.c_uint64)]
+                ("pass_index", C.c_uint64), ("grown", C.c_void_p)]
 
 
 _lib = None
@@ -136,25 +140,33 @@ class OracleBrain:
 
     def __init__(self, n_input: int, n_output: int, n_hidden: int, n_syn: int,
                  events_per_pass: int, *, syn_offset: int = 0, global_events: int = 0,
-                 params: Optional[Params] = None, **param_overrides):
+                 syn_capacity: int = 0, params: Optional[Params] = None, **param_overrides):
         self._lib = load()
         self.p = params if params is not None else default_params(**param_overrides)
         n_nrn = n_input + n_output + n_hidden
-        self.syn = np.zeros(n_syn, dtype=SYN_DTYPE)
+        cap = max(int(syn_capacity), int(n_syn))  # 0 = the creation size (as the C-ABI)
+        self._syn = np.zeros(cap, dtype=SYN_DTYPE)
         self.last_fired = np.zeros(n_nrn, dtype=np.uint64)
         self.last_visited = np.zeros(n_nrn, dtype=np.uint64)
+        self._grown = np.zeros(max(1, self.p.compact_every * self.p.max_spikes), dtype=SYN_DTYPE)
         self.s = State()
         self.s.dims = Dims(n_input, n_output, n_hidden, n_syn, events_per_pass, syn_offset,
-                           global_events)
+                           global_events, cap)
         self.s.p = self.p
         self.s.n_nrn = n_nrn
         self.s.rng = self.p.seed
         self._bind()
 
+    @property
+    def syn(self) -> np.ndarray:
+        """The current records (n_syn changes at structural updates)."""
+        return self._syn[: int(self.s.dims.n_syn)]
+
     def _bind(self) -> None:
-        self.s.syn = self.syn.ctypes.data
+        self.s.syn = self._syn.ctypes.data
         self.s.last_fired = self.last_fired.ctypes.data
         self.s.last_visited = self.last_visited.ctypes.data
+        self.s.grown = self._grown.ctypes.data
 
     # state ---------------------------------------------------------------------------------
     def n_neuron(self) -> int:
@@ -166,7 +178,7 @@ class OracleBrain:
                                       d.n_output, self.s.n_nrn, seed, nthreads)
 
     def set_synapses(self, syn: np.ndarray) -> None:
-        self.syn[:] = syn
+        self._syn[: syn.shape[0]] = syn
 
     def checksum(self) -> int:
         return checksum(self.syn, int(self.s.dims.syn_offset))

@@ -69,6 +69,18 @@ def pick(seed, stream, pass_index, t, n_syn):
     return (((o[1] << 32) | o[0]) * n_syn) >> 64
 
 
+U64M = (1 << 64) - 1
+GENESIS_KEY = 0xA24BAED4963EE407
+TOMB = 0xFFFFFFFF
+
+
+def splitmix64_at(seed, k):
+    z = (seed + ((k + 1) * 0x9E3779B97F4A7C15)) & U64M
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & U64M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & U64M
+    return z ^ (z >> 31)
+
+
 class MetalEmu:
     """State of one Brain: synapse list, lastFired cells, scalars."""
 
@@ -85,6 +97,11 @@ class MetalEmu:
         self.p = params
         self.stim = (0, 0)
         self.pass_index = 0
+        self.n_in = 256
+        self.capacity = len(self.src)
+        self.grown = {}  # slot -> (src, dst, w) grown since the last structural update
+        self.pruned = 0
+        self.n_grown = 0
 
     def kernel(self):
         """One dispatch of monte_carlo_traversal over roundup(EVENTS,256) threads
@@ -102,6 +119,9 @@ class MetalEmu:
         budget = p["max_spikes"]   # host reset, brain.cpp:90 (sequentially consistent)
         now_tg = clock.load()      # every TG caches the same pass-start value under C1
         ticked = False
+        stores = []
+        visit_dst = ([self.dst[rec[t] if random else t] for t in range(grid if random else min(grid, n_syn))]
+                     if p.get("track_visits") else None)
         for tid in range(grid):
             if not random and tid >= n_syn:
                 break                               # brain.metal:61
@@ -109,6 +129,9 @@ class MetalEmu:
                 break
             e = rec[tid] if random else tid
             now = now_tg
+            if self.src[e] == TOMB:
+                ticked |= tid == 0
+                continue                            # removed synapse (README §5)
             lp = lastF[self.src[e]].load()
             if (now - lp) & U64 > p["window_pre"]:
                 ticked |= tid == 0
@@ -123,11 +146,14 @@ class MetalEmu:
             w = w0[e]
             prob = metal_clamp(F(w * w) * F(p["base_scale"]), F(0.0), F(1.0))
             fired = prob > rand01((tid & U32) ^ (now & U32))
+            slot = None
             if fired:
                 old = budget
                 budget -= 1
                 if old == 0:
                     fired = False
+                else:
+                    slot = p["max_spikes"] - old    # budget position of this spike
             dW = F(F(p["a_ltp"]) * F(F(1.0) - w)) if fired else F(F(-p["a_ltd"]) * w)
             R = self.reward
             rb = rbar.load()
@@ -137,10 +163,26 @@ class MetalEmu:
             isi = F((now - ld) & U64)
             est = F(F(1e6) / isi) if isi > F(0.0) else F(0.0)
             dW = F(dW + F(F(F(p["eta_home"]) * F(F(p["target_rate_hz"]) - est)) * w))
-            self.w[e] = metal_clamp(F(w + dW), F(p["w_min"]), F(p["w_max"]))
+            nw = metal_clamp(F(w + dW), F(p["w_min"]), F(p["w_max"]))
+            stores.append((e, nw))                  # applied after the sweep, last writer wins
             if fired:
                 lastF[self.dst[e]].store(now)
+                if p.get("p_new", 0) > 0 and p.get("compact_every", 0) > 0:
+                    x = splitmix64_at(p["seed"] ^ GENESIS_KEY, ((self.pass_index << 32) | slot) & U64M)
+                    if F(F(x >> 40) * F(1.0 / 16777216.0)) < F(p["p_new"]):
+                        span = len(self.lastF) - self.n_in
+                        dst2 = self.n_in + (((x & U32) * span) >> 32)
+                        self.grown[(self.pass_index % p["compact_every"]) * p["max_spikes"] + slot] = (
+                            self.src[e], dst2, F(p["w_init"]))
             ticked |= tid == 0
+        last = {}
+        for e, nw in stores:
+            last[e] = nw
+        for e, nw in last.items():
+            self.w[e] = nw
+            if p.get("w_prune", 0) > 0 and nw < F(p["w_prune"]):
+                self.src[e] = self.dst[e] = TOMB
+                self.pruned += 1
         for c in lastF:
             c.commit()
         rbar.commit()
@@ -150,8 +192,24 @@ class MetalEmu:
             self.clock = (now_tg + p["clock_inc"]) & U64
         if p.get("track_visits"):
             for tid in range(grid if random else min(grid, n_syn)):
-                self.lastV[self.dst[rec[tid] if random else tid]] = now_tg
+                dv = visit_dst[tid]
+                if dv != TOMB:
+                    self.lastV[dv] = now_tg
         self.pass_index += 1
+        ce = p.get("compact_every", 0)
+        if ce and self.pass_index % ce == 0:          # structural update
+            keep = [i for i in range(len(self.src)) if self.src[i] != TOMB]
+            self.src = [self.src[i] for i in keep]
+            self.dst = [self.dst[i] for i in keep]
+            self.w = [self.w[i] for i in keep]
+            for slot in sorted(self.grown):
+                if len(self.src) < self.capacity:
+                    s_, d_, w_ = self.grown[slot]
+                    self.src.append(s_)
+                    self.dst.append(d_)
+                    self.w.append(w_)
+                    self.n_grown += 1
+            self.grown = {}
 
     def one_pass(self):
         """run_one_pass minus the host driver: stimulus, kernel, renorm (brain.cpp:87-141)."""

@@ -1,0 +1,116 @@
+"""GPU parity of structural plasticity (README §5; contract in include/abnn/abnn.h):
+pruning to tombstones in k_apply, synaptogenesis into per-pass budget slots,
+and the structural update (stable compaction + ordered append) -- HIP path vs
+the CPU oracle, bit-exact, pass by pass, record count included.  No reference
+code exists for this; the oracle is cross-checked against an independent
+Python restatement in tests/test_oracle.py."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SP = dict(w_prune=0.105, p_new=0.35, w_init=0.5, compact_every=2)
+
+
+def _pair(mode=0, n_hidden=3000, n_syn=120_000, events=120_000, cap_extra=20_000, syn_offset=0,
+          global_events=0, **over):
+    import abnn_amd
+    from oracle import oracle as O
+
+    kw = dict(SP, mode=mode, seed=13)
+    kw.update(over)
+    cap = n_syn + cap_extra
+    g = abnn_amd.Brain(256, 256, n_hidden, n_syn, events, syn_offset=syn_offset,
+                       global_events=global_events, syn_capacity=cap, **kw)
+    o = O.OracleBrain(256, 256, n_hidden, n_syn, events, syn_offset=syn_offset,
+                      global_events=global_events, syn_capacity=cap, **kw)
+    g.build_random_graph(21)
+    o.build_random_graph(21, nthreads=16)
+    g.set_auto_stimulus(0, 256)
+    o.set_auto_stimulus(0, 256)
+    return g, o
+
+
+def _same(g, o, what=""):
+    assert g.n_syn() == int(o.s.dims.n_syn), f"n_syn {what}"
+    assert np.array_equal(g.download_synapses().view(np.uint32), o.syn.view(np.uint32)), f"synapses {what}"
+    assert np.array_equal(g.last_fired(), o.last_fired), f"lastFired {what}"
+    sg, so = g.scalars(), o.scalars()
+    assert sg["clock"] == so["clock"] and sg["pass_index"] == so["pass_index"], what
+    assert np.float32(sg["rbar"]) == np.float32(so["rbar"]), what
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_plasticity_every_pass(gpu, mode):
+    g, o = _pair(mode, events=120_000 if mode == 0 else 60_000)
+    sizes = set()
+    for k in range(12):
+        if k == 6:
+            g.set_reward(0.4)
+            o.set_reward(0.4)
+        g.encode_traversal(1)
+        o.pass_serial()
+        _same(g, o, f"pass {k}")
+        sizes.add(g.n_syn())
+    st = g.stats()
+    assert st == o.stats()
+    assert st["pruned"] > 0 and st["grown"] > 0 and len(sizes) > 1
+    assert g.visited_events() == (min(g.n_syn(), 120_064) if mode == 0 else 60_000)
+
+
+@pytest.mark.parametrize("ce", [1, 3])
+def test_plasticity_compact_schedule(gpu, ce):
+    g, o = _pair(0, compact_every=ce)
+    for k in range(7):
+        g.encode_traversal(1)
+        o.pass_threaded(nthreads=16)
+        _same(g, o, f"pass {k}")
+    assert g.stats() == o.stats()
+
+
+def test_plasticity_large_with_visits(gpu):
+    g, o = _pair(0, n_hidden=99_488, n_syn=1_000_000, events=1_000_000, cap_extra=100_000,
+                 track_visits=1)
+    for _ in range(8):
+        g.encode_traversal(1)
+        o.pass_threaded(nthreads=16)
+    _same(g, o)
+    assert np.array_equal(g.last_visited(), o.last_visited)
+    assert g.stats() == o.stats()
+
+
+def test_plasticity_virtual_shards_vs_oracle_shards(gpu):
+    import torch
+
+    from abnn_amd.shard import global_events, shard_ranges
+
+    world, n_syn, events, passes = 2, 240_000, 240_000, 8
+    ge = global_events(n_syn, events, world)
+    pairs = [_pair(0, n_syn=hi - lo, events=events, syn_offset=lo, global_events=ge)
+             for lo, hi in shard_ranges(n_syn, world)]
+    dev = torch.device("cuda", 0)
+    summ = torch.zeros(world, 4, dtype=torch.int64, device=dev)
+    fired = torch.zeros(world, 2560, dtype=torch.int32, device=dev)
+    tot = torch.zeros(2560, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for k in range(passes):
+        for r, (g, _) in enumerate(pairs):
+            g.shard_gate(summ[r].data_ptr(), stream)
+        for r, (g, _) in enumerate(pairs):
+            g.shard_apply(summ.data_ptr(), world, r, fired[r].data_ptr(), stream)
+        torch.sum(fired, dim=0, dtype=torch.int32, out=tot)
+        for g, _ in pairs:
+            g.shard_commit(summ.data_ptr(), world, tot.data_ptr(), stream)
+        osumm = np.zeros((world, 4), dtype=np.int64)
+        for r, (_, o) in enumerate(pairs):
+            o.shard_gate(osumm[r])
+        ofired = np.zeros((world, 2560), dtype=np.int32)
+        for r, (_, o) in enumerate(pairs):
+            o.shard_apply(osumm.reshape(-1), world, r, ofired[r])
+        otot = ofired.sum(axis=0).astype(np.int32)
+        for _, o in pairs:
+            o.shard_commit(osumm.reshape(-1), world, otot)
+    torch.cuda.synchronize()
+    for g, o in pairs:
+        _same(g, o, "shard")
+        assert g.stats() == o.stats()

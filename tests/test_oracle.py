@@ -300,3 +300,95 @@ def test_random_mode_shard_phases_world1_equal_serial():
     assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32))
     assert np.array_equal(a.last_fired, b.last_fired)
     assert a.scalars() == b.scalars()
+
+
+# ---- structural plasticity (README §5; build-defined contract in include/abnn/abnn.h) ----
+
+SP = dict(w_prune=0.105, p_new=0.35, w_init=0.5, compact_every=2)
+
+
+def _sp_brain(mode=0, cap_extra=20_000, n_hidden=3000, n_syn=120_000, events=120_000, **over):
+    kw = dict(SP)
+    kw.update(over)
+    ob = O.OracleBrain(256, 256, n_hidden, n_syn, events, mode=mode, seed=13,
+                       syn_capacity=n_syn + cap_extra, **kw)
+    ob.build_random_graph(seed=21)
+    ob.set_auto_stimulus(0, 256)
+    return ob
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_structural_plasticity_matches_python_restatement(mode):
+    ob = _sp_brain(mode, events=30_000 if mode else 120_000, track_visits=1)
+    emu = _emu_from(ob, ob.s.dims.events_per_pass)
+    emu.p.update(SP)
+    emu.p["track_visits"] = 1
+    emu.capacity = int(ob.s.dims.syn_capacity)
+    emu.stim = (0, 256)
+    n0 = ob.n_syn = None
+    sizes = []
+    for k in range(9):
+        if k == 5:
+            ob.set_reward(0.4)
+            emu.reward = np.float32(0.4)
+        ob.pass_serial()
+        emu.one_pass()
+        sizes.append(int(ob.s.dims.n_syn))
+        assert int(ob.s.dims.n_syn) == len(emu.src), k
+        assert np.array_equal(ob.syn["src"], np.array(emu.src, dtype=np.uint32)), k
+        assert np.array_equal(ob.syn["dst"], np.array(emu.dst, dtype=np.uint32)), k
+        _compare(ob, emu)
+        assert np.array_equal(ob.last_visited, np.array(emu.lastV, dtype=np.uint64)), k
+    st = ob.stats()
+    assert st["pruned"] == emu.pruned > 0 and st["grown"] == emu.n_grown > 0
+    assert len(set(sizes)) > 1  # the graph changed size
+
+
+def test_structural_update_semantics():
+    ob = _sp_brain(0)
+    n_nrn = ob.n_neuron()
+    for _ in range(8):
+        ob.pass_serial()
+    s = ob.syn
+    live = s["src"] != 0xFFFFFFFF
+    # odd number of passes since the last update would leave tombstones; after an
+    # even pass count (compact_every = 2) every tombstone has been compacted away
+    assert live.all()
+    grown = s[s["w"] == np.float32(0.5)]
+    assert grown.shape[0] > 0 and (grown["dst"] >= 256).all() and (grown["dst"] < n_nrn).all()
+    assert ob.stats()["grown"] >= grown.shape[0] - 10  # (a few original weights may be 0.5 exactly)
+    assert int(ob.s.dims.n_syn) <= int(ob.s.dims.syn_capacity)
+
+
+def test_structural_capacity_caps_growth():
+    ob = _sp_brain(0, cap_extra=0, w_prune=0.0)  # nothing is removed, nothing can be added
+    n0 = int(ob.s.dims.n_syn)
+    for _ in range(6):
+        ob.pass_serial()
+    assert int(ob.s.dims.n_syn) == n0 and ob.stats()["grown"] == 0 and ob.stats()["pruned"] == 0
+
+
+@pytest.mark.parametrize("mode,nthreads", [(0, 1), (0, 5), (1, 4)])
+def test_structural_threaded_equals_serial(mode, nthreads):
+    a, b = _sp_brain(mode), _sp_brain(mode)
+    for _ in range(7):
+        a.pass_serial()
+        b.pass_threaded(nthreads=nthreads)
+    assert int(a.s.dims.n_syn) == int(b.s.dims.n_syn)
+    assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32))
+    assert np.array_equal(a.last_fired, b.last_fired)
+    assert a.scalars() == b.scalars() and a.stats() == b.stats()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_structural_shard_world1_equals_serial(mode):
+    a, b = _sp_brain(mode), _sp_brain(mode)
+    for _ in range(6):
+        a.pass_serial()
+        summ = np.zeros(4, dtype=np.int64)
+        b.shard_gate(summ)
+        fired = np.zeros(2560, dtype=np.int32)
+        b.shard_apply(summ, 1, 0, fired)
+        b.shard_commit(summ, 1, fired)
+    assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32))
+    assert a.stats() == b.stats()
