@@ -118,7 +118,8 @@ class ShardedBrain:
     """The rank-local shard of a graph of ``n_syn_global`` synapses on GPU ``device``."""
 
     def __init__(self, comm, n_input: int, n_output: int, n_hidden: int, n_syn_global: int,
-                 events_per_pass: int, *, device: int = 0, **param_overrides):
+                 events_per_pass: int, *, device: int = 0, capacity_factor: float = 1.0,
+                 **param_overrides):
         import torch
 
         self.comm = comm
@@ -128,8 +129,10 @@ class ShardedBrain:
         self.n_syn_global = n_syn_global
         self.global_events = global_events(n_syn_global, events_per_pass, self.world,
                                            int(param_overrides.get("mode", 0)))
+        cap = int((hi - lo) * capacity_factor) if capacity_factor > 1.0 else 0  # synaptogenesis headroom
         self.brain = Brain(n_input, n_output, n_hidden, hi - lo, events_per_pass, device=device,
-                           syn_offset=lo, global_events=self.global_events, **param_overrides)
+                           syn_offset=lo, global_events=self.global_events, syn_capacity=cap,
+                           **param_overrides)
         dev = torch.device("cuda", device)
         self._torch = torch
         self.summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device=dev)

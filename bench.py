@@ -47,7 +47,14 @@ def parse():
                          "README §4 random-edge picks (include/abnn/abnn.h)")
     ap.add_argument("--events", type=int, default=0,
                     help="override EVENTS_PER_PASS (e.g. = N_SYN for the config-3 full sweep)")
+    ap.add_argument("--plasticity", action="store_true",
+                    help="config-5 dynamics: reward-modulated STDP (reward 0.25) with pruning "
+                         "(w < 0.105) and synaptogenesis (p_new 0.25, w_init 0.5, +1%% capacity), "
+                         "structural update every 50 passes (README §5, include/abnn/abnn.h)")
     return ap.parse_args()
+
+
+PLASTICITY = dict(w_prune=0.105, p_new=0.25, w_init=0.5, compact_every=50)
 
 
 def algorithmic_bytes(stats: dict, track_visits: bool) -> int:
@@ -78,7 +85,7 @@ def load_traffic(config: str):
         return None
 
 
-def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int) -> dict:
+def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, extra: dict) -> dict:
     """The threaded C oracle ("port") on the host cores.  Sweep: the pass only
     ever touches the first E synapses, so the sample holds exactly those and
     produces the identical pass results.  Random mode: picks span the whole
@@ -94,9 +101,13 @@ def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int) ->
     else:
         n_syn = E = O.visited_events(events, wl.n_syn)
         what = f"first {E:,} synapses of the {wl.name} graph (all the sweep touches)"
-    ob = O.OracleBrain(wl.n_input, wl.n_output, wl.n_hidden, n_syn, events, mode=mode)
+    ob = O.OracleBrain(wl.n_input, wl.n_output, wl.n_hidden, n_syn, events, mode=mode,
+                       syn_capacity=int(n_syn * 1.01) if extra else 0, **extra)
     ob.build_random_graph(1, nthreads=threads)
     ob.set_auto_stimulus(0, wl.n_input)
+    if extra:
+        ob.set_reward(0.25)
+        what += " with the same plasticity settings"
     ob.pass_threaded(6, nthreads=threads)
     t0 = time.perf_counter()
     ob.pass_threaded(timed_passes, nthreads=threads)
@@ -116,6 +127,7 @@ def main():
     wl = CONFIGS[args.config]
     mode = 1 if args.mode == "random" else 0
     events = args.events or wl.events
+    extra = dict(PLASTICITY) if args.plasticity else {}
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -137,14 +149,19 @@ def main():
 
     if world > 1:
         sb = ShardedBrain(TorchComm(), wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, events,
-                          device=device, mode=mode)
+                          device=device, mode=mode, capacity_factor=1.01 if args.plasticity else 1.0,
+                          **extra)
         brain = sb.brain
         step = sb.step
     else:
-        brain = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, events, device=device, mode=mode)
+        cap = int(wl.n_syn * 1.01) if args.plasticity else 0
+        brain = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, events, device=device, mode=mode,
+                      syn_capacity=cap, **extra)
         step = brain.encode_traversal
     brain.build_random_graph(1)
     brain.set_auto_stimulus(0, wl.n_input)
+    if args.plasticity:
+        brain.set_reward(0.25)  # reward-modulated STDP active (MSL:105-107)
     local_events = brain.visited_events()
 
     def sync():
@@ -204,7 +221,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-            cpu = cpu_baseline(wl, events, mode, threads, args.cpu_passes)
+            cpu = cpu_baseline(wl, events, mode, threads, args.cpu_passes, extra)
         out = {
             "metric": "traversal events/sec at 1B synapses, 5M neurons; achieved HBM GB/s",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
@@ -215,6 +232,9 @@ def main():
                 "workload": f"{wl.name}: {wl.note}", "n_neuron": wl.n_neuron, "n_syn": wl.n_syn,
                 "events_per_pass_per_gpu": events, "visited_events_per_pass_per_gpu": local_events,
                 "mode": args.mode,
+                "plasticity": (dict(PLASTICITY, syn_capacity_factor=1.01, reward=0.25,
+                                    n_syn_after=brain.n_syn(), pruned=stats.get("pruned", 0),
+                                    grown=stats.get("grown", 0)) if args.plasticity else None),
                 "parallelism": (f"synapse-shard dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)"))
                                if world > 1 else "single GPU",
                 "pre_gated_frac": stats["pre_gated"] / max(1, stats["events"]),
