@@ -95,3 +95,79 @@ def test_sharded_gloo_equals_unsharded(world, track):
     # events >= every shard's size: each shard sweeps its whole range, so the
     # rank-ordered union is the unsharded full sweep
     mp.spawn(_worker, args=(world, _free_port(), N_SYN, track), nprocs=world, join=True)
+
+
+SP = dict(w_prune=0.105, p_new=0.35, w_init=0.5, compact_every=2)
+
+
+def _shard_brains(world, events, extra, O, shard_ranges, ge, cap_factor):
+    out = []
+    for lo, hi in shard_ranges(N_SYN, world):
+        ob = O.OracleBrain(256, 256, N_HIDDEN, hi - lo, events, syn_offset=lo, global_events=ge,
+                           syn_capacity=int((hi - lo) * cap_factor), **extra)
+        ob.build_random_graph(seed=11, nthreads=2)
+        ob.set_auto_stimulus(0, 256)
+        out.append(ob)
+    return out
+
+
+def _worker_modes(rank, world, port, events, extra):
+    """Random-edge mode / structural plasticity: shards pick and grow within
+    their own records, so the reference is the same shard phases run in one
+    process (what the exchange must reproduce), not an unsharded run."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+    from abnn_amd.shard import TorchComm, global_events, shard_ranges, sharded_pass
+    from oracle import oracle as O
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = TorchComm()
+        ge = global_events(N_SYN, events, world, extra.get("mode", 0))
+        cap = 1.1 if extra.get("p_new") else 1.0
+        ob = _shard_brains(world, events, extra, O, shard_ranges, ge, cap)[rank]
+        eng = CpuShardEngine(ob)
+        summary = torch.zeros(4, dtype=torch.int64)
+        gathered = torch.zeros(4 * world, dtype=torch.int64)
+        fired = torch.zeros(2560, dtype=torch.int32)
+        for k in range(PASSES):
+            if k == 4:
+                ob.set_reward(0.3)
+            sharded_pass(eng, comm, summary, gathered, fired)
+
+        ref = _shard_brains(world, events, extra, O, shard_ranges, ge, cap)
+        for k in range(PASSES):
+            if k == 4:
+                for r in ref:
+                    r.set_reward(0.3)
+            summ = np.zeros((world, 4), dtype=np.int64)
+            for q, r in enumerate(ref):
+                r.shard_gate(summ[q])
+            fr = np.zeros((world, 2560), dtype=np.int32)
+            for q, r in enumerate(ref):
+                r.shard_apply(summ.reshape(-1), world, q, fr[q])
+            tot = fr.sum(axis=0).astype(np.int32)
+            for r in ref:
+                r.shard_commit(summ.reshape(-1), world, tot)
+        me = ref[rank]
+        assert int(ob.s.dims.n_syn) == int(me.s.dims.n_syn)
+        assert np.array_equal(ob.syn.view(np.uint32), me.syn.view(np.uint32))
+        assert np.array_equal(ob.last_fired, me.last_fired)
+        assert ob.scalars() == me.scalars() and ob.stats() == me.stats()
+        if extra.get("p_new"):
+            assert ob.stats()["pruned"] > 0 or ob.stats()["grown"] > 0
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("extra,events", [(dict(mode=1, seed=5), 120_000),
+                                          (dict(SP, seed=5), N_SYN),
+                                          (dict(SP, mode=1, seed=5), 120_000)],
+                         ids=["random", "plasticity", "random+plasticity"])
+def test_sharded_gloo_modes_equal_phase_sequence(extra, events):
+    mp.spawn(_worker_modes, args=(2, _free_port(), events, extra), nprocs=2, join=True)
