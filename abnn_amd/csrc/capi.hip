@@ -70,6 +70,10 @@ struct abnn_brain {
     uint64_t* u64_scratch = nullptr;
     int cus = 256, per_cu = 1;     // gate partition inputs (configure)
     uint64_t pass_host = 0;        // mirror of pass_index (structural-update schedule)
+    // structural updates (compact_every > 0): the second record buffer the
+    // compaction writes into (swapped with d.syn), and its scan scratch
+    uint4* syn_alt = nullptr;
+    uint64_t* compact_offsets = nullptr;
 };
 
 namespace {
@@ -93,7 +97,8 @@ void free_all(abnn_brain* b)
     void* ptrs[] = {b->d.syn,       b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->d.bitmap,    b->d.filter,     b->d.range_cnt,     b->d.tile_desc,
                     b->d.tile_mask, b->d.tile_pre,   b->d.g1idx,    b->d.g2e,         b->d.apply_partial,
-                    b->d.claim,     b->d.g2src,      b->d.grown,
+                    b->d.claim,     b->d.g2src,      b->d.grown,         b->syn_alt,
+                    b->d.dead,      b->compact_offsets,
                     b->d.fired,     b->d.summary,    b->d.work,          b->idx_scratch,
                     b->u64_scratch,  const_cast<uint4*>(b->d.dummy)};
     for (void* p : ptrs)
@@ -204,25 +209,20 @@ abnn_status structural_update(abnn_brain* b)
     const uint64_t n = b->dims.n_syn, cap = b->dims.syn_capacity;
     ST_TRY(sync_all(b));
     const uint64_t nb = (n + kCompactChunk - 1) / kCompactChunk;
-    uint32_t* counts = nullptr;
-    uint64_t* offsets = nullptr;
-    uint4* dst = nullptr;
-    ST_TRY(dalloc(&counts, nb));
-    ST_TRY(dalloc(&offsets, nb));
-    abnn_status st = dalloc(&dst, cap + kDummyRecords);  // zeroed: padding stays zero
-    if (st != ABNN_OK) {
-        (void)hipFree(counts);
-        (void)hipFree(offsets);
-        return st;
-    }
+    uint32_t* dead = d.dead;  // tombstones per block, tallied by k_apply (null: pruning off)
+    uint64_t* offsets = b->compact_offsets;
+    // Double-buffered: records past n_syn are never read as events (the gate
+    // masks lanes beyond the sweep, picks stay below n_syn), so the spare
+    // buffer needs no clearing.
+    uint4* dst = b->syn_alt;
     std::vector<uint32_t> hc(nb);
     std::vector<uint64_t> ho(nb);
-    hipError_t e = launch_count_live(d.syn, n, counts, nullptr);
-    if (e == hipSuccess && nb) e = hipMemcpy(hc.data(), counts, nb * 4, hipMemcpyDeviceToHost);
+    hipError_t e = hipSuccess;
+    if (dead && nb) e = hipMemcpy(hc.data(), dead, nb * 4, hipMemcpyDeviceToHost);
     uint64_t live = 0;
     for (uint64_t i = 0; i < nb; ++i) {
         ho[i] = live;
-        live += hc[i];
+        live += std::min<uint64_t>(kCompactChunk, n - i * kCompactChunk) - (dead ? hc[i] : 0u);
     }
     if (e == hipSuccess && nb) e = hipMemcpy(offsets, ho.data(), nb * 8, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = launch_compact(d.syn, n, offsets, dst, nullptr);
@@ -239,15 +239,13 @@ abnn_status structural_update(abnn_brain* b)
         if (e == hipSuccess) e = hipMemset(d.grown, 0, slots * sizeof(uint4));
         added = app.size();
     }
+    if (e == hipSuccess && dead && nb) e = hipMemset(dead, 0, nb * 4);
     if (e == hipSuccess) e = hipDeviceSynchronize();
-    (void)hipFree(counts);
-    (void)hipFree(offsets);
     if (e != hipSuccess) {
-        (void)hipFree(dst);
         set_err(std::string("structural update: ") + hipGetErrorString(e));
         return ABNN_ERR_HIP;
     }
-    (void)hipFree(d.syn);
+    b->syn_alt = d.syn;
     d.syn = dst;
     b->dims.n_syn = live + added;
     uint64_t grown = 0;
@@ -458,6 +456,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.dummy = dummy;
     if ((s = dalloc(&d.apply_partial, kTileBlocks)) != ABNN_OK) return fail(s);
     if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, cap)) != ABNN_OK) return fail(s);
+    if (p.compact_every > 0) {  // structural updates: the compaction's second buffer + scratch
+        const uint64_t nb = (cap + kCompactChunk - 1) / kCompactChunk;
+        if ((s = dalloc(&b->syn_alt, cap + kDummyRecords)) != ABNN_OK) return fail(s);
+        if ((s = dalloc(&b->compact_offsets, nb)) != ABNN_OK) return fail(s);
+        if (p.w_prune > 0.0f && (s = dalloc(&d.dead, nb)) != ABNN_OK) return fail(s);
+    }
     if (genesis) {
         if ((s = dalloc(&d.g2src, max_tiles * kTile)) != ABNN_OK) return fail(s);
         if ((s = dalloc(&d.grown, (uint64_t)p.compact_every * p.max_spikes)) != ABNN_OK) return fail(s);

@@ -54,6 +54,7 @@ struct DeviceState {
     uint4* apply_partial;     // [kTileBlocks] {updated, fired, pruned, 0} per apply workgroup
     uint32_t* g2src;          // genesis on: [max tiles * kTile] src of the visited record
     uint4* grown;             // genesis on: [compact_every * max_spikes] grown records (w = 1: used)
+    uint32_t* dead;           // pruning on: tombstones per kCompactChunk records (structural update)
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     int32_t* fired;           // [max_spikes] internal spike list (world = 1)
     int64_t* summary;         // [ABNN_SUMMARY_WORDS] internal (world = 1)
@@ -107,9 +108,8 @@ hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int6
 hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
                            uint32_t world, const int32_t* fired, hipStream_t s);
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);
-// Structural update: live records per kCompactChunk block, then a stable
-// compaction into `dst` at the given per-block offsets.
-hipError_t launch_count_live(const uint4* syn, uint64_t n, uint32_t* counts, hipStream_t s);
+// Structural update: stable compaction into `dst`, block b of kCompactChunk
+// records starting at offsets[b] (live counts from the k_apply tombstone tally).
 hipError_t launch_compact(const uint4* syn, uint64_t n, const uint64_t* offsets, uint4* dst, hipStream_t s);
 hipError_t launch_generate(const DeviceState& d, uint32_t n_in, uint32_t n_out, uint64_t seed,
                            hipStream_t s);

@@ -674,6 +674,7 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
         if (store && prune && w < kp.w_prune) {  // README §5: the synapse is removed
             __builtin_nontemporal_store(u32x4_t{0xFFFFFFFFu, 0xFFFFFFFFu, __float_as_uint(w), 0u},
                                         reinterpret_cast<u32x4_t*>(d.syn + ri));
+            if (d.dead) atomicAdd(d.dead + ri / kCompactChunk, 1u);  // tally for the structural update
             ++npr;
         } else if (store) {
             __builtin_nontemporal_store(__float_as_uint(w), reinterpret_cast<uint32_t*>(d.syn + ri) + 2);
@@ -786,44 +787,33 @@ __global__ __launch_bounds__(256) void k_renorm(DeviceState d, uint64_t base)
 }
 
 // ---------------------------------------------------------------------------
-// Structural update (README §5): stable removal of the tombstones.  Each
-// thread owns kCompactChunk / kCompactThreads consecutive records.
-__global__ __launch_bounds__(kCompactThreads) void k_count_live(const uint4* syn, uint64_t n, uint32_t* counts)
-{
-    __shared__ uint32_t s_c[kCompactThreads / 64];
-    const uint64_t base = (uint64_t)blockIdx.x * kCompactChunk + (uint64_t)threadIdx.x * 4;
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        if (base + j < n && syn[base + j].x != 0xFFFFFFFFu) ++c;
-    c = wave_sum(c);
-    if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int w = 0; w < kCompactThreads / 64; ++w) t += s_c[w];
-        counts[blockIdx.x] = t;
-    }
-}
-
+// Structural update (README §5): stable removal of the tombstones.  Block b
+// moves records [b * kCompactChunk, (b + 1) * kCompactChunk) to dst from
+// offsets[b] on, in four coalesced rounds of kCompactThreads consecutive
+// records (one block scan of the live flags per round), streaming both ways.
 __global__ __launch_bounds__(kCompactThreads) void k_compact(const uint4* syn, uint64_t n, const uint64_t* offsets,
                                                              uint4* dst)
 {
     static_assert(kCompactThreads == kScanThreads, "block_exclusive_scan is sized for kScanThreads");
     __shared__ uint64_t s_wave[kCompactThreads / 64];
-    const uint64_t base = (uint64_t)blockIdx.x * kCompactChunk + (uint64_t)threadIdx.x * 4;
+    const uint64_t base = (uint64_t)blockIdx.x * kCompactChunk;
     uint4 r[4];
-    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // all four loads in flight first
+        const uint64_t i = base + (uint64_t)j * kCompactThreads + threadIdx.x;
+        r[j] = i < n ? load_stream16(syn + i) : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+    }
+    uint64_t o = offsets[blockIdx.x];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        r[j] = base + j < n ? syn[base + j] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
-        c += r[j].x != 0xFFFFFFFFu ? 1u : 0u;
+        const bool live = r[j].x != 0xFFFFFFFFu;
+        uint64_t tot;
+        const uint64_t pre = block_exclusive_scan(live ? 1u : 0u, &tot, s_wave);
+        if (live)
+            __builtin_nontemporal_store(u32x4_t{r[j].x, r[j].y, r[j].z, r[j].w},
+                                        reinterpret_cast<u32x4_t*>(dst + o + pre));
+        o += tot;
     }
-    uint64_t total;
-    uint64_t o = offsets[blockIdx.x] + block_exclusive_scan(c, &total, s_wave);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        if (r[j].x != 0xFFFFFFFFu) dst[o++] = r[j];
 }
 
 // ---------------------------------------------------------------------------
@@ -1010,14 +1000,6 @@ hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s)
 {
     hipLaunchKernelGGL(k_renorm, dim3(blocks_for(d.n_nrn > 0 ? d.n_nrn : 1)), dim3(256), 0, s, d,
                        base);
-    return hipGetLastError();
-}
-
-hipError_t launch_count_live(const uint4* syn, uint64_t n, uint32_t* counts, hipStream_t s)
-{
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_count_live, dim3((uint32_t)((n + kCompactChunk - 1) / kCompactChunk)),
-                       dim3(kCompactThreads), 0, s, syn, n, counts);
     return hipGetLastError();
 }
 
