@@ -1,5 +1,7 @@
 """Pass time with and without hipGraph replay (ABNN_GRAPH), timing off,
-config 3, one process per setting (the env var is read at create)."""
+config 3, one process per setting (the env var is read at create).  The
+graph path was measured slower (profiles/r01_hipgraph_ab.txt) and removed
+from the library; re-adding it is what this script would A/B again."""
 import os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROG = r'''
