@@ -12,14 +12,14 @@ namespace abnn {
 
 // Pre-spike filter kept in LDS by every gate workgroup: the exact recent-spike
 // bitmap folded modulo filter_words 32-bit words (16384 words = 512 Ki bits =
-// 64 KiB by default).  When the bitmap itself fits, the filter IS the bitmap.
+// 32 KiB by default).  When the bitmap itself fits, the filter IS the bitmap.
 constexpr int kMaxFilterWords = 16384;
 constexpr int kTile = 64;          // one tile = 64 consecutive pre-gated events of a range = one wave
 constexpr int kTileBlocks = 2048;  // grid of the tile kernels (x 4 waves = 8192 waves, all resident)
 constexpr int kScanThreads = 1024; // the range and tile scans are one workgroup each
 constexpr int kMaxGateBlocks = 1024;
-constexpr int kMaxRanges = 16384;
-static_assert(kTileBlocks % kScanThreads == 0, "k_finalize sums the apply partials in whole rounds");  // kMaxGateBlocks x up to 16 waves; staged whole in LDS by k_tiles
+constexpr int kMaxRanges = 16384;  // kMaxGateBlocks x up to 16 waves; k_tiles holds them in registers
+static_assert(kTileBlocks % kScanThreads == 0, "k_finalize sums the apply partials in whole rounds");
 constexpr int kDummyRecords = 64 * 16;  // >= 64 lanes x max events per lane; also the record-buffer padding
 constexpr int kStageEntries = 448;      // per gate wave: 4-B event offsets staged in LDS
 

@@ -1,29 +1,32 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of one C1 traversal pass.
 //
 // Reference hot path: monte_carlo_traversal (abnn/src/core/kernels/brain.metal:41-130)
-// and renormalise_clock_and_times (brain.metal:135-145).  One pass = six launches,
-// each doing one HBM-friendly thing:
+// and renormalise_clock_and_times (brain.metal:135-145).  One pass = seven
+// launches, each doing one HBM-friendly thing:
 //
 //   k_bitmap   : lastFired (u64, 8 B/neuron, read once) -> exact recent-spike
 //                bitmap, bit i = (now - lastFired[i]) <= WINDOW_PRE, OR-folded
-//                modulo 512 Ki bits into the 64 KiB pre-spike filter; the
-//                per-pass stimulus stamp is fused here.
+//                into the LDS filter image; the per-pass stimulus stamp is
+//                fused here.
 //   k_gate     : THE streaming kernel.  Persistent workgroups whose waves each
-//                sweep one contiguous range of events with non-temporal dwordx4 loads of
-//                the 16-B SynapsePacked records (1 KiB per wave-instruction,
-//                next iteration's loads in flight while the current one is
-//                gated).  Pre-spike gate (brain.metal:73-77) = one LDS filter
-//                bit (+ an L2 bitmap word on a filter hit unless the filter is
-//                exact); refractory gate (brain.metal:79-83) = a real 8-B gather
-//                of lastFired[dst] for the few events that pass; spike-candidate
-//                test (brain.metal:91-92); each wave compacts its gated events
-//                in event order into its own region with their wave-local
-//                candidate prefix (ballots only, no barrier).
-//   k_scan     : one workgroup: exclusive candidate prefix over the wave
-//                ranges = the ordered global spike budget of schedule C1
-//                (brain.metal:85-98 without its races) + the apply tiling.
+//                sweep one contiguous range of events, loading only the src
+//                word of every 16-B SynapsePacked record (the same HBM lines,
+//                one VGPR per event in flight).  Pre-spike gate
+//                (brain.metal:73-77) = one LDS filter bit + an L2 bitmap word
+//                on a filter hit; passing events are staged in event order as
+//                4-B offsets and flushed once per range.  Random-edge mode:
+//                the same loop on Philox-picked records.
+//   k_tiles    : one workgroup: 64-entry tiles over the ranges (descriptors).
+//   k_refrac   : per tile: the record re-read, the refractory gate
+//                (brain.metal:79-83) with a real lastFired[dst] gather, the
+//                spike-candidate test (brain.metal:91-92), isi.
+//   k_scan     : one workgroup: exclusive candidate prefix over the tiles =
+//                the ordered global spike budget of schedule C1
+//                (brain.metal:85-98 without its races) + the shard summary.
 //   k_apply    : weight update (brain.metal:101-122) of every gated event that
-//                still had budget; spikes land at their budget position.
+//                still had budget (non-temporal stores; pruning, synaptogenesis);
+//                spikes land at their budget position.  k_claim precedes it in
+//                random mode (highest event wins a record).
 //   k_finalize : deferred lastFired stamps (brain.metal:125-126), rBar EWMA
 //                (brain.metal:110-113), one clock tick (brain.metal:129).
 //   k_renorm   : brain.metal:135-145 with the base read once (no race).
