@@ -67,7 +67,7 @@ class Scalars(C.Structure):
 
 
 MODE_SWEEP, MODE_RANDOM = 0, 1  # abnn_params.mode (include/abnn/abnn.h)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class Stats(C.Structure):
@@ -135,9 +135,10 @@ SIGNATURES = [
     ("abnn_set_auto_stimulus", C.c_int, [_VP, _U64, _U64]),
     ("abnn_traverse", C.c_int, [_VP, _U32, _VP]),
     ("abnn_synchronize", C.c_int, [_VP, _VP]),
+    ("abnn_exchange_bytes", C.c_uint64, [_VP]),
     ("abnn_shard_gate", C.c_int, [_VP, _VP, _VP]),
-    ("abnn_shard_apply", C.c_int, [_VP, _VP, _U32, _U32, _VP, _VP]),
-    ("abnn_shard_commit", C.c_int, [_VP, _VP, _U32, _VP, _VP]),
+    ("abnn_shard_apply", C.c_int, [_VP, _VP, _U32, _U32, _VP]),
+    ("abnn_shard_commit", C.c_int, [_VP, _VP, _U32, _VP]),
     ("abnn_get_stats", C.c_int, [_VP, C.POINTER(Stats)]),
     ("abnn_reset_stats", C.c_int, [_VP]),
     ("abnn_enable_timing", C.c_int, [_VP, C.c_int]),

@@ -200,16 +200,18 @@ class Brain:
     def synchronize(self, stream=None) -> None:
         call("abnn_synchronize", self._h, _stream_ptr(stream))
 
-    def shard_gate(self, summary_ptr: int, stream=None) -> None:
-        call("abnn_shard_gate", self._h, summary_ptr, _stream_ptr(stream))
+    def exchange_bytes(self) -> int:
+        """Bytes of this shard's exchange record (summary + local spike list, abnn.h)."""
+        return int(self._lib.abnn_exchange_bytes(self._h))
 
-    def shard_apply(self, summaries_ptr: int, world: int, rank: int, fired_ptr: int,
-                    stream=None) -> None:
-        call("abnn_shard_apply", self._h, summaries_ptr, world, rank, fired_ptr,
-             _stream_ptr(stream))
+    def shard_gate(self, xchg_ptr: int, stream=None) -> None:
+        call("abnn_shard_gate", self._h, xchg_ptr, _stream_ptr(stream))
 
-    def shard_commit(self, summaries_ptr: int, world: int, fired_ptr: int, stream=None) -> None:
-        call("abnn_shard_commit", self._h, summaries_ptr, world, fired_ptr, _stream_ptr(stream))
+    def shard_apply(self, gathered_ptr: int, world: int, rank: int, stream=None) -> None:
+        call("abnn_shard_apply", self._h, gathered_ptr, world, rank, _stream_ptr(stream))
+
+    def shard_commit(self, gathered_ptr: int, world: int, stream=None) -> None:
+        call("abnn_shard_commit", self._h, gathered_ptr, world, _stream_ptr(stream))
 
     # ---- statistics / timing ------------------------------------------------------------------
     def stats(self) -> dict:

@@ -99,7 +99,7 @@ void free_all(abnn_brain* b)
                     b->d.tile_mask, b->d.tile_pre,   b->d.g1idx,    b->d.g2e,         b->d.apply_partial,
                     b->d.claim,     b->d.g2src,      b->d.grown,         b->syn_alt,
                     b->d.dead,      b->compact_offsets,
-                    b->d.fired,     b->d.summary,    b->d.work,          b->idx_scratch,
+                    b->d.xchg,      b->d.work,          b->idx_scratch,
                     b->u64_scratch,  const_cast<uint4*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -257,7 +257,7 @@ abnn_status structural_update(abnn_brain* b)
 }
 
 // bitmap + streaming gate + chunk scan: the first half of every pass.
-abnn_status run_gate(abnn_brain* b, int64_t* summary_out, hipStream_t s)
+abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, bool sharded, hipStream_t s)
 {
     HIP_TRY(launch_bitmap(b->d, b->kp, b->stim_first, b->stim_count, s));
     EventPair* ev = nullptr;
@@ -265,14 +265,14 @@ abnn_status run_gate(abnn_brain* b, int64_t* summary_out, hipStream_t s)
     HIP_TRY(launch_gate(b->d, b->kp, s));
     if (ev) HIP_TRY(hipEventRecord(ev->b, s));
     HIP_TRY(launch_refrac(b->d, b->kp, s));
-    HIP_TRY(launch_scan(b->d, b->kp, summary_out, s));
+    HIP_TRY(launch_scan(b->d, b->kp, xchg_out, sharded, s));
     return ABNN_OK;
 }
 
-abnn_status run_commit(abnn_brain* b, const int64_t* summaries, uint32_t world,
-                       const int32_t* fired, bool renorm, hipStream_t s)
+abnn_status run_commit(abnn_brain* b, const int32_t* gathered, uint32_t world, bool renorm,
+                       hipStream_t s)
 {
-    HIP_TRY(launch_finalize(b->d, b->kp, summaries, world, fired, s));
+    HIP_TRY(launch_finalize(b->d, b->kp, gathered, world, s));
     host_tick(b);
     if (renorm) {  // renormalise_if_needed, brain.cpp:125-141; kernel brain.metal:135-145
         HIP_TRY(launch_renorm(b->d, b->clock_host, s));
@@ -466,8 +466,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
         if ((s = dalloc(&d.g2src, max_tiles * kTile)) != ABNN_OK) return fail(s);
         if ((s = dalloc(&d.grown, (uint64_t)p.compact_every * p.max_spikes)) != ABNN_OK) return fail(s);
     }
-    if ((s = dalloc(&d.fired, p.max_spikes + 1u)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.summary, ABNN_SUMMARY_WORDS)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.xchg, xchg_words(p.max_spikes))) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
     *out = b;
@@ -700,9 +699,9 @@ abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream)
     for (uint32_t i = 0; i < passes; ++i) {
         // the host reads the clock at encode time, before the pass (brain.cpp:127-128)
         const bool renorm = b->clock_host > b->params.renorm_thresh;
-        ST_TRY(run_gate(b, b->d.summary, s));
-        HIP_TRY(launch_apply(b->d, b->kp, b->d.summary, 1, 0, b->d.fired, s));
-        ST_TRY(run_commit(b, b->d.summary, 1, b->d.fired, renorm, s));
+        ST_TRY(run_gate(b, b->d.xchg, false, s));
+        HIP_TRY(launch_apply(b->d, b->kp, b->d.xchg, 1, 0, b->d.xchg + 2 * ABNN_SUMMARY_WORDS, s));
+        ST_TRY(run_commit(b, b->d.xchg, 1, renorm, s));
     }
     return ABNN_OK;
 }
@@ -715,37 +714,42 @@ abnn_status abnn_synchronize(abnn_brain* b, void* stream)
     return sync_all(b);
 }
 
-abnn_status abnn_shard_gate(abnn_brain* b, int64_t* summary_dev, void* stream)
+uint64_t abnn_exchange_bytes(const abnn_brain* b)
 {
-    REQUIRE(b && summary_dev, "null argument");
+    return b ? 4ull * xchg_words(b->params.max_spikes) : 0;
+}
+
+abnn_status abnn_shard_gate(abnn_brain* b, void* xchg_dev, void* stream)
+{
+    REQUIRE(b && xchg_dev, "null argument");
+    REQUIRE(((uintptr_t)xchg_dev & 7u) == 0, "exchange record must be 8-B aligned");
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
     b->pending_renorm = b->clock_host > b->params.renorm_thresh;
-    return run_gate(b, summary_dev, s);
+    return run_gate(b, static_cast<int32_t*>(xchg_dev), true, s);
 }
 
-abnn_status abnn_shard_apply(abnn_brain* b, const int64_t* summaries_dev, uint32_t world,
-                             uint32_t rank, int32_t* fired_dev, void* stream)
+abnn_status abnn_shard_apply(abnn_brain* b, const void* gathered_dev, uint32_t world, uint32_t rank,
+                             void* stream)
 {
-    REQUIRE(b && summaries_dev && fired_dev, "null argument");
+    REQUIRE(b && gathered_dev, "null argument");
     REQUIRE(world >= 1 && rank < world, "bad world/rank");
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
-    HIP_TRY(hipMemsetAsync(fired_dev, 0, (size_t)b->params.max_spikes * 4, s));
-    HIP_TRY(launch_apply(b->d, b->kp, summaries_dev, world, rank, fired_dev, s));
+    HIP_TRY(launch_apply(b->d, b->kp, static_cast<const int32_t*>(gathered_dev), world, rank,
+                         nullptr, s));
     return ABNN_OK;
 }
 
-abnn_status abnn_shard_commit(abnn_brain* b, const int64_t* summaries_dev, uint32_t world,
-                              const int32_t* fired_dev, void* stream)
+abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t world, void* stream)
 {
-    REQUIRE(b && summaries_dev && fired_dev, "null argument");
+    REQUIRE(b && gathered_dev, "null argument");
     REQUIRE(world >= 1, "bad world");
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
     const bool renorm = b->pending_renorm;
     b->pending_renorm = false;
-    return run_commit(b, summaries_dev, world, fired_dev, renorm, s);
+    return run_commit(b, static_cast<const int32_t*>(gathered_dev), world, renorm, s);
 }
 
 abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out)

@@ -56,8 +56,7 @@ struct DeviceState {
     uint4* grown;             // genesis on: [compact_every * max_spikes] grown records (w = 1: used)
     uint32_t* dead;           // pruning on: tombstones per kCompactChunk records (structural update)
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
-    int32_t* fired;           // [max_spikes] internal spike list (world = 1)
-    int64_t* summary;         // [ABNN_SUMMARY_WORDS] internal (world = 1)
+    int32_t* xchg;            // internal exchange record (world = 1): summary + spike list
     PassWork* work;
     uint64_t n_syn;           // local records
     uint64_t n_nrn;
@@ -86,6 +85,13 @@ struct KernelParams {
     uint32_t compact_every;
 };
 
+// Shard exchange record (abnn.h): ABNN_SUMMARY_WORDS int64, then max_spikes
+// int32 spikes padded to 8 B -- in int32 words:
+__host__ __device__ constexpr uint32_t xchg_words(uint32_t max_spikes)
+{
+    return 2 * ABNN_SUMMARY_WORDS + ((max_spikes + 1u) & ~1u);
+}
+
 constexpr int kCompactThreads = 1024;  // structural update: 4 consecutive records per thread
 constexpr int kCompactChunk = 4 * kCompactThreads;
 
@@ -101,12 +107,15 @@ hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t 
                          uint64_t stim_count, hipStream_t s);
 hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s);
 hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream_t s);
-hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int64_t* summary_out,
-                       hipStream_t s);
-hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
-                        uint32_t world, uint32_t rank, int32_t* fired, hipStream_t s);
-hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
-                           uint32_t world, const int32_t* fired, hipStream_t s);
+// launch_scan writes the exchange record's summary; with `spike_list` also its
+// spike list (sharded passes).  launch_apply writes the list into `spikes`
+// when non-null (the single-GPU pass, where it is the only rank).
+hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out,
+                       bool spike_list, hipStream_t s);
+hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
+                        uint32_t world, uint32_t rank, int32_t* spikes, hipStream_t s);
+hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
+                           uint32_t world, hipStream_t s);
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);
 // Structural update: stable compaction into `dst`, block b of kCompactChunk
 // records starting at offsets[b] (live counts from the k_apply tombstone tally).

@@ -540,8 +540,9 @@ __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
 // Up to kSuper tiles per round: wave w scans a contiguous block of 64-tile
 // chunks held in registers; rounds carry the prefix (warm-up passes only).
 __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelParams kp,
-                                                       int64_t* summary_out)
+                                                       int32_t* xchg_out)
 {
+    int64_t* summary_out = reinterpret_cast<int64_t*>(xchg_out);
     constexpr uint32_t NWv = kScanThreads / 64, kCh = 16, kSuper = NWv * kCh * 64;
     __shared__ uint32_t s_wt[NWv];
     __shared__ uint64_t s_red[NWv];
@@ -607,17 +608,41 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelPara
 }
 
 // ---------------------------------------------------------------------------
+// k_spikes (sharded passes only): this shard's spike list in local budget
+// order, written into its exchange record before the all-gather, so that every
+// rank can stamp every rank's spikes in k_finalize.  Same tile walk as k_apply.
+// The single-GPU pass skips it: k_apply writes the list there, in the same
+// order, at no extra launch.
+__global__ __launch_bounds__(256) void k_spikes(DeviceState d, KernelParams kp, int32_t* spikes)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
+    const uint64_t budget = kp.max_spikes;
+    const uint32_t T = d.work->total_tiles;
+    for (uint32_t tile = wave; tile < T; tile += nwaves) {
+        const uint64_t P = d.tile_pre[tile];
+        if (P >= budget) continue;
+        const uint4 m = d.tile_mask[tile];
+        const uint64_t bc = m.z | ((uint64_t)m.w << 32);
+        if (!((bc >> lane) & 1u)) continue;
+        const uint64_t pre = P + mbcnt64(bc);
+        if (pre < budget) spikes[pre] = (int32_t)d.g2e[(uint64_t)tile * kTile + lane].y;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_claim (random mode): every event that will reach the update raises its
 // record's claim to its event index + 1, so k_apply lets only the highest
 // store (the last writer in event order).  Same tile walk as k_apply.
-__global__ __launch_bounds__(256) void k_claim(DeviceState d, KernelParams kp, const int64_t* summaries,
+__global__ __launch_bounds__(256) void k_claim(DeviceState d, KernelParams kp, const int32_t* gathered,
                                                uint32_t rank)
 {
+    const uint32_t words = xchg_words(kp.max_spikes);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
     const uint64_t budget = kp.max_spikes, pass = *d.pass_index;
     uint64_t off = 0;
-    for (uint32_t q = 0; q < rank; ++q) off += (uint64_t)summaries[q * ABNN_SUMMARY_WORDS + 0];
+    for (uint32_t q = 0; q < rank; ++q) off += (uint64_t)*reinterpret_cast<const int64_t*>(gathered + q * words);
     off = off < budget ? off : budget;
     const uint32_t T = d.work->total_tiles;
     for (uint32_t tile = wave; tile < T; tile += nwaves) {
@@ -636,16 +661,16 @@ __global__ __launch_bounds__(256) void k_claim(DeviceState d, KernelParams kp, c
 // k_apply: weight update of the gated events that still had budget; one wave
 // per tile, tiles past the budget skipped on one load.
 __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
-                                               const int64_t* summaries, uint32_t world,
-                                               uint32_t rank, int32_t* fired)
+                                               const int32_t* gathered, uint32_t rank,
+                                               int32_t* spikes)
 {
+    const uint32_t words = xchg_words(kp.max_spikes);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
     const uint64_t budget = kp.max_spikes;
     const float R = *d.reward, rb = *d.rbar;  // pass-start values (C1), brain.metal:105-106
     uint64_t off = 0;
-    for (uint32_t q = 0; q < rank && q < world; ++q)
-        off += (uint64_t)summaries[q * ABNN_SUMMARY_WORDS + 0];
+    for (uint32_t q = 0; q < rank; ++q) off += (uint64_t)*reinterpret_cast<const int64_t*>(gathered + q * words);
     off = off < budget ? off : budget;
 
     const uint32_t T = d.work->total_tiles;
@@ -683,8 +708,8 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
             __builtin_nontemporal_store(__float_as_uint(w), reinterpret_cast<uint32_t*>(d.syn + ri) + 2);
         }
         ++upd;
-        if (f) {
-            fired[pre] = (int32_t)e.y;  // dst, spike list in budget order
+        if (f) {  // its stamp comes from the exchange record (k_finalize)
+            if (spikes) spikes[pre] = (int32_t)e.y;  // single GPU: off == 0, local order
             ++nf;
             if (genesis) {  // README §5 synaptogenesis: slot `pre` of this pass
                 const uint64_t x = splitmix64_at(d.seed ^ ABNN_GENESIS_KEY, (pass << 32) | pre);
@@ -715,29 +740,33 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
 // ---------------------------------------------------------------------------
 // k_finalize: stamps, rBar, clock tick, statistics (one workgroup).
 __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, KernelParams kp,
-                                                           const int64_t* summaries, uint32_t world,
-                                                           const int32_t* fired)
+                                                           const int32_t* gathered, uint32_t world)
 {
     constexpr uint32_t kU = 4;
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, words = xchg_words(kp.max_spikes);
     const uint64_t now = *d.clock;
     const uint64_t budget = kp.max_spikes;
-    uint64_t total = 0, events = 0;
+    uint64_t events = 0, off = 0;
+    int64_t t0 = 0;
     for (uint32_t r = 0; r < world; ++r) {
-        total += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 0];
-        events += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 2];
-    }
-    const uint64_t n_fired = total < budget ? total : budget;
-    for (uint64_t i0 = 0; i0 < n_fired; i0 += kU * kScanThreads) {
-        uint32_t n[kU];
+        const int64_t* sm = reinterpret_cast<const int64_t*>(gathered + r * words);
+        const int32_t* sp = gathered + r * words + 2 * ABNN_SUMMARY_WORDS;
+        events += (uint64_t)sm[2];
+        t0 |= sm[1];
+        // rank r's spikes fill budget slots [off, off + n): brain.metal:125-126, deferred
+        const uint64_t room = budget - off, n = (uint64_t)sm[0] < room ? (uint64_t)sm[0] : room;
+        for (uint64_t i0 = 0; i0 < n; i0 += kU * kScanThreads) {
+            uint32_t nrn[kU];
 #pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-            const uint64_t i = i0 + u * kScanThreads + tid;
-            n[u] = i < n_fired ? (uint32_t)fired[i] : 0xFFFFFFFFu;
+            for (uint32_t u = 0; u < kU; ++u) {
+                const uint64_t i = i0 + u * kScanThreads + tid;
+                nrn[u] = i < n ? (uint32_t)sp[i] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kU; ++u)
+                if (nrn[u] < d.n_nrn) d.last_fired[nrn[u]] = now;
         }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u)
-            if (n[u] < d.n_nrn) d.last_fired[n[u]] = now;  // brain.metal:125-126, deferred
+        off += n;
     }
     uint32_t upd = 0, nf = 0, npr = 0;
 #pragma unroll
@@ -765,7 +794,7 @@ __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, Kernel
             tp += s_p[w];
         }
         const float R = *d.reward, rb = *d.rbar;
-        if (summaries[1] != 0 && budget > 0)
+        if (t0 != 0 && budget > 0)
             *d.rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
         if (events > 0) *d.clock = now + kp.clock_inc; // brain.metal:129
         *d.pass_index += 1;
@@ -972,30 +1001,35 @@ hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int64_t* summary_out,
-                       hipStream_t s)
+hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out,
+                       bool spike_list, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, d, kp, summary_out);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, d, kp, xchg_out);
+    if (!spike_list) return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_spikes, dim3(kTileBlocks), dim3(256), 0, s, d, kp,
+                       xchg_out + 2 * ABNN_SUMMARY_WORDS);
     return hipGetLastError();
 }
 
-hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
-                        uint32_t world, uint32_t rank, int32_t* fired, hipStream_t s)
+hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
+                        uint32_t world, uint32_t rank, int32_t* spikes, hipStream_t s)
 {
+    if (spikes && (world != 1 || rank != 0)) return hipErrorInvalidValue;
     if (d.mode == ABNN_MODE_RANDOM) {
-        hipLaunchKernelGGL(k_claim, dim3(kTileBlocks), dim3(256), 0, s, d, kp, summaries, rank);
+        hipLaunchKernelGGL(k_claim, dim3(kTileBlocks), dim3(256), 0, s, d, kp, gathered, rank);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_apply, dim3(kTileBlocks), dim3(256), 0, s, d, kp, summaries, world,
-                       rank, fired);
+    hipLaunchKernelGGL(k_apply, dim3(kTileBlocks), dim3(256), 0, s, d, kp, gathered, rank, spikes);
     return hipGetLastError();
 }
 
-hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int64_t* summaries,
-                           uint32_t world, const int32_t* fired, hipStream_t s)
+hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
+                           uint32_t world, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kScanThreads), 0, s, d, kp, summaries, world, fired);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kScanThreads), 0, s, d, kp, gathered, world);
     return hipGetLastError();
 }
 

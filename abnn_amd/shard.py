@@ -3,16 +3,15 @@
 The reference is single-GPU (no NCCL/MPI anywhere).  The build
 shards the synapse array in contiguous ranges across ranks, replicates the
 neuron state (lastFired, lastVisited, clock, reward, rBar) and keeps schedule
-C1 bit-exact with two tiny exchanges per pass:
-
-  1. all-gather of each shard's summary (4 x int64: spike candidates capped at
-     the budget, global-event-0 gated flag, visited events, gated events) --
-     every rank then knows its offset in the ordered global spike budget;
-  2. all-reduce(SUM) of the spike list (max_spikes x int32): every shard writes
-     its spikes at their global budget positions, the other slots are zero.
-     All stamps of a pass write the same value ``now``, so this sparse merge
-     equals the north-star all-reduce(MAX) over lastFired exactly, at 10 KB
-     instead of 40 MB per pass.
+C1 bit-exact with ONE exchange per pass: after the gate phase
+every rank all-gathers each rank's record (include/abnn/abnn.h) -- its
+summary (4 x int64: spike candidates capped at the budget, global-event-0
+flag, visited events, gated events) followed by its spikes in local budget
+order (max_spikes x int32).  From the gathered records every rank knows its
+offset in the ordered global spike budget (apply) and the global spike list
+(rank order = budget order: commit stamps it).  All stamps of a pass write the
+same value ``now``, so this equals the north-star all-reduce(MAX) over
+lastFired exactly, at ~10 KB per rank instead of 40 MB per pass.
 
 ``lastVisited`` feeds no decision (brain.metal:44), so it is merged lazily with
 all-reduce(MAX) by :meth:`ShardedBrain.sync_visits`.
@@ -24,7 +23,6 @@ from typing import Protocol
 import numpy as np
 
 from .brain import Brain, visited_events
-from ._lib import SUMMARY_WORDS
 
 
 def shard_ranges(n_syn_global: int, world: int) -> list[tuple[int, int]]:
@@ -47,11 +45,11 @@ def global_events(n_syn_global: int, events_per_pass: int, world: int, mode: int
 class Engine(Protocol):
     """One shard's pass phases (the GPU Brain, or a CPU stand-in in tests)."""
 
-    def gate(self, summary) -> None: ...
+    def gate(self, xchg) -> None: ...
 
-    def apply(self, summaries, world: int, rank: int, fired) -> None: ...
+    def apply(self, gathered, world: int, rank: int) -> None: ...
 
-    def commit(self, summaries, world: int, fired) -> None: ...
+    def commit(self, gathered, world: int) -> None: ...
 
 
 class TorchComm:
@@ -83,20 +81,16 @@ class TorchComm:
     def all_gather(self, out, inp) -> None:
         self._run(lambda o, i: self._dist.all_gather_into_tensor(o, i, group=self.group), out, inp)
 
-    def all_reduce_sum(self, t) -> None:
-        self._run(lambda x: self._dist.all_reduce(x, op=self._dist.ReduceOp.SUM, group=self.group), t)
-
     def all_reduce_max(self, t) -> None:
         self._run(lambda x: self._dist.all_reduce(x, op=self._dist.ReduceOp.MAX, group=self.group), t)
 
 
-def sharded_pass(engine: Engine, comm, summary, gathered, fired) -> None:
-    """One C1 pass over all shards: gate -> all-gather -> apply -> all-reduce -> commit."""
-    engine.gate(summary)
-    comm.all_gather(gathered, summary)
-    engine.apply(gathered, comm.world, comm.rank, fired)
-    comm.all_reduce_sum(fired)
-    engine.commit(gathered, comm.world, fired)
+def sharded_pass(engine: Engine, comm, xchg, gathered) -> None:
+    """One C1 pass over all shards: gate -> all-gather of the records -> apply -> commit."""
+    engine.gate(xchg)
+    comm.all_gather(gathered, xchg)
+    engine.apply(gathered, comm.world, comm.rank)
+    engine.commit(gathered, comm.world)
 
 
 class _GpuEngine:
@@ -104,14 +98,14 @@ class _GpuEngine:
         self.brain = brain
         self._stream = stream_fn
 
-    def gate(self, summary) -> None:
-        self.brain.shard_gate(summary.data_ptr(), self._stream())
+    def gate(self, xchg) -> None:
+        self.brain.shard_gate(xchg.data_ptr(), self._stream())
 
-    def apply(self, summaries, world, rank, fired) -> None:
-        self.brain.shard_apply(summaries.data_ptr(), world, rank, fired.data_ptr(), self._stream())
+    def apply(self, gathered, world, rank) -> None:
+        self.brain.shard_apply(gathered.data_ptr(), world, rank, self._stream())
 
-    def commit(self, summaries, world, fired) -> None:
-        self.brain.shard_commit(summaries.data_ptr(), world, fired.data_ptr(), self._stream())
+    def commit(self, gathered, world) -> None:
+        self.brain.shard_commit(gathered.data_ptr(), world, self._stream())
 
 
 class ShardedBrain:
@@ -135,15 +129,14 @@ class ShardedBrain:
                            **param_overrides)
         dev = torch.device("cuda", device)
         self._torch = torch
-        self.summary = torch.zeros(SUMMARY_WORDS, dtype=torch.int64, device=dev)
-        self.gathered = torch.zeros(SUMMARY_WORDS * self.world, dtype=torch.int64, device=dev)
-        spikes = max(1, int(self.brain.params.max_spikes))
-        self.fired = torch.zeros(spikes, dtype=torch.int32, device=dev)
+        words = self.brain.exchange_bytes() // 4
+        self.xchg = torch.zeros(words, dtype=torch.int32, device=dev)
+        self.gathered = torch.zeros(words * self.world, dtype=torch.int32, device=dev)
         self.engine = _GpuEngine(self.brain, lambda: torch.cuda.current_stream(dev))
 
     def step(self, passes: int = 1) -> None:
         for _ in range(passes):
-            sharded_pass(self.engine, self.comm, self.summary, self.gathered, self.fired)
+            sharded_pass(self.engine, self.comm, self.xchg, self.gathered)
 
     def local_events(self) -> int:
         return self.brain.visited_events()
@@ -152,6 +145,6 @@ class ShardedBrain:
         """Lazy all-reduce(MAX) of lastVisited (never read by a decision)."""
         torch = self._torch
         lv = self.brain.last_visited().view(np.int64)
-        t = torch.from_numpy(lv.copy()).to(self.summary.device)
+        t = torch.from_numpy(lv.copy()).to(self.xchg.device)
         self.comm.all_reduce_max(t)
         self.brain.set_last_visited(t.cpu().numpy().view(np.uint64))

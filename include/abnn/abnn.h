@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ABNN_ABI_VERSION 2
+#define ABNN_ABI_VERSION 3
 
 typedef enum abnn_status {
     ABNN_OK = 0,
@@ -261,26 +261,29 @@ abnn_status abnn_set_auto_stimulus(abnn_brain* b, uint64_t first, uint64_t count
 abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream);
 abnn_status abnn_synchronize(abnn_brain* b, void* stream);
 
-/* ---- sharded passes (synapse-shard data parallelism, DESIGN.md §6) --------
- * One pass on rank r of W = three calls with two tiny exchanges between them:
- *   abnn_shard_gate   -> writes this shard's summary (ABNN_SUMMARY_WORDS int64)
- *                        to `summary_dev`;
- *   [all-gather the W summaries into `summaries_dev` (W*ABNN_SUMMARY_WORDS)]
- *   abnn_shard_apply  -> zeroes `fired_dev` (max_spikes int32) and writes this
- *                        shard's spikes at their global budget positions;
- *   [all-reduce(SUM) `fired_dev` across ranks]
- *   abnn_shard_commit -> stamps lastFired, updates rBar, ticks the clock,
- *                        renormalises if due.
- * All pointers are device pointers; the exchanges are the caller's (RCCL via
- * torch.distributed in abnn_amd/shard.py).  W = 1 with the local summary is
+/* ---- sharded passes (synapse-shard data parallelism, DESIGN.md §7) --------
+ * One pass on rank r of W = three calls around ONE exchange:
+ *   abnn_shard_gate   -> writes this shard's exchange record to `xchg_dev`
+ *                        (abnn_exchange_bytes(b) bytes): ABNN_SUMMARY_WORDS
+ *                        int64 {spike candidates capped at the budget, global
+ *                        event 0 reached the update, visited events, passed the
+ *                        refractory gate}, then the shard's spikes (dst, int32)
+ *                        in local budget order, max_spikes slots (padded to 8 B);
+ *   [all-gather the W records, rank order, into `gathered_dev`]
+ *   abnn_shard_apply  -> weight updates of this shard's events that fall inside
+ *                        the global budget (offset = capped sum of lower ranks);
+ *   abnn_shard_commit -> stamps every shard's spikes in rank order (= global
+ *                        budget order, the first max_spikes), updates rBar,
+ *                        ticks the clock, renormalises if due.
+ * All pointers are device pointers; the exchange is the caller's (RCCL via
+ * torch.distributed in abnn_amd/shard.py).  W = 1 with the local record is
  * exactly abnn_traverse.                                                     */
-#define ABNN_SUMMARY_WORDS 4 /* {spike candidates (capped), t0 updated, events, g2} */
-abnn_status abnn_shard_gate(abnn_brain* b, int64_t* summary_dev, void* stream);
-abnn_status abnn_shard_apply(abnn_brain* b, const int64_t* summaries_dev,
-                             uint32_t world, uint32_t rank, int32_t* fired_dev,
-                             void* stream);
-abnn_status abnn_shard_commit(abnn_brain* b, const int64_t* summaries_dev,
-                              uint32_t world, const int32_t* fired_dev,
+#define ABNN_SUMMARY_WORDS 4
+uint64_t abnn_exchange_bytes(const abnn_brain* b);
+abnn_status abnn_shard_gate(abnn_brain* b, void* xchg_dev, void* stream);
+abnn_status abnn_shard_apply(abnn_brain* b, const void* gathered_dev, uint32_t world,
+                             uint32_t rank, void* stream);
+abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t world,
                               void* stream);
 
 /* ---- statistics / timing ---------------------------------------------------- */

@@ -519,8 +519,12 @@ static uint64_t apply_range(oracle_state* s, const oracle_g2* g, uint64_t n, uin
     return nf;
 }
 
-int64_t oracle_shard_gate(oracle_state* s, oracle_g2* out, uint64_t cap,
-                          int64_t summary[ABNN_SUMMARY_WORDS])
+uint32_t oracle_exchange_words(uint32_t max_spikes)
+{
+    return 2u * ABNN_SUMMARY_WORDS + ((max_spikes + 1u) & ~1u);
+}
+
+int64_t oracle_shard_gate(oracle_state* s, oracle_g2* out, uint64_t cap, int32_t* xchg)
 {
     (void)pass_begin(s); /* stimulus; the renorm decision is re-taken in commit */
     uint64_t E = events_of(s);
@@ -530,27 +534,32 @@ int64_t oracle_shard_gate(oracle_state* s, oracle_g2* out, uint64_t cap,
     s->stats.pre_gated += c.g1;
     s->stats.post_gated += c.g2;
     s->stats.events += E;
+    int64_t* summary = (int64_t*)xchg;
+    int32_t* spikes = xchg + 2 * ABNN_SUMMARY_WORDS;
     summary[0] = (int64_t)(c.cand < s->p.max_spikes ? c.cand : s->p.max_spikes);
     summary[1] = c.t0;
     summary[2] = (int64_t)E;
     summary[3] = (int64_t)c.g2;
+    memset(spikes, 0, sizeof(int32_t) * ((s->p.max_spikes + 1u) & ~1u));
+    for (uint64_t j = 0; j < g.n; ++j)  /* local spikes in local budget order */
+        if (g.v[j].cand) spikes[g.v[j].pre] = (int32_t)s->syn[rec_index(s, g.v[j].t)].dst;
     return g.overflow ? -1 : (int64_t)g.n;
 }
 
-static uint64_t shard_offset(const int64_t* summaries, uint32_t rank, uint32_t budget)
+static uint64_t shard_offset(const int32_t* gathered, uint32_t rank, uint32_t budget)
 {
+    const uint32_t words = oracle_exchange_words(budget);
     uint64_t off = 0;
-    for (uint32_t r = 0; r < rank; ++r) off += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 0];
+    for (uint32_t r = 0; r < rank; ++r) off += (uint64_t) * (const int64_t*)(gathered + r * words);
     return off < budget ? off : budget;
 }
 
 void oracle_shard_apply(oracle_state* s, const oracle_g2* g2, int64_t n_g2,
-                        const int64_t* summaries, uint32_t world, uint32_t rank,
-                        int32_t* fired)
+                        const int32_t* gathered, uint32_t world, uint32_t rank)
 {
     (void)world;
-    memset(fired, 0, sizeof(int32_t) * s->p.max_spikes);
-    uint64_t off = shard_offset(summaries, rank, s->p.max_spikes);
+    int32_t* fired = (int32_t*)calloc(s->p.max_spikes + 1u, sizeof(int32_t)); /* unused: stamps come from the records */
+    uint64_t off = shard_offset(gathered, rank, s->p.max_spikes);
     uint64_t nu = 0;
     pend_list pend = {NULL, 0, 0};
     const int random = s->p.mode == ABNN_MODE_RANDOM;
@@ -560,21 +569,27 @@ void oracle_shard_apply(oracle_state* s, const oracle_g2* g2, int64_t n_g2,
     s->stats.pruned += np;
     s->stats.updated += nu;
     s->stats.fired += nf;
+    free(fired);
 }
 
-void oracle_shard_commit(oracle_state* s, const int64_t* summaries, uint32_t world,
-                         const int32_t* fired)
+void oracle_shard_commit(oracle_state* s, const int32_t* gathered, uint32_t world)
 {
-    uint64_t total = 0, events = 0;
-    for (uint32_t r = 0; r < world; ++r) {
-        total += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 0];
-        events += (uint64_t)summaries[r * ABNN_SUMMARY_WORDS + 2];
-    }
-    uint64_t n_fired = total < s->p.max_spikes ? total : s->p.max_spikes;
+    const uint32_t words = oracle_exchange_words(s->p.max_spikes);
+    const uint64_t budget = s->p.max_spikes;
+    uint64_t events = 0, off = 0;
+    int64_t t0 = 0;
     int renorm = s->clock > s->p.renorm_thresh;
     uint64_t now = s->clock;
-    for (uint64_t i = 0; i < n_fired; ++i) s->last_fired[(uint32_t)fired[i]] = now;
-    if (summaries[1] && s->p.max_spikes > 0)
+    for (uint32_t r = 0; r < world; ++r) {
+        const int64_t* sm = (const int64_t*)(gathered + r * words);
+        const int32_t* sp = gathered + r * words + 2 * ABNN_SUMMARY_WORDS;
+        events += (uint64_t)sm[2];
+        t0 |= sm[1];
+        uint64_t room = budget - off, n = (uint64_t)sm[0] < room ? (uint64_t)sm[0] : room;
+        for (uint64_t i = 0; i < n; ++i) s->last_fired[(uint32_t)sp[i]] = now;  /* rank order = budget order */
+        off += n;
+    }
+    if (t0 && s->p.max_spikes > 0)
         s->rbar = s->rbar + s->p.alpha_rbar * (s->reward - s->rbar);
     if (events > 0) s->clock = now + s->p.clock_inc;
     if (renorm) {

@@ -75,14 +75,15 @@ void oracle_pass_serial(oracle_state* s);
  * the CPU baseline timed by bench.py. */
 void oracle_pass_threaded(oracle_state* s, int nthreads);
 
-/* Sharded phases (the host exchange is the caller's; see tests/). */
-int64_t oracle_shard_gate(oracle_state* s, oracle_g2* out, uint64_t cap,
-                          int64_t summary[ABNN_SUMMARY_WORDS]);
+/* Sharded phases with one exchange (abnn.h): gate writes this shard's
+ * record (summary + local spike list, oracle_exchange_words int32), the
+ * caller all-gathers the W records in rank order, apply and commit read
+ * them.  Returns the number of stored G2 entries (-1: `out` overflowed). */
+uint32_t oracle_exchange_words(uint32_t max_spikes);
+int64_t oracle_shard_gate(oracle_state* s, oracle_g2* out, uint64_t cap, int32_t* xchg);
 void oracle_shard_apply(oracle_state* s, const oracle_g2* g2, int64_t n_g2,
-                        const int64_t* summaries, uint32_t world, uint32_t rank,
-                        int32_t* fired);
-void oracle_shard_commit(oracle_state* s, const int64_t* summaries, uint32_t world,
-                         const int32_t* fired);
+                        const int32_t* gathered, uint32_t world, uint32_t rank);
+void oracle_shard_commit(oracle_state* s, const int32_t* gathered, uint32_t world);
 
 #ifdef __cplusplus
 }

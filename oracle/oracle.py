@@ -80,9 +80,10 @@ def load() -> C.CDLL:
             "oracle_read_outputs": (None, [C.POINTER(State), vp, u32]),
             "oracle_pass_serial": (None, [C.POINTER(State)]),
             "oracle_pass_threaded": (None, [C.POINTER(State), C.c_int]),
+            "oracle_exchange_words": (u32, [u32]),
             "oracle_shard_gate": (C.c_int64, [C.POINTER(State), vp, u64, vp]),
-            "oracle_shard_apply": (None, [C.POINTER(State), vp, C.c_int64, vp, u32, u32, vp]),
-            "oracle_shard_commit": (None, [C.POINTER(State), vp, u32, vp]),
+            "oracle_shard_apply": (None, [C.POINTER(State), vp, C.c_int64, vp, u32, u32]),
+            "oracle_shard_commit": (None, [C.POINTER(State), vp, u32]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(lib, name)
@@ -223,24 +224,28 @@ class OracleBrain:
         for _ in range(passes):
             self._lib.oracle_pass_threaded(C.byref(self.s), nthreads)
 
-    # shard phases --------------------------------------------------------------------------
-    def shard_gate(self, summary: np.ndarray) -> np.ndarray:
+    # shard phases (one exchange: include/abnn/abnn.h) ------------------------------------
+    def exchange_words(self) -> int:
+        """int32 words of one shard's exchange record (summary + local spike list)."""
+        return int(self._lib.oracle_exchange_words(self.p.max_spikes))
+
+    def shard_gate(self, xchg: np.ndarray) -> np.ndarray:
+        """Gate phase; writes this shard's record into `xchg` (int32, exchange_words())."""
+        assert xchg.dtype == np.int32 and xchg.shape[0] >= self.exchange_words()
         ev = visited_events(int(self.s.dims.events_per_pass), int(self.s.dims.n_syn), int(self.p.mode))
         buf = np.zeros(max(1, ev), dtype=G2_DTYPE)
-        n = self._lib.oracle_shard_gate(C.byref(self.s), buf.ctypes.data, buf.shape[0],
-                                        summary.ctypes.data)
+        n = self._lib.oracle_shard_gate(C.byref(self.s), buf.ctypes.data, buf.shape[0], xchg.ctypes.data)
         if n < 0:
             raise RuntimeError("oracle_shard_gate overflow")
         self._g2 = buf[:n].copy()
         return self._g2
 
-    def shard_apply(self, summaries: np.ndarray, world: int, rank: int, fired: np.ndarray) -> None:
+    def shard_apply(self, gathered: np.ndarray, world: int, rank: int) -> None:
         self._lib.oracle_shard_apply(C.byref(self.s), self._g2.ctypes.data, self._g2.shape[0],
-                                     summaries.ctypes.data, world, rank, fired.ctypes.data)
+                                     gathered.ctypes.data, world, rank)
 
-    def shard_commit(self, summaries: np.ndarray, world: int, fired: np.ndarray) -> None:
-        self._lib.oracle_shard_commit(C.byref(self.s), summaries.ctypes.data, world,
-                                      fired.ctypes.data)
+    def shard_commit(self, gathered: np.ndarray, world: int) -> None:
+        self._lib.oracle_shard_commit(C.byref(self.s), gathered.ctypes.data, world)
 
     @property
     def clock(self) -> int:

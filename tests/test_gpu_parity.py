@@ -9,6 +9,8 @@ import os
 import numpy as np
 import pytest
 
+from shard_helpers import GpuShards, oracle_shard_pass
+
 pytestmark = pytest.mark.gpu
 
 
@@ -145,22 +147,12 @@ def _virtual_shard_run(world, n_syn, events, passes, n_hidden=30_000, seed=4):
         b.build_random_graph(seed)
         b.set_auto_stimulus(0, 256)
         shards.append(b)
-    dev = torch.device("cuda", 0)
-    summ = torch.zeros(world, 4, dtype=torch.int64, device=dev)
-    fired = torch.zeros(world, 2560, dtype=torch.int32, device=dev)
-    tot = torch.zeros(2560, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    gs = GpuShards(shards)
     for k in range(passes):
         if k == 6:
             for b in shards:
                 b.set_reward(0.125)
-        for r, b in enumerate(shards):
-            b.shard_gate(summ[r].data_ptr(), stream)
-        for r, b in enumerate(shards):
-            b.shard_apply(summ.data_ptr(), world, r, fired[r].data_ptr(), stream)
-        torch.sum(fired, dim=0, dtype=torch.int32, out=tot)
-        for b in shards:
-            b.shard_commit(summ.data_ptr(), world, tot.data_ptr(), stream)
+        gs.pass_()
     torch.cuda.synchronize()
     return shards
 
@@ -199,15 +191,7 @@ def test_virtual_shards_partial_sweep_vs_oracle_shards(gpu):
         if k == 6:
             for ob in obs:
                 ob.set_reward(0.125)
-        summ = np.zeros((world, 4), dtype=np.int64)
-        for r, ob in enumerate(obs):
-            ob.shard_gate(summ[r])
-        fired = np.zeros((world, 2560), dtype=np.int32)
-        for r, ob in enumerate(obs):
-            ob.shard_apply(summ.reshape(-1), world, r, fired[r])
-        tot = fired.sum(axis=0).astype(np.int32)
-        for ob in obs:
-            ob.shard_commit(summ.reshape(-1), world, tot)
+        oracle_shard_pass(obs)
     for b, ob in zip(shards, obs):
         _assert_same(b, ob, "shard")
 

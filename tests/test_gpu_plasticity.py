@@ -7,6 +7,8 @@ Python restatement in tests/test_oracle.py."""
 import numpy as np
 import pytest
 
+from shard_helpers import GpuShards, oracle_shard_pass
+
 pytestmark = pytest.mark.gpu
 
 SP = dict(w_prune=0.105, p_new=0.35, w_init=0.5, compact_every=2)
@@ -88,28 +90,10 @@ def test_plasticity_virtual_shards_vs_oracle_shards(gpu):
     ge = global_events(n_syn, events, world)
     pairs = [_pair(0, n_syn=hi - lo, events=events, syn_offset=lo, global_events=ge)
              for lo, hi in shard_ranges(n_syn, world)]
-    dev = torch.device("cuda", 0)
-    summ = torch.zeros(world, 4, dtype=torch.int64, device=dev)
-    fired = torch.zeros(world, 2560, dtype=torch.int32, device=dev)
-    tot = torch.zeros(2560, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    gs = GpuShards([g for g, _ in pairs])
     for k in range(passes):
-        for r, (g, _) in enumerate(pairs):
-            g.shard_gate(summ[r].data_ptr(), stream)
-        for r, (g, _) in enumerate(pairs):
-            g.shard_apply(summ.data_ptr(), world, r, fired[r].data_ptr(), stream)
-        torch.sum(fired, dim=0, dtype=torch.int32, out=tot)
-        for g, _ in pairs:
-            g.shard_commit(summ.data_ptr(), world, tot.data_ptr(), stream)
-        osumm = np.zeros((world, 4), dtype=np.int64)
-        for r, (_, o) in enumerate(pairs):
-            o.shard_gate(osumm[r])
-        ofired = np.zeros((world, 2560), dtype=np.int32)
-        for r, (_, o) in enumerate(pairs):
-            o.shard_apply(osumm.reshape(-1), world, r, ofired[r])
-        otot = ofired.sum(axis=0).astype(np.int32)
-        for _, o in pairs:
-            o.shard_commit(osumm.reshape(-1), world, otot)
+        gs.pass_()
+        oracle_shard_pass([o for _, o in pairs])
     torch.cuda.synchronize()
     for g, o in pairs:
         _same(g, o, "shard")

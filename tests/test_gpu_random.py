@@ -6,6 +6,8 @@ an independent Python restatement in tests/test_oracle.py) is the only pin."""
 import numpy as np
 import pytest
 
+from shard_helpers import GpuShards, oracle_shard_pass
+
 pytestmark = pytest.mark.gpu
 
 
@@ -106,28 +108,10 @@ def test_random_virtual_shards_vs_oracle_shards(gpu):
         ob.build_random_graph(4, nthreads=16)
         ob.set_auto_stimulus(0, 256)
         obs.append(ob)
-    dev = torch.device("cuda", 0)
-    summ = torch.zeros(world, 4, dtype=torch.int64, device=dev)
-    fired = torch.zeros(world, 2560, dtype=torch.int32, device=dev)
-    tot = torch.zeros(2560, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    gs = GpuShards(shards)
     for k in range(passes):
-        for r, b in enumerate(shards):
-            b.shard_gate(summ[r].data_ptr(), stream)
-        for r, b in enumerate(shards):
-            b.shard_apply(summ.data_ptr(), world, r, fired[r].data_ptr(), stream)
-        torch.sum(fired, dim=0, dtype=torch.int32, out=tot)
-        for b in shards:
-            b.shard_commit(summ.data_ptr(), world, tot.data_ptr(), stream)
-        osumm = np.zeros((world, 4), dtype=np.int64)
-        for r, ob in enumerate(obs):
-            ob.shard_gate(osumm[r])
-        ofired = np.zeros((world, 2560), dtype=np.int32)
-        for r, ob in enumerate(obs):
-            ob.shard_apply(osumm.reshape(-1), world, r, ofired[r])
-        otot = ofired.sum(axis=0).astype(np.int32)
-        for ob in obs:
-            ob.shard_commit(osumm.reshape(-1), world, otot)
+        gs.pass_()
+        oracle_shard_pass(obs)
     torch.cuda.synchronize()
     for b, ob in zip(shards, obs):
         _same(b, ob, "shard")

@@ -6,6 +6,7 @@ import pytest
 
 from oracle import oracle as O
 from py_reference import MetalEmu, rand01 as py_rand01
+from shard_helpers import oracle_shard_pass
 
 PARAMS = dict(base_scale=0.8, refractory=2, window_pre=5, clock_inc=1, target_rate_hz=1000.0,
               eta_home=1e-6, eta_reward=1e-3, alpha_rbar=0.001, a_ltp=0.04, a_ltd=0.02,
@@ -185,15 +186,7 @@ def _sharded_full(world, passes=8):
         if k == 5:
             for ob in shards:
                 ob.set_reward(-0.5)
-        summ = np.zeros((world, 4), dtype=np.int64)
-        for r, ob in enumerate(shards):
-            ob.shard_gate(summ[r])
-        fired = np.zeros((world, 2560), dtype=np.int32)
-        for r, ob in enumerate(shards):
-            ob.shard_apply(summ.reshape(-1), world, r, fired[r])
-        tot = fired.sum(axis=0).astype(np.int32)
-        for ob in shards:
-            ob.shard_commit(summ.reshape(-1), world, tot)
+        oracle_shard_pass(shards)
     return shards
 
 
@@ -292,11 +285,7 @@ def test_random_mode_shard_phases_world1_equal_serial():
     a, b = _random_brain(), _random_brain()
     for _ in range(6):
         a.pass_serial()
-        summ = np.zeros(4, dtype=np.int64)
-        b.shard_gate(summ)
-        fired = np.zeros(2560, dtype=np.int32)
-        b.shard_apply(summ, 1, 0, fired)
-        b.shard_commit(summ, 1, fired)
+        oracle_shard_pass([b])
     assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32))
     assert np.array_equal(a.last_fired, b.last_fired)
     assert a.scalars() == b.scalars()
@@ -385,10 +374,6 @@ def test_structural_shard_world1_equals_serial(mode):
     a, b = _sp_brain(mode), _sp_brain(mode)
     for _ in range(6):
         a.pass_serial()
-        summ = np.zeros(4, dtype=np.int64)
-        b.shard_gate(summ)
-        fired = np.zeros(2560, dtype=np.int32)
-        b.shard_apply(summ, 1, 0, fired)
-        b.shard_commit(summ, 1, fired)
+        oracle_shard_pass([b])
     assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32))
     assert a.stats() == b.stats()

@@ -20,14 +20,14 @@ class CpuShardEngine:
     def __init__(self, ob):
         self.ob = ob
 
-    def gate(self, summary):
-        self.ob.shard_gate(summary.numpy())
+    def gate(self, xchg):
+        self.ob.shard_gate(xchg.numpy())
 
-    def apply(self, summaries, world, rank, fired):
-        self.ob.shard_apply(summaries.numpy(), world, rank, fired.numpy())
+    def apply(self, gathered, world, rank):
+        self.ob.shard_apply(gathered.numpy(), world, rank)
 
-    def commit(self, summaries, world, fired):
-        self.ob.shard_commit(summaries.numpy(), world, fired.numpy())
+    def commit(self, gathered, world):
+        self.ob.shard_commit(gathered.numpy(), world)
 
 
 def _free_port():
@@ -59,13 +59,13 @@ def _worker(rank, world, port, events, track):
         ob.build_random_graph(seed=11, nthreads=2)
         ob.set_auto_stimulus(0, 256)
         eng = CpuShardEngine(ob)
-        summary = torch.zeros(4, dtype=torch.int64)
-        gathered = torch.zeros(4 * world, dtype=torch.int64)
-        fired = torch.zeros(2560, dtype=torch.int32)
+        words = ob.exchange_words()
+        xchg = torch.zeros(words, dtype=torch.int32)
+        gathered = torch.zeros(words * world, dtype=torch.int32)
         for k in range(PASSES):
             if k == 6:
                 ob.set_reward(0.25)
-            sharded_pass(eng, comm, summary, gathered, fired)
+            sharded_pass(eng, comm, xchg, gathered)
         if track:  # lazy lastVisited merge (all-reduce MAX)
             t = torch.from_numpy(ob.last_visited.view(np.int64).copy())
             comm.all_reduce_max(t)
@@ -123,6 +123,9 @@ def _worker_modes(rank, world, port, events, extra):
     from abnn_amd.shard import TorchComm, global_events, shard_ranges, sharded_pass
     from oracle import oracle as O
 
+    sys.path.insert(0, os.path.join(root, "tests"))
+    from shard_helpers import oracle_shard_pass
+
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -132,28 +135,20 @@ def _worker_modes(rank, world, port, events, extra):
         cap = 1.1 if extra.get("p_new") else 1.0
         ob = _shard_brains(world, events, extra, O, shard_ranges, ge, cap)[rank]
         eng = CpuShardEngine(ob)
-        summary = torch.zeros(4, dtype=torch.int64)
-        gathered = torch.zeros(4 * world, dtype=torch.int64)
-        fired = torch.zeros(2560, dtype=torch.int32)
+        words = ob.exchange_words()
+        xchg = torch.zeros(words, dtype=torch.int32)
+        gathered = torch.zeros(words * world, dtype=torch.int32)
         for k in range(PASSES):
             if k == 4:
                 ob.set_reward(0.3)
-            sharded_pass(eng, comm, summary, gathered, fired)
+            sharded_pass(eng, comm, xchg, gathered)
 
         ref = _shard_brains(world, events, extra, O, shard_ranges, ge, cap)
         for k in range(PASSES):
             if k == 4:
                 for r in ref:
                     r.set_reward(0.3)
-            summ = np.zeros((world, 4), dtype=np.int64)
-            for q, r in enumerate(ref):
-                r.shard_gate(summ[q])
-            fr = np.zeros((world, 2560), dtype=np.int32)
-            for q, r in enumerate(ref):
-                r.shard_apply(summ.reshape(-1), world, q, fr[q])
-            tot = fr.sum(axis=0).astype(np.int32)
-            for r in ref:
-                r.shard_commit(summ.reshape(-1), world, tot)
+            oracle_shard_pass(ref)
         me = ref[rank]
         assert int(ob.s.dims.n_syn) == int(me.s.dims.n_syn)
         assert np.array_equal(ob.syn.view(np.uint32), me.syn.view(np.uint32))
