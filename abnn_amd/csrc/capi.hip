@@ -72,7 +72,7 @@ struct abnn_brain {
     uint64_t pass_host = 0;        // mirror of pass_index (structural-update schedule)
     // structural updates (compact_every > 0): the second record buffer the
     // compaction writes into (swapped with d.syn), and its scan scratch
-    uint4* syn_alt = nullptr;
+    SynArrays syn_alt{};
     uint64_t* compact_offsets = nullptr;
 };
 
@@ -94,13 +94,15 @@ void free_all(abnn_brain* b)
 {
     if (!b) return;
     (void)hipSetDevice(b->device);
-    void* ptrs[] = {b->d.syn,       b->d.last_fired, b->d.last_visited,  b->scalar_block,
+    void* ptrs[] = {b->d.syn.src,   b->d.syn.dst,    b->d.syn.w,
+                    b->syn_alt.src, b->syn_alt.dst,  b->syn_alt.w,
+                    b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->d.bitmap,    b->d.filter,     b->d.range_cnt,     b->d.tile_desc,
                     b->d.tile_mask, b->d.tile_pre,   b->d.g1idx,    b->d.g2e,         b->d.apply_partial,
-                    b->d.claim,     b->d.g2src,      b->d.grown,         b->syn_alt,
+                    b->d.claim,     b->d.g2src,      b->d.grown,
                     b->d.dead,      b->compact_offsets,
                     b->d.xchg,      b->d.work,          b->idx_scratch,
-                    b->u64_scratch,  const_cast<uint4*>(b->d.dummy)};
+                    b->u64_scratch,  const_cast<uint32_t*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : b->events) {
@@ -142,6 +144,56 @@ abnn_status ensure_idx_scratch(abnn_brain* b, uint64_t n)
     b->idx_cap = 0;
     ST_TRY(dalloc(&b->idx_scratch, n));
     b->idx_cap = n;
+    return ABNN_OK;
+}
+
+// Device records are three arrays (SynArrays); abnn_synapse is the host
+// interchange format.  Capacity `count` per array.
+abnn_status alloc_syn(SynArrays* a, uint64_t count)
+{
+    ST_TRY(dalloc(&a->src, count));
+    ST_TRY(dalloc(&a->dst, count));
+    return dalloc(&a->w, count);
+}
+
+// Chunked copies between device arrays [first, first + n) and host records.
+constexpr uint64_t kXferRecs = 1u << 22;
+
+abnn_status records_d2h(const SynArrays& a, uint64_t first, uint64_t n, abnn_synapse* out)
+{
+    std::vector<uint32_t> s, t;
+    std::vector<float> w;
+    for (uint64_t i = 0; i < n; i += kXferRecs) {
+        const uint64_t m = std::min<uint64_t>(kXferRecs, n - i);
+        s.resize(m);
+        t.resize(m);
+        w.resize(m);
+        HIP_TRY(hipMemcpy(s.data(), a.src + first + i, m * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(t.data(), a.dst + first + i, m * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(w.data(), a.w + first + i, m * 4, hipMemcpyDeviceToHost));
+        for (uint64_t k = 0; k < m; ++k) out[i + k] = {s[k], t[k], w[k], 0.0f};
+    }
+    return ABNN_OK;
+}
+
+abnn_status records_h2d(const SynArrays& a, uint64_t first, uint64_t n, const abnn_synapse* in)
+{
+    std::vector<uint32_t> s, t;
+    std::vector<float> w;
+    for (uint64_t i = 0; i < n; i += kXferRecs) {
+        const uint64_t m = std::min<uint64_t>(kXferRecs, n - i);
+        s.resize(m);
+        t.resize(m);
+        w.resize(m);
+        for (uint64_t k = 0; k < m; ++k) {
+            s[k] = in[i + k].src;
+            t[k] = in[i + k].dst;
+            w[k] = in[i + k].w;
+        }
+        HIP_TRY(hipMemcpy(a.src + first + i, s.data(), m * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(a.dst + first + i, t.data(), m * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(a.w + first + i, w.data(), m * 4, hipMemcpyHostToDevice));
+    }
     return ABNN_OK;
 }
 
@@ -214,7 +266,7 @@ abnn_status structural_update(abnn_brain* b)
     // Double-buffered: records past n_syn are never read as events (the gate
     // masks lanes beyond the sweep, picks stay below n_syn), so the spare
     // buffer needs no clearing.
-    uint4* dst = b->syn_alt;
+    const SynArrays dst = b->syn_alt;
     std::vector<uint32_t> hc(nb);
     std::vector<uint64_t> ho(nb);
     hipError_t e = hipSuccess;
@@ -231,11 +283,15 @@ abnn_status structural_update(abnn_brain* b)
         const uint64_t slots = (uint64_t)b->params.compact_every * b->params.max_spikes;
         std::vector<uint4> g(slots);
         e = hipMemcpy(g.data(), d.grown, slots * sizeof(uint4), hipMemcpyDeviceToHost);
-        std::vector<uint4> app;
+        std::vector<abnn_synapse> app;
         for (uint64_t j = 0; e == hipSuccess && j < slots && live + app.size() < cap; ++j)
-            if (g[j].w == 1u) app.push_back(make_uint4(g[j].x, g[j].y, g[j].z, 0u));
-        if (e == hipSuccess && !app.empty())
-            e = hipMemcpy(dst + live, app.data(), app.size() * sizeof(uint4), hipMemcpyHostToDevice);
+            if (g[j].w == 1u) {
+                float w;
+                std::memcpy(&w, &g[j].z, 4);
+                app.push_back({g[j].x, g[j].y, w, 0.0f});
+            }
+        if (e == hipSuccess && !app.empty() && records_h2d(dst, live, app.size(), app.data()) != ABNN_OK)
+            e = hipErrorUnknown;
         if (e == hipSuccess) e = hipMemset(d.grown, 0, slots * sizeof(uint4));
         added = app.size();
     }
@@ -432,7 +488,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     abnn_status s;
     // build_buffers, brain.cpp:52-69: allocate and zero every buffer.
     // padded: the gate's last iteration reads up to one iteration past the sweep
-    if ((s = dalloc(&d.syn, cap + kDummyRecords)) != ABNN_OK) return fail(s);
+    if ((s = alloc_syn(&d.syn, cap + kDummyRecords)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_fired, n_nrn)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_visited, n_nrn)) != ABNN_OK) return fail(s);
     uint64_t* sb = nullptr;
@@ -451,14 +507,14 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.tile_pre, max_tiles)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.g1idx, iters * iter_events)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.g2e, max_tiles * kTile)) != ABNN_OK) return fail(s);
-    uint4* dummy = nullptr;
+    uint32_t* dummy = nullptr;
     if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
     d.dummy = dummy;
     if ((s = dalloc(&d.apply_partial, kTileBlocks)) != ABNN_OK) return fail(s);
     if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, cap)) != ABNN_OK) return fail(s);
     if (p.compact_every > 0) {  // structural updates: the compaction's second buffer + scratch
         const uint64_t nb = (cap + kCompactChunk - 1) / kCompactChunk;
-        if ((s = dalloc(&b->syn_alt, cap + kDummyRecords)) != ABNN_OK) return fail(s);
+        if ((s = alloc_syn(&b->syn_alt, cap + kDummyRecords)) != ABNN_OK) return fail(s);
         if ((s = dalloc(&b->compact_offsets, nb)) != ABNN_OK) return fail(s);
         if (p.w_prune > 0.0f && (s = dalloc(&d.dead, nb)) != ABNN_OK) return fail(s);
     }
@@ -500,7 +556,9 @@ abnn_status abnn_get_params(const abnn_brain* b, abnn_params* out)
 abnn_status abnn_state_ptrs(abnn_brain* b, abnn_state* out)
 {
     REQUIRE(b && out, "null argument");
-    out->synapses = reinterpret_cast<abnn_synapse*>(b->d.syn);
+    out->syn_src = b->d.syn.src;
+    out->syn_dst = b->d.syn.dst;
+    out->syn_w = b->d.syn.w;
     out->last_fired = b->d.last_fired;
     out->last_visited = b->d.last_visited;
     out->clock = b->d.clock;
@@ -517,8 +575,7 @@ abnn_status abnn_upload_synapses(abnn_brain* b, uint64_t first, const abnn_synap
     REQUIRE(first <= b->dims.n_syn && n <= b->dims.n_syn - first, "range out of bounds");
     ST_TRY(validate_records(b, src, n));
     ST_TRY(sync_all(b));
-    HIP_TRY(hipMemcpy(b->d.syn + first, src, n * sizeof(abnn_synapse), hipMemcpyHostToDevice));
-    return ABNN_OK;
+    return records_h2d(b->d.syn, first, n, src);
 }
 
 abnn_status abnn_download_synapses(abnn_brain* b, uint64_t first, abnn_synapse* dst, uint64_t n)
@@ -526,8 +583,7 @@ abnn_status abnn_download_synapses(abnn_brain* b, uint64_t first, abnn_synapse* 
     REQUIRE(b && (dst || n == 0), "null argument");
     REQUIRE(first <= b->dims.n_syn && n <= b->dims.n_syn - first, "range out of bounds");
     ST_TRY(sync_all(b));
-    HIP_TRY(hipMemcpy(dst, b->d.syn + first, n * sizeof(abnn_synapse), hipMemcpyDeviceToHost));
-    return ABNN_OK;
+    return records_d2h(b->d.syn, first, n, dst);
 }
 
 abnn_status abnn_generate_synapses(abnn_brain* b, uint64_t seed)
@@ -812,9 +868,8 @@ abnn_status abnn_save_bnn(abnn_brain* b, const char* path)
     for (uint64_t i = 0; ok && i < b->dims.n_syn; i += kIoRecs) {
         const uint64_t n = std::min<uint64_t>(kIoRecs, b->dims.n_syn - i);
         buf.resize(n);
-        if (hipMemcpy(buf.data(), b->d.syn + i, n * 16, hipMemcpyDeviceToHost) != hipSuccess) {
+        if (records_d2h(b->d.syn, i, n, buf.data()) != ABNN_OK) {
             std::fclose(f);
-            set_err("hipMemcpy D2H failed");
             return ABNN_ERR_HIP;
         }
         ok = std::fwrite(buf.data(), 16, n, f) == n;  // brain.cpp:165-166
@@ -861,10 +916,7 @@ abnn_status abnn_load_bnn(abnn_brain* b, const char* path)
             return ABNN_ERR_IO;
         }
         st = validate_records(b, buf.data(), n);
-        if (st == ABNN_OK && hipMemcpy(b->d.syn + i, buf.data(), n * 16, hipMemcpyHostToDevice) != hipSuccess) {
-            set_err("hipMemcpy H2D failed");
-            st = ABNN_ERR_HIP;
-        }
+        if (st == ABNN_OK) st = records_h2d(b->d.syn, i, n, buf.data());
         if (st != ABNN_OK) {
             std::fclose(f);
             return st;
@@ -895,7 +947,7 @@ abnn_status abnn_save_flat(abnn_brain* b, const char* path)
         for (uint64_t i = 0; ok && i < b->dims.n_syn; i += kIoRecs) {
             const uint64_t n = std::min<uint64_t>(kIoRecs, b->dims.n_syn - i);
             buf.resize(n);
-            if (hipMemcpy(buf.data(), b->d.syn + i, n * 16, hipMemcpyDeviceToHost) != hipSuccess) {
+            if (records_d2h(b->d.syn, i, n, buf.data()) != ABNN_OK) {
                 ok = false;
                 break;
             }
@@ -976,7 +1028,7 @@ abnn_status abnn_load_flat(abnn_brain* b, const char* path)
             std::fclose(f);
             return st;
         }
-        ok = hipMemcpy(b->d.syn + i, buf.data(), n * 16, hipMemcpyHostToDevice) == hipSuccess;
+        ok = records_h2d(b->d.syn, i, n, buf.data()) == ABNN_OK;
     }
     std::vector<uint64_t> ts(b->n_nrn);
     if (ok) ok = std::fseek(f, weights_at + (long)(4 * N), SEEK_SET) == 0;

@@ -20,7 +20,7 @@ constexpr int kScanThreads = 1024; // the range and tile scans are one workgroup
 constexpr int kMaxGateBlocks = 1024;
 constexpr int kMaxRanges = 16384;  // kMaxGateBlocks x up to 16 waves; k_tiles holds them in registers
 static_assert(kTileBlocks % kScanThreads == 0, "k_finalize sums the apply partials in whole rounds");
-constexpr int kDummyRecords = 64 * 16;  // >= 64 lanes x max events per lane; also the record-buffer padding
+constexpr int kDummyRecords = 64 * 32;  // >= 64 lanes x max events per lane; also the record-buffer padding
 constexpr int kStageEntries = 448;      // per gate wave: 4-B event offsets staged in LDS
 
 // Per-pass bookkeeping in device memory (one per handle).
@@ -33,9 +33,20 @@ struct alignas(16) PassWork {
     abnn_stats stats;      // cumulative (finalize adds)
 };
 
+// Synapse records on the device, structure of arrays: record i is
+// {src[i], dst[i], w[i]} (SynapsePacked without its never-read pad).  The
+// sweep's gate streams only src: 4 B per visited event instead of 16.  Each
+// array holds capacity + kDummyRecords entries (zero padding: the gate's last
+// iteration reads past the sweep).
+struct SynArrays {
+    uint32_t* src;
+    uint32_t* dst;
+    float* w;
+};
+
 // Kernel-facing view of a handle's device state.
 struct DeviceState {
-    uint4* syn;               // abnn_synapse[n_syn + kDummyRecords] viewed as 16-B vectors (zero padding)
+    SynArrays syn;            // [capacity + kDummyRecords] each
     uint64_t* last_fired;     // [n_nrn]
     uint64_t* last_visited;   // [n_nrn]
     uint64_t* clock;          // [1]
@@ -50,7 +61,7 @@ struct DeviceState {
     uint32_t* tile_pre;       // [max_tiles] exclusive candidate prefix (capped; = budget: skip)
     uint32_t* g1idx;          // [iters * iter_events] pre-gated event offsets (event - region), per-range regions
     uint4* g2e;               // [max_tiles * kTile] {event - region, dst, w, isi} of the events that passed
-    const uint4* dummy;       // [kDummyRecords] zero records: target of masked-off stream loads
+    const uint32_t* dummy;    // [kDummyRecords] zeros: target of the stream loads past a range
     uint4* apply_partial;     // [kTileBlocks] {updated, fired, pruned, 0} per apply workgroup
     uint32_t* g2src;          // genesis on: [max tiles * kTile] src of the visited record
     uint4* grown;             // genesis on: [compact_every * max_spikes] grown records (w = 1: used)
@@ -119,7 +130,8 @@ hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const i
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);
 // Structural update: stable compaction into `dst`, block b of kCompactChunk
 // records starting at offsets[b] (live counts from the k_apply tombstone tally).
-hipError_t launch_compact(const uint4* syn, uint64_t n, const uint64_t* offsets, uint4* dst, hipStream_t s);
+hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offsets, const SynArrays& dst,
+                          hipStream_t s);
 hipError_t launch_generate(const DeviceState& d, uint32_t n_in, uint32_t n_out, uint64_t seed,
                            hipStream_t s);
 hipError_t launch_checksum(const DeviceState& d, uint64_t* out_dev, hipStream_t s);

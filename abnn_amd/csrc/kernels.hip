@@ -101,17 +101,6 @@ __device__ __forceinline__ float updated_weight(const KernelParams& kp, float w,
     return clampf(w + dW, kp.w_min, kp.w_max);                      // brain.metal:121
 }
 
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-
-// Streaming 16-B load that should not displace the L2/MALL-resident neuron
-// state (bitmap, lastFired): non-temporal dwordx4.
-__device__ __forceinline__ uint4 load_stream16(const uint4* p)
-{
-    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -354,26 +343,27 @@ __device__ void build_tiles(const DeviceState& d, uint32_t* lds)
 
 // ---------------------------------------------------------------------------
 // k_gate: the streaming kernel (see file header).  Every wave owns one
-// contiguous range of events.  The pre-spike gate reads only the src word of
-// each 16-B record (the same lines stream from HBM; one register per event
-// instead of four), so a wave keeps K events per lane in flight in K VGPRs.
-// Loads use a wave-uniform base: the record buffer is padded by
-// kDummyRecords, so the sweep's last iteration reads past its end instead of
-// masking lanes, and the prefetch after a range's last iteration reads the
-// zero dummy block.  Pre-gated events (~0.2 % in steady state) are staged as
-// 4-B event offsets, kStageEntries per wave, so a wave usually flushes once,
-// at the end of its range (vmcnt retires in issue order, stores included: a
-// store between the prefetch and its wait delays the whole stream).
+// contiguous range of events.  The pre-spike gate needs only the src of each
+// record, and the records are held as arrays (SynArrays), so the sweep
+// streams 4 B per event: a wave keeps K events per lane in flight in K VGPRs,
+// each load one coalesced 256-B line segment.  Loads use a wave-uniform base:
+// the arrays are padded by kDummyRecords, so the sweep's last iteration reads
+// past its end instead of masking lanes, and the prefetch after a range's
+// last iteration reads the zero dummy block.  Pre-gated events (~0.2 % in
+// steady state) are staged as 4-B event offsets, kStageEntries per wave, so a
+// wave usually flushes once, at the end of its range (vmcnt retires in issue
+// order, stores included: a store between the prefetch and its wait delays
+// the whole stream).
 template <int BLOCK, int K, int FW, bool kTrack, bool kRandom>
 __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
     constexpr int NW = BLOCK / 64;
     constexpr uint32_t IE = 64 * K;
     constexpr uint32_t kFlushAt = kStageEntries - 64;  // one k-step adds at most 64
+    constexpr int KD = kTrack ? K : 1;                 // dst words in flight (track_visits)
     static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
     __shared__ uint32_t s_filter[FW];
     __shared__ uint32_t s_stage[NW][kStageEntries];
-    using Word = typename std::conditional<kTrack, u32x2_t, uint32_t>::type;  // {src[, dst]}
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wid = wave_uniform(tid >> 6);
@@ -390,23 +380,28 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         for (int i = tid; i < FW / 4; i += BLOCK) dst[i] = src[i];
     }
 
-    Word nxt[K];
+    uint32_t nxs[K], nxd[KD];
     const uint64_t pass = kRandom ? *d.pass_index : 0;
     auto issue = [&](uint64_t it, bool live) {
         if constexpr (kRandom) {  // random-edge mode: a per-lane random record per event
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const uint64_t t = it * IE + k * 64 + lane;
-                const uint4* p = (live && t < d.events)
-                                     ? d.syn + pick_record(d.seed, d.syn_offset, pass, t, d.n_syn)
-                                     : d.dummy + (k * 64 + lane);
-                nxt[k] = __builtin_nontemporal_load(reinterpret_cast<const Word*>(p));
+                const bool real = live && t < d.events;
+                const uint64_t e = real ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : 0;
+                nxs[k] = __builtin_nontemporal_load(real ? d.syn.src + e : d.dummy + (k * 64 + lane));
+                if constexpr (kTrack)
+                    nxd[k] = __builtin_nontemporal_load(real ? d.syn.dst + e : d.dummy + (k * 64 + lane));
             }
         } else {
-            const uint4* base = live ? d.syn + it * IE : d.dummy;  // wave-uniform
+            const uint32_t* bs = live ? d.syn.src + it * IE : d.dummy;  // wave-uniform
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                nxt[k] = __builtin_nontemporal_load(reinterpret_cast<const Word*>(base + k * 64 + lane));
+            for (int k = 0; k < K; ++k) nxs[k] = __builtin_nontemporal_load(bs + k * 64 + lane);
+            if constexpr (kTrack) {
+                const uint32_t* bd = live ? d.syn.dst + it * IE : d.dummy;
+#pragma unroll
+                for (int k = 0; k < K; ++k) nxd[k] = __builtin_nontemporal_load(bd + k * 64 + lane);
+            }
         }
     };
     issue(it_begin, it_begin < it_end);
@@ -422,17 +417,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     };
     for (uint64_t it = it_begin; it < it_end; ++it) {
         uint32_t src[K];
-        uint32_t dst[K];
+        uint32_t dst[KD];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if constexpr (kTrack) {
-                src[k] = nxt[k].x;
-                dst[k] = nxt[k].y;
-            } else {
-                src[k] = nxt[k];
-                dst[k] = 0;
-            }
-        }
+        for (int k = 0; k < K; ++k) src[k] = nxs[k];
+#pragma unroll
+        for (int k = 0; k < KD; ++k) dst[k] = kTrack ? nxd[k] : 0u;
         const uint64_t base = it * IE;
         uint32_t vmask = (K == 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);  // events of this lane that exist
         if (base + IE > d.events) {  // only the sweep's last iteration
@@ -520,16 +509,18 @@ __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
         bool valid = lane < td.z;
         const uint32_t rel = valid ? d.g1idx[region + td.y + lane] : 0u;
         // the gate kept only the event offset: dst and w come from the record
-        const uint4 rec = valid ? d.syn[rec_index(d, region + rel, pass)] : make_uint4(0u, 0u, 0u, 0u);
-        valid = valid && rec.y < nn;
-        const uint64_t ld = valid ? d.last_fired[rec.y] : 0ull;
+        const uint64_t ri = valid ? rec_index(d, region + rel, pass) : 0;
+        const uint32_t dst = valid ? d.syn.dst[ri] : 0u;
+        const float w = valid ? d.syn.w[ri] : 0.0f;
+        valid = valid && dst < nn;  // tombstones (dst = 0xFFFFFFFF) never pass
+        const uint64_t ld = valid ? d.last_fired[dst] : 0ull;
         const bool g2 = valid && (now - ld) > (uint64_t)kp.refractory;
         const uint64_t tg = d.syn_offset + region + rel;
-        const bool cand = g2 && spike_candidate(kp, __uint_as_float(rec.z), tg, now);
+        const bool cand = g2 && spike_candidate(kp, w, tg, now);
         const uint64_t bg = __ballot(g2), bc = __ballot(cand);
         if (g2 && tg == 0) d.work->t0_g2 = 1;
-        if (g2) d.g2e[(uint64_t)tile * kTile + lane] = make_uint4(rel, rec.y, rec.z, __float_as_uint((float)(now - ld)));
-        if (g2 && d.g2src) d.g2src[(uint64_t)tile * kTile + lane] = rec.x;  // synaptogenesis keeps src
+        if (g2) d.g2e[(uint64_t)tile * kTile + lane] = make_uint4(rel, dst, __float_as_uint(w), __float_as_uint((float)(now - ld)));
+        if (g2 && d.g2src) d.g2src[(uint64_t)tile * kTile + lane] = d.syn.src[ri];  // synaptogenesis keeps src
         if (lane == 0)
             d.tile_mask[tile] = make_uint4((uint32_t)bg, (uint32_t)(bg >> 32), (uint32_t)bc, (uint32_t)(bc >> 32));
     }
@@ -700,12 +691,13 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
         // middle of the next pass's record stream (+30 us of gate time,
         // tools/exp_variants.py).
         if (store && prune && w < kp.w_prune) {  // README §5: the synapse is removed
-            __builtin_nontemporal_store(u32x4_t{0xFFFFFFFFu, 0xFFFFFFFFu, __float_as_uint(w), 0u},
-                                        reinterpret_cast<u32x4_t*>(d.syn + ri));
+            __builtin_nontemporal_store(0xFFFFFFFFu, d.syn.src + ri);
+            __builtin_nontemporal_store(0xFFFFFFFFu, d.syn.dst + ri);
+            __builtin_nontemporal_store(w, d.syn.w + ri);
             if (d.dead) atomicAdd(d.dead + ri / kCompactChunk, 1u);  // tally for the structural update
             ++npr;
         } else if (store) {
-            __builtin_nontemporal_store(__float_as_uint(w), reinterpret_cast<uint32_t*>(d.syn + ri) + 2);
+            __builtin_nontemporal_store(w, d.syn.w + ri);
         }
         ++upd;
         if (f) {  // its stamp comes from the exchange record (k_finalize)
@@ -823,27 +815,33 @@ __global__ __launch_bounds__(256) void k_renorm(DeviceState d, uint64_t base)
 // moves records [b * kCompactChunk, (b + 1) * kCompactChunk) to dst from
 // offsets[b] on, in four coalesced rounds of kCompactThreads consecutive
 // records (one block scan of the live flags per round), streaming both ways.
-__global__ __launch_bounds__(kCompactThreads) void k_compact(const uint4* syn, uint64_t n, const uint64_t* offsets,
-                                                             uint4* dst)
+__global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint64_t n, const uint64_t* offsets,
+                                                             SynArrays dst)
 {
     static_assert(kCompactThreads == kScanThreads, "block_exclusive_scan is sized for kScanThreads");
     __shared__ uint64_t s_wave[kCompactThreads / 64];
     const uint64_t base = (uint64_t)blockIdx.x * kCompactChunk;
-    uint4 r[4];
+    uint32_t rs[4], rd[4];
+    float rw[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // all four loads in flight first
+    for (int j = 0; j < 4; ++j) {  // all loads in flight first
         const uint64_t i = base + (uint64_t)j * kCompactThreads + threadIdx.x;
-        r[j] = i < n ? load_stream16(syn + i) : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+        const bool in = i < n;
+        rs[j] = in ? __builtin_nontemporal_load(syn.src + i) : 0xFFFFFFFFu;
+        rd[j] = in ? __builtin_nontemporal_load(syn.dst + i) : 0u;
+        rw[j] = in ? __builtin_nontemporal_load(syn.w + i) : 0.0f;
     }
     uint64_t o = offsets[blockIdx.x];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const bool live = r[j].x != 0xFFFFFFFFu;
+        const bool live = rs[j] != 0xFFFFFFFFu;
         uint64_t tot;
         const uint64_t pre = block_exclusive_scan(live ? 1u : 0u, &tot, s_wave);
-        if (live)
-            __builtin_nontemporal_store(u32x4_t{r[j].x, r[j].y, r[j].z, r[j].w},
-                                        reinterpret_cast<u32x4_t*>(dst + o + pre));
+        if (live) {
+            __builtin_nontemporal_store(rs[j], dst.src + o + pre);
+            __builtin_nontemporal_store(rd[j], dst.dst + o + pre);
+            __builtin_nontemporal_store(rw[j], dst.w + o + pre);
+        }
         o += tot;
     }
 }
@@ -860,20 +858,22 @@ __global__ __launch_bounds__(256) void k_generate(DeviceState d, uint32_t n_in, 
     for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < d.n_syn; k += stride) {
         const uint64_t i = d.syn_offset + k;
         const uint64_t x2 = splitmix64_at(seed, 3u * i + 2u);
-        uint4 r;
+        uint32_t src, dst;
+        float w;
         if (i < n_io) {
-            r.x = (uint32_t)(i / n_out);
-            r.y = n_in + (uint32_t)(i % n_out);
-            r.z = __float_as_uint(0.4f + unit24(x2) * (0.8f - 0.4f));
+            src = (uint32_t)(i / n_out);
+            dst = n_in + (uint32_t)(i % n_out);
+            w = 0.4f + unit24(x2) * (0.8f - 0.4f);
         } else {
             const uint64_t x0 = splitmix64_at(seed, 3u * i + 0u);
             const uint64_t x1 = splitmix64_at(seed, 3u * i + 1u);
-            r.x = (uint32_t)(lo + (((x0 >> 32) * range) >> 32));
-            r.y = (uint32_t)(lo + (((x1 >> 32) * range) >> 32));
-            r.z = __float_as_uint(0.1f + unit24(x2) * (0.2f - 0.1f));
+            src = (uint32_t)(lo + (((x0 >> 32) * range) >> 32));
+            dst = (uint32_t)(lo + (((x1 >> 32) * range) >> 32));
+            w = 0.1f + unit24(x2) * (0.2f - 0.1f);
         }
-        r.w = 0u;
-        d.syn[k] = r;
+        d.syn.src[k] = src;
+        d.syn.dst[k] = dst;
+        d.syn.w[k] = w;
     }
 }
 
@@ -883,10 +883,9 @@ __global__ __launch_bounds__(256) void k_checksum(DeviceState d, uint64_t* out)
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     uint64_t acc = 0;
     for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < d.n_syn; k += stride) {
-        const uint4 r = d.syn[k];
         const uint64_t i = d.syn_offset + k;
-        const uint64_t a = ((uint64_t)r.x << 32) | r.y;
-        const uint64_t b = ((uint64_t)r.z << 32) | r.w;
+        const uint64_t a = ((uint64_t)d.syn.src[k] << 32) | d.syn.dst[k];
+        const uint64_t b = (uint64_t)__float_as_uint(d.syn.w[k]) << 32;  // pad = 0
         acc += mix64(a ^ mix64(b + i * 0x9E3779B97F4A7C15ull));
     }
     acc = wave_sum(acc);
@@ -946,7 +945,10 @@ int occupancy_shape(bool track, bool random)
     X(1024, 8, 8192)        \
     X(1024, 4, 8192)        \
     X(256, 16, 8192)        \
-    X(256, 8, 8192)
+    X(256, 8, 8192)         \
+    X(512, 32, 8192)        \
+    X(256, 32, 8192)        \
+    X(1024, 16, 8192)
 
 constexpr uint64_t shape_key(uint32_t b, uint32_t k, uint32_t fw) { return ((uint64_t)b << 40) | ((uint64_t)k << 32) | fw; }
 
@@ -1040,7 +1042,8 @@ hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_compact(const uint4* syn, uint64_t n, const uint64_t* offsets, uint4* dst, hipStream_t s)
+hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offsets, const SynArrays& dst,
+                          hipStream_t s)
 {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_compact, dim3((uint32_t)((n + kCompactChunk - 1) / kCompactChunk)),

@@ -2,8 +2,9 @@
 """Benchmark: traversal events/s of the C1 synapse sweep on MI355X.
 
 Workload (BASELINE.json configs[2], constants.h defaults): N_NRN = 5,000,512
-(256 in + 256 out + 5M hidden), N_SYN = 1e9 (16 GB of 16-B SynapsePacked in
-HBM), EVENTS_PER_PASS = 150M (150,000,128 visits per pass).  Synthetic graph =
+(256 in + 256 out + 5M hidden), N_SYN = 1e9 (12 GB of src/dst/w arrays in
+HBM; SynapsePacked's never-read pad is not stored), EVENTS_PER_PASS = 150M
+(150,000,128 visits per pass).  Synthetic graph =
 the build_random_graph recipe (brain-engine.cpp:31-53) with the portable RNG,
 generated on the GPU; every pass stamps all 256 inputs.
 
@@ -59,12 +60,13 @@ PLASTICITY = dict(w_prune=0.105, p_new=0.25, w_init=0.5, compact_every=50)
 
 def algorithmic_bytes(stats: dict, track_visits: bool) -> int:
     """Bytes the streaming gate kernel must move from HBM: the
-    16-B SynapsePacked record of every visited event (+8 B lastVisited write per
-    event with track_visits).  The pre-spike lookup of lastFired[src] is served
-    by the per-pass 64 KiB LDS filter / L2 bitmap built by k_bitmap, which reads
-    lastFired once per pass (8 B per neuron, k_bitmap's own bytes)."""
+    4-B src word of every visited event -- the records are held as arrays and
+    the pre-spike gate reads nothing else (+4 B dst read and 8 B lastVisited
+    write per event with track_visits).  The pre-spike lookup of lastFired[src]
+    is served by the per-pass LDS filter / L2 bitmap built by k_bitmap, which
+    reads lastFired once per pass (8 B per neuron, k_bitmap's own bytes)."""
     e = stats["events"]
-    return 16 * e + (8 * e if track_visits else 0)
+    return 4 * e + (12 * e if track_visits else 0)
 
 
 def survey_bytes(stats: dict, track_visits: bool) -> int:
@@ -207,8 +209,8 @@ def main():
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
             "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4),
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "bytes_formula": ("16*E (SynapsePacked stream; E visited events) -- DESIGN.md §5" if mode == 0 else
-                              "16*E (one random SynapsePacked record per pick; HBM moves >= 64 B per "
+            "bytes_formula": ("4*E (src-array stream; E visited events) -- DESIGN.md §5" if mode == 0 else
+                              "4*E (one random src word per pick; HBM moves >= 64 B per "
                               "random access) -- DESIGN.md §5"),
             "survey_formula_bytes_per_launch": int(survey_per_launch),
             "survey_formula_achieved": round(survey_per_launch / (avg_gate_ms * 1e-3) / 1e9, 1),

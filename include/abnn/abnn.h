@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ABNN_ABI_VERSION 3
+#define ABNN_ABI_VERSION 4
 
 typedef enum abnn_status {
     ABNN_OK = 0,
@@ -51,7 +51,12 @@ typedef enum abnn_status {
     ABNN_ERR_NO_DEVICE = 6       /* no HIP device / bad ordinal                   */
 } abnn_status;
 
-/* SynapsePacked -- brain.metal:11, brain.h:21, README §2.2.  16 bytes, AoS. */
+/* SynapsePacked -- brain.metal:11, brain.h:21, README §2.2.  16 bytes, AoS.
+ * This is the INTERCHANGE format (upload/download, .bnn, the C++ wrapper).
+ * On the device the records are held as three arrays (abnn_state, DESIGN.md
+ * §4): the sweep's gate needs only `src`, so it streams 4 B per event instead
+ * of 16.  `pad` is not stored; downloads return 0 (the reference never writes
+ * or reads it: brain.metal:11, brain-engine.cpp:31-53). */
 typedef struct abnn_synapse {
     uint32_t src;
     uint32_t dst;
@@ -173,9 +178,12 @@ typedef struct abnn_stats {
     uint64_t grown;          /* synapses appended by structural updates          */
 } abnn_stats;
 
-/* Borrowed device pointers (brain.h:54-58 buffer getters). */
+/* Borrowed device pointers (brain.h:54-58 buffer getters).  bufSyn_ is held
+ * as a structure of arrays: record i is {syn_src[i], syn_dst[i], syn_w[i], 0}. */
 typedef struct abnn_state {
-    abnn_synapse* synapses;  /* n_syn records (bufSyn_)                  */
+    uint32_t* syn_src;       /* n_syn (bufSyn_ .src)                     */
+    uint32_t* syn_dst;       /* n_syn (bufSyn_ .dst)                     */
+    float* syn_w;            /* n_syn (bufSyn_ .w)                       */
     uint64_t* last_fired;    /* N_NRN (bufLastFire_)                     */
     uint64_t* last_visited;  /* N_NRN (bufLastVisit_)                    */
     uint64_t* clock;         /* 1 (bufClock_)                            */
