@@ -79,7 +79,7 @@ def main():
             "fetch_bytes_corrected": f_kib * 1024 * 2,
             "write_bytes": w_kib * 1024,
             "bytes_per_launch": f_kib * 1024 * 2 + w_kib * 1024,
-            "correction": "FETCH_SIZE x2 (gfx950 wide-stream undercount), KiB -> bytes",
+            "correction": "FETCH_SIZE x2 (gfx950 stream undercount; calibrated for 4-B nt streams in profiles/r01l_fetch_calibration_dword.txt), KiB -> bytes",
             "launches_used": min(len(fetch), len(write)),
         })
         lines.append(f"k_gate PMC per launch: FETCH_SIZE {f_kib:.0f} KiB (x2 -> {f_kib*2048/1e9:.3f} GB), "
