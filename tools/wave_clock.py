@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of the gate kernel (diagnostics, ABNN_WAVE_CLOCK).
+
+Runs config 3 for `warm` passes, then reads the last pass's per-wave clocks
+{start, stream done, end} (100 MHz s_memrealtime) and prints the spread of
+start, stream-end and end times, the tail (refractory stage) durations and the
+latest waves.  usage: ABNN_WAVE_CLOCK=1 python tools/wave_clock.py [passes]
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("ABNN_WAVE_CLOCK", "1")
+from abnn_amd import CONFIGS, Brain  # noqa: E402
+
+wl = CONFIGS[os.environ.get("CFG", "c3")]
+b = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, device=0)
+b.build_random_graph(1)
+b.set_auto_stimulus(0, wl.n_input)
+passes = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+for p in range(passes):
+    b.encode_traversal(1)
+    b.synchronize()
+    nr = 16384
+    buf = np.zeros(4 * nr, dtype=np.uint64)
+    f = b._lib.abnn_debug_wave_clock
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    f.restype = ctypes.c_int
+    assert f(b._h, buf.ctypes.data, buf.size) == 0
+    w = buf.reshape(-1, 4)
+    w = w[w[:, 0] > 0]
+    t0 = w[:, 0].min()
+    st, se, en = (w[:, 0] - t0) * 10e-3, (w[:, 1] - t0) * 10e-3, (w[:, 2] - t0) * 10e-3  # us
+    q = lambda x: " ".join(f"{v:7.1f}" for v in np.percentile(x, [0, 10, 50, 90, 99, 100]))
+    print(f"pass {p}: waves {len(w)}   percentiles 0/10/50/90/99/100 (us)")
+    print(f"  start       {q(st)}")
+    print(f"  stream end  {q(se)}")
+    print(f"  end         {q(en)}")
+    print(f"  stream dur  {q(se - st)}")
+    print(f"  tail dur    {q(en - se)}")
+    np.save(os.path.join(os.environ.get("OUT", "gpurun_out"), f"wave_clock_p{p}.npy"), buf.reshape(-1, 4)[:len(w)])
+    late = np.argsort(en)[-6:]
+    print("  latest waves (range: start/stream-end/end us):",
+          "  ".join(f"{i}:{st[i]:.1f}/{se[i]:.1f}/{en[i]:.1f}" for i in late))
