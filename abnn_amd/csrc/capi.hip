@@ -97,12 +97,12 @@ void free_all(abnn_brain* b)
     void* ptrs[] = {b->d.syn.src,   b->d.syn.dst,    b->d.syn.w,
                     b->syn_alt.src, b->syn_alt.dst,  b->syn_alt.w,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
-                    b->d.bitmap,    b->d.filter,     b->d.range_cnt,     b->d.tile_desc,
-                    b->d.tile_mask, b->d.tile_pre,   b->d.g1idx,    b->d.g2e,         b->d.apply_partial,
-                    b->d.claim,     b->d.g2src,      b->d.grown,
+                    b->d.bitmap,    b->d.filter,     b->d.range_info,    b->d.g2x,
+                    b->d.g1idx,     b->d.chunk_cnt,  b->d.ovf,
+                    b->d.apply_partial, b->d.claim,  b->d.g2src,      b->d.grown,
                     b->d.dead,      b->compact_offsets,
-                    b->d.xchg,      b->d.work,          b->idx_scratch,
-                    b->u64_scratch,  const_cast<uint32_t*>(b->d.dummy)};
+                    b->d.work,      b->idx_scratch,
+                    b->u64_scratch,  b->d.wave_clock,  const_cast<uint32_t*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : b->events) {
@@ -312,8 +312,9 @@ abnn_status structural_update(abnn_brain* b)
     return ABNN_OK;
 }
 
-// bitmap + streaming gate + chunk scan: the first half of every pass.
-abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, bool sharded, hipStream_t s)
+// bitmap + streaming gate (with the refractory stage) [+ the exchange record
+// of a sharded pass]: the first half of every pass.
+abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
 {
     HIP_TRY(launch_bitmap(b->d, b->kp, b->stim_first, b->stim_count, s));
     EventPair* ev = nullptr;
@@ -321,7 +322,7 @@ abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, bool sharded, hipStream_t
     HIP_TRY(launch_gate(b->d, b->kp, s));
     if (ev) HIP_TRY(hipEventRecord(ev->b, s));
     HIP_TRY(launch_refrac(b->d, b->kp, s));
-    HIP_TRY(launch_scan(b->d, b->kp, xchg_out, sharded, s));
+    if (xchg_out) HIP_TRY(launch_scan(b->d, b->kp, xchg_out, s));
     return ABNN_OK;
 }
 
@@ -433,7 +434,6 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     const uint64_t iter_events = 64ull * gate_k;  // one wave iteration
     const uint64_t iters = (E + iter_events - 1) / iter_events;
     REQUIRE(iters < 0x7FFFFFFFull, "too many events for one handle");
-    REQUIRE(E / kTile + (uint64_t)kMaxRanges < 0xFFFFFFFFull, "too many events for one handle");
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -500,17 +500,17 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.pass_index = sb + 2;
     if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.filter, kMaxFilterWords)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.range_cnt, max_ranges)) != ABNN_OK) return fail(s);
-    const uint64_t max_tiles = E / kTile + max_ranges + 1;
-    if ((s = dalloc(&d.tile_mask, max_tiles)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.tile_desc, max_tiles)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.tile_pre, max_tiles)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.range_info, max_ranges)) != ABNN_OK) return fail(s);
+    // per-range regions of refractory survivors (16 B per event: every event of
+    // a range may pass in the warm-up passes)
+    if ((s = dalloc(&d.g2x, iters * iter_events)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.g1idx, iters * iter_events)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.g2e, max_tiles * kTile)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.chunk_cnt, iters * iter_events / kChunkSlotDiv + 8)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.ovf, iters * iter_events / kChunk + max_ranges)) != ABNN_OK) return fail(s);
     uint32_t* dummy = nullptr;
     if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
     d.dummy = dummy;
-    if ((s = dalloc(&d.apply_partial, kTileBlocks)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.apply_partial, kMaxApplyBlocks)) != ABNN_OK) return fail(s);
     if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, cap)) != ABNN_OK) return fail(s);
     if (p.compact_every > 0) {  // structural updates: the compaction's second buffer + scratch
         const uint64_t nb = (cap + kCompactChunk - 1) / kCompactChunk;
@@ -519,12 +519,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
         if (p.w_prune > 0.0f && (s = dalloc(&d.dead, nb)) != ABNN_OK) return fail(s);
     }
     if (genesis) {
-        if ((s = dalloc(&d.g2src, max_tiles * kTile)) != ABNN_OK) return fail(s);
+        if ((s = dalloc(&d.g2src, iters * iter_events)) != ABNN_OK) return fail(s);
         if ((s = dalloc(&d.grown, (uint64_t)p.compact_every * p.max_spikes)) != ABNN_OK) return fail(s);
     }
-    if ((s = dalloc(&d.xchg, xchg_words(p.max_spikes))) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
+    if (std::getenv("ABNN_WAVE_CLOCK") && (s = dalloc(&d.wave_clock, 4 * max_ranges)) != ABNN_OK) return fail(s);
     *out = b;
     return ABNN_OK;
 }
@@ -755,9 +755,9 @@ abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream)
     for (uint32_t i = 0; i < passes; ++i) {
         // the host reads the clock at encode time, before the pass (brain.cpp:127-128)
         const bool renorm = b->clock_host > b->params.renorm_thresh;
-        ST_TRY(run_gate(b, b->d.xchg, false, s));
-        HIP_TRY(launch_apply(b->d, b->kp, b->d.xchg, 1, 0, b->d.xchg + 2 * ABNN_SUMMARY_WORDS, s));
-        ST_TRY(run_commit(b, b->d.xchg, 1, renorm, s));
+        ST_TRY(run_gate(b, nullptr, s));
+        HIP_TRY(launch_apply(b->d, b->kp, nullptr, 0, s));
+        ST_TRY(run_commit(b, nullptr, 1, renorm, s));
     }
     return ABNN_OK;
 }
@@ -782,7 +782,7 @@ abnn_status abnn_shard_gate(abnn_brain* b, void* xchg_dev, void* stream)
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
     b->pending_renorm = b->clock_host > b->params.renorm_thresh;
-    return run_gate(b, static_cast<int32_t*>(xchg_dev), true, s);
+    return run_gate(b, static_cast<int32_t*>(xchg_dev), s);
 }
 
 abnn_status abnn_shard_apply(abnn_brain* b, const void* gathered_dev, uint32_t world, uint32_t rank,
@@ -792,8 +792,7 @@ abnn_status abnn_shard_apply(abnn_brain* b, const void* gathered_dev, uint32_t w
     REQUIRE(world >= 1 && rank < world, "bad world/rank");
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
-    HIP_TRY(launch_apply(b->d, b->kp, static_cast<const int32_t*>(gathered_dev), world, rank,
-                         nullptr, s));
+    HIP_TRY(launch_apply(b->d, b->kp, static_cast<const int32_t*>(gathered_dev), rank, s));
     return ABNN_OK;
 }
 
@@ -806,6 +805,16 @@ abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t 
     const bool renorm = b->pending_renorm;
     b->pending_renorm = false;
     return run_commit(b, static_cast<const int32_t*>(gathered_dev), world, renorm, s);
+}
+
+// Diagnostics (not part of abnn.h): the last pass's per-wave gate times
+// {start, stream done, end, hw id} in 100 MHz ticks; needs ABNN_WAVE_CLOCK at create.
+abnn_status abnn_debug_wave_clock(abnn_brain* b, uint64_t* out, uint64_t n)
+{
+    REQUIRE(b && out && b->d.wave_clock, "wave clock not enabled");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(out, b->d.wave_clock, std::min<uint64_t>(n, 4ull * b->d.n_ranges) * 8, hipMemcpyDeviceToHost));
+    return ABNN_OK;
 }
 
 abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out)

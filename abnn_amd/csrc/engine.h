@@ -14,22 +14,24 @@ namespace abnn {
 // bitmap folded modulo filter_words 32-bit words (16384 words = 512 Ki bits =
 // 32 KiB by default).  When the bitmap itself fits, the filter IS the bitmap.
 constexpr int kMaxFilterWords = 16384;
-constexpr int kTile = 64;          // one tile = 64 consecutive pre-gated events of a range = one wave
-constexpr int kTileBlocks = 2048;  // grid of the tile kernels (x 4 waves = 8192 waves, all resident)
-constexpr int kScanThreads = 1024; // the range and tile scans are one workgroup each
+constexpr int kScanThreads = 1024; // k_scan and k_finalize are one workgroup each
 constexpr int kMaxGateBlocks = 1024;
-constexpr int kMaxRanges = 16384;  // kMaxGateBlocks x up to 16 waves; k_tiles holds them in registers
-static_assert(kTileBlocks % kScanThreads == 0, "k_finalize sums the apply partials in whole rounds");
+constexpr int kMaxRanges = 16384;  // kMaxGateBlocks x up to 16 waves (one range per gate wave)
+constexpr int kApplyThreads = 1024;  // budget-walk workgroups (k_spikes, k_claim, k_apply)
+constexpr uint32_t kWalkBlocks = 256; // their grid: 4096 waves, one work item (chunk) per wave at a time
+constexpr int kMaxApplyBlocks = kWalkBlocks;
+static_assert(kMaxApplyBlocks <= kScanThreads, "k_finalize reads one apply partial per thread");
+static_assert(kMaxRanges % kApplyThreads == 0, "range prefix: whole ranges per thread");
 constexpr int kDummyRecords = 64 * 32;  // >= 64 lanes x max events per lane; also the record-buffer padding
-constexpr int kStageEntries = 448;      // per gate wave: 4-B event offsets staged in LDS
+constexpr uint32_t kChunk = 384;        // pre-gated events per chunk (staged in LDS by a gate wave)
+constexpr uint32_t kChunkSlotDiv = 128; // chunk_cnt index = (region + c * kChunk) / 128 (unique per chunk)
+constexpr int kRefracBlocks = 512;      // k_refrac grid (x 4 waves; one queued chunk per wave at a time)
 
 // Per-pass bookkeeping in device memory (one per handle).
 struct alignas(16) PassWork {
-    uint32_t total_tiles;  // tiles of pre-gated entries this pass
-    uint32_t t0_g2;        // global event 0 passed both gates this pass
-    uint64_t events;       // visited events of this shard this pass
-    uint64_t g1;           // passed the pre-gate
-    uint64_t g2;           // passed the refractory gate
+    uint32_t t0_g2;        // global event 0 passed both gates this pass (re-armed by k_finalize)
+    uint32_t n_ovf;        // full chunks queued for k_refrac this pass (re-armed by k_finalize)
+    uint32_t pad[2];
     abnn_stats stats;      // cumulative (finalize adds)
 };
 
@@ -55,20 +57,19 @@ struct DeviceState {
     float* rbar;              // [1]
     uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
     uint32_t* filter;         // [filter_words] folded bitmap
-    uint32_t* range_cnt;      // [n_ranges] pre-gated entries of each range
-    uint4* tile_desc;         // [max_tiles] {range, first entry in the range, entries, 0}
-    uint4* tile_mask;         // [max_tiles] {passed refractory, spike candidate} lane masks (2 x u64)
-    uint32_t* tile_pre;       // [max_tiles] exclusive candidate prefix (capped; = budget: skip)
-    uint32_t* g1idx;          // [iters * iter_events] pre-gated event offsets (event - region), per-range regions
-    uint4* g2e;               // [max_tiles * kTile] {event - region, dst, w, isi} of the events that passed
+    uint4* range_info;        // [n_ranges] {pre-gated, passed refractory, candidates, chunks} per gate wave
+    uint32_t* g1idx;          // [iters * iter_events] per-range regions: offsets of full chunks (k_refrac input)
+    uint4* g2x;               // [iters * iter_events] per-range regions: {event - region, isi | cand << 31, w, dst}
+    uint2* chunk_cnt;         // [iters * iter_events / kChunkSlotDiv + 8] {survivors, candidates} per chunk
+    uint2* ovf;               // [iters * iter_events / kChunk + n_ranges] queued full chunks {range, chunk}
     const uint32_t* dummy;    // [kDummyRecords] zeros: target of the stream loads past a range
-    uint4* apply_partial;     // [kTileBlocks] {updated, fired, pruned, 0} per apply workgroup
-    uint32_t* g2src;          // genesis on: [max tiles * kTile] src of the visited record
+    uint4* apply_partial;     // [kMaxApplyBlocks] {updated, fired, pruned, 0} per apply workgroup
+    uint32_t* g2src;          // genesis on: [iters * iter_events] src of the g2x entry's record
     uint4* grown;             // genesis on: [compact_every * max_spikes] grown records (w = 1: used)
     uint32_t* dead;           // pruning on: tombstones per kCompactChunk records (structural update)
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
-    int32_t* xchg;            // internal exchange record (world = 1): summary + spike list
     PassWork* work;
+    uint64_t* wave_clock;     // diagnostics only (ABNN_WAVE_CLOCK): [4 * n_ranges] per-wave gate times
     uint64_t n_syn;           // local records
     uint64_t n_nrn;
     uint32_t n_input;
@@ -118,13 +119,11 @@ hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t 
                          uint64_t stim_count, hipStream_t s);
 hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s);
 hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream_t s);
-// launch_scan writes the exchange record's summary; with `spike_list` also its
-// spike list (sharded passes).  launch_apply writes the list into `spikes`
-// when non-null (the single-GPU pass, where it is the only rank).
-hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out,
-                       bool spike_list, hipStream_t s);
+// Sharded passes: this shard's exchange record (summary + local spike list).
+hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out, hipStream_t s);
+// gathered == nullptr: single-GPU pass (no exchange; k_apply stamps the spikes).
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
-                        uint32_t world, uint32_t rank, int32_t* spikes, hipStream_t s);
+                        uint32_t rank, hipStream_t s);
 hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
                            uint32_t world, hipStream_t s);
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);

@@ -33,6 +33,7 @@
 //
 // All fp32 arithmetic is compiled with -ffp-contract=off and written operation
 // for operation like the oracle, so weights are bit-identical to the CPU.
+#include <algorithm>
 #include <type_traits>
 
 #include "engine.h"
@@ -239,106 +240,81 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
 }
 
 // ---------------------------------------------------------------------------
-// Pre-gated entries are processed as tiles of kTile (= 64 = one wave)
-// consecutive entries of one range; tile order = event order;
-// tile_desc[t] = {range, first entry of the tile in its range, entries, 0}.
-// These steps move a few MB per pass: they are bound by dependent-load
-// latency, so every loop below keeps all of a thread's loads in flight at
-// once, scans run on DPP over coalesced chunks, and no tile waits on another.
+// Per-range results of the gate.  A range is the contiguous block of events
+// one gate wave sweeps; range order = event order.  The pre-gated events of a
+// range are cut, in event order, into chunks of kChunk: chunk c occupies
+// [region + c kChunk, region + (c + 1) kChunk) of the range's region in g1idx
+// (offsets, full chunks only) and g2x (refractory survivors, compacted to the
+// chunk's start).  g2x entry = {event - region, isi bits | candidate << 31,
+// w bits, dst}, with isi = (float)(now - lastFired[dst]) >= 0 (its sign bit is
+// free) and w, dst as read at pass start (C1).  chunk_cnt[chunk_slot] =
+// {survivors, candidates} of a full chunk (slots of full chunks never
+// collide; the last chunk's survivors are the range's total minus theirs);
+// range_info[r] = {pre-gated, survivors, candidates, full chunks}.  The last (partial) chunk of a range is processed by its gate wave
+// at the end of its range; full chunks (dense parts of the graph, warm-up
+// passes) are queued for k_refrac so that no wave's stream waits on them.
 
-// Inclusive wave scan on DPP (row_shr within 16-lane rows, then the gfx9
-// row broadcasts): six VALU ops, no LDS crossbar round trips.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+__device__ __forceinline__ uint64_t region_of(const DeviceState& d, uint32_t r)
 {
-    int v = (int)x;
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-    return (uint32_t)v;
+    return range_begin(r, d.iters, d.n_ranges) * d.iter_events;
 }
 
-__device__ __forceinline__ uint32_t lane63(uint32_t x)
+__device__ __forceinline__ uint64_t chunk_slot(uint64_t region, uint32_t c)
 {
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    return (region + (uint64_t)c * kChunk) / kChunkSlotDiv;
 }
 
-__device__ __forceinline__ uint32_t tiles_of(uint32_t n) { return (n + kTile - 1) / kTile; }
-
-// Tile descriptors and the pre-gated total, by one workgroup of NT threads.
-// Wave w owns a contiguous block of ranges read as
-// coalesced 64-range chunks (at most 16 with NT = kScanThreads); the chunk scans are recomputed in the second sweep
-// rather than kept.  `lds` is scratch of >= 64 + 3 * kBig words.
-template <int NT>
-__device__ void build_tiles(const DeviceState& d, uint32_t* lds)
+// Refractory stage (brain.metal:79-83, 91-92, 116) of n <= kChunk pre-gated
+// offsets of one chunk, by one wave, in event order: dst and w gathered from
+// the record arrays, the 8-B lastFired[dst] gather, the candidate test; the
+// survivors are written compacted from g2x[base] on.  `rel_at(q)` yields the
+// q-th offset.  Batches of R rounds of 64 keep every load of a lane in flight
+// at once.  Returns {survivors, candidates}.
+template <int R, bool kRandom, class RelAt>
+__device__ __forceinline__ uint2 refrac_chunk(const DeviceState& d, const KernelParams& kp, uint64_t region,
+                                              uint64_t base, uint32_t n, uint64_t now, uint64_t pass,
+                                              RelAt&& rel_at)
 {
-    constexpr uint32_t NWv = NT / 64, kCh = kMaxRanges / NT, kBig = 256;
-    uint32_t* s_wt = lds;                                       // [NWv] tiles per wave
-    uint64_t* s_wg1 = reinterpret_cast<uint64_t*>(lds + 16);    // [NWv] entries per wave
-    uint32_t* s_nbig = lds + 48;
-    uint32_t* s_big = lds + 64;                                 // {range, first tile, entries} x kBig
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = wave_uniform(tid >> 6), NR = d.n_ranges;
-    const uint32_t per = ((NR + NWv - 1) / NWv + 63) & ~63u, nch = per / 64;
-    if (tid == 0) *s_nbig = 0;
-    uint32_t cnt[kCh];
+    const uint32_t lane = threadIdx.x & 63, nn = (uint32_t)d.n_nrn;
+    uint32_t n_g2 = 0, n_cand = 0;
+    auto record_of = [&](uint32_t rel) -> uint64_t {
+        const uint64_t t = region + rel;
+        return kRandom ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : t;
+    };
+    for (uint32_t b0 = 0; b0 < n; b0 += R * 64) {
+        uint32_t rel[R], dst[R];
+        float w[R];
+        uint64_t ld[R];
 #pragma unroll
-    for (uint32_t c = 0; c < kCh; ++c) {
-        const uint32_t r = w * per + c * 64 + lane;
-        cnt[c] = (c < nch && r < NR) ? d.range_cnt[r] : 0u;
-    }
-    uint32_t run = 0;
-    uint64_t g1 = 0;
-#pragma unroll
-    for (uint32_t c = 0; c < kCh; ++c) {
-        run += lane63(wave_incl_scan(tiles_of(cnt[c])));
-        g1 += cnt[c];
-    }
-    g1 = wave_sum(g1);
-    if (lane == 0) {
-        s_wt[w] = run;
-        s_wg1[w] = g1;
-    }
-    __syncthreads();
-    uint32_t off = 0, total = 0;
-#pragma unroll
-    for (uint32_t v = 0; v < NWv; ++v) {
-        off += v < w ? s_wt[v] : 0u;
-        total += s_wt[v];
-    }
-    run = 0;
-#pragma unroll
-    for (uint32_t c = 0; c < kCh; ++c) {
-        const uint32_t r = w * per + c * 64 + lane;
-        const uint32_t n = cnt[c], nt = tiles_of(n), x = wave_incl_scan(nt);
-        const uint32_t t0 = off + run + x - nt;
-        run += lane63(x);
-        uint32_t q = 0;
-        if (nt > 4) {  // long ranges (the dense input block) are filled cooperatively
-            const uint32_t slot = atomicAdd(s_nbig, 1u);
-            if (slot < kBig) {
-                s_big[3 * slot] = r;
-                s_big[3 * slot + 1] = t0;
-                s_big[3 * slot + 2] = n;
-                q = nt;
-            }
+        for (int j = 0; j < R; ++j) {
+            const uint32_t q = b0 + j * 64 + lane;
+            const bool v = q < n;
+            rel[j] = v ? rel_at(q) : 0u;
+            const uint64_t ri = v ? record_of(rel[j]) : 0;
+            dst[j] = v ? d.syn.dst[ri] : 0xFFFFFFFFu;  // tombstones (dst = 0xFFFFFFFF) never pass
+            w[j] = v ? d.syn.w[ri] : 0.0f;
         }
-        for (; q < nt; ++q) d.tile_desc[t0 + q] = make_uint4(r, q * kTile, min(n - q * kTile, (uint32_t)kTile), 0u);
+#pragma unroll
+        for (int j = 0; j < R; ++j) ld[j] = dst[j] < nn ? d.last_fired[dst[j]] : 0ull;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            if (b0 + (uint32_t)j * 64 >= n) break;  // wave-uniform
+            const bool g2 = dst[j] < nn && (now - ld[j]) > (uint64_t)kp.refractory;  // brain.metal:79-83
+            const uint64_t tg = d.syn_offset + region + rel[j];
+            const bool cand = g2 && spike_candidate(kp, w[j], tg, now);
+            const uint64_t bg = __ballot(g2);
+            if (g2) {
+                const uint64_t o = base + n_g2 + mbcnt64(bg);
+                const uint32_t isi = __float_as_uint((float)(now - ld[j])) | (cand ? 0x80000000u : 0u);
+                d.g2x[o] = make_uint4(rel[j], isi, __float_as_uint(w[j]), dst[j]);
+                if (d.g2src) d.g2src[o] = d.syn.src[record_of(rel[j])];  // synaptogenesis keeps src
+                if (tg == 0) d.work->t0_g2 = 1u;
+            }
+            n_g2 += (uint32_t)__popcll(bg);
+            n_cand += (uint32_t)__popcll(__ballot(cand));
+        }
     }
-    __syncthreads();
-    const uint32_t nbig = min(*s_nbig, kBig);
-    for (uint32_t b = 0; b < nbig; ++b) {
-        const uint32_t r = s_big[3 * b], t0 = s_big[3 * b + 1], n = s_big[3 * b + 2], nt = tiles_of(n);
-        for (uint32_t q = tid; q < nt; q += NT)
-            d.tile_desc[t0 + q] = make_uint4(r, q * kTile, min(n - q * kTile, (uint32_t)kTile), 0u);
-    }
-    if (tid == 0) {
-        uint64_t tg1 = 0;
-        for (uint32_t v = 0; v < NWv; ++v) tg1 += s_wg1[v];
-        d.work->total_tiles = total;
-        d.work->g1 = tg1;
-    }
+    return make_uint2(n_g2, n_cand);
 }
 
 // ---------------------------------------------------------------------------
@@ -350,20 +326,20 @@ __device__ void build_tiles(const DeviceState& d, uint32_t* lds)
 // the arrays are padded by kDummyRecords, so the sweep's last iteration reads
 // past its end instead of masking lanes, and the prefetch after a range's
 // last iteration reads the zero dummy block.  Pre-gated events (~0.2 % in
-// steady state) are staged as 4-B event offsets, kStageEntries per wave, so a
-// wave usually flushes once, at the end of its range (vmcnt retires in issue
-// order, stores included: a store between the prefetch and its wait delays
-// the whole stream).
+// steady state) are staged in LDS as 4-B event offsets; a full chunk goes to
+// g1idx and onto the k_refrac queue, and the range's last chunk is run
+// through the refractory stage by the wave itself once its stream is done.
+// (vmcnt retires in issue order, stores included: a store between the
+// prefetch and its wait delays the whole stream, so chunks are rare.)
 template <int BLOCK, int K, int FW, bool kTrack, bool kRandom>
-__global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
+__global__ __launch_bounds__(BLOCK, 4) void k_gate(DeviceState d, KernelParams kp)  // >= 4 waves per SIMD: <= 128 VGPRs
 {
     constexpr int NW = BLOCK / 64;
     constexpr uint32_t IE = 64 * K;
-    constexpr uint32_t kFlushAt = kStageEntries - 64;  // one k-step adds at most 64
     constexpr int KD = kTrack ? K : 1;                 // dst words in flight (track_visits)
     static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
     __shared__ uint32_t s_filter[FW];
-    __shared__ uint32_t s_stage[NW][kStageEntries];
+    __shared__ uint32_t s_stage[NW][kChunk + 64];      // a chunk + one k-step
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wid = wave_uniform(tid >> 6);
@@ -404,16 +380,29 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             }
         }
     };
+    const uint64_t t_start = d.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0;
     issue(it_begin, it_begin < it_end);
     __syncthreads();
 
     const uint32_t nn = (uint32_t)d.n_nrn;  // N_NRN < 2^32 (checked at create)
-    uint32_t pend = 0, flushed = 0;
-    auto flush = [&]() {  // wave-uniform: write the staged offsets, in order
-        for (uint32_t q = lane; q < pend; q += 64)
-            __builtin_nontemporal_store(stage[q], d.g1idx + region + flushed + q);
-        flushed += pend;
-        pend = 0;
+    uint32_t pend = 0, nch = 0, oslot = 0;
+    // wave-uniform: a full chunk of staged offsets to g1idx and the k_refrac
+    // queue; the (< 64) entries past it move to the front of the stage
+    auto chunk_out = [&]() {
+        const uint64_t base = region + (uint64_t)nch * kChunk;
+#pragma unroll
+        for (uint32_t q = 0; q < kChunk; q += 64) __builtin_nontemporal_store(stage[q + lane], d.g1idx + base + q + lane);
+        const uint32_t rest = pend - kChunk;
+        const uint32_t x = lane < rest ? stage[kChunk + lane] : 0u;
+        if (lane < rest) stage[lane] = x;
+        // queue slot: claimed now, written at the next chunk or the range's
+        // end, so the stream never waits on the atomic's return
+        if (lane == 0) {
+            if (nch > 0) d.ovf[oslot] = make_uint2(r, nch - 1);
+            oslot = atomicAdd(&d.work->n_ovf, 1u);
+        }
+        ++nch;
+        pend = rest;
     };
     for (uint64_t it = it_begin; it < it_end; ++it) {
         uint32_t src[K];
@@ -474,213 +463,233 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             const uint64_t b1 = __ballot(g1);
             if (g1) stage[pend + mbcnt64(b1)] = rel + k * 64 + lane;
             pend += (uint32_t)__popcll(b1);
-            if (pend >= kFlushAt) flush();
+            if (pend >= kChunk) chunk_out();  // a k-step stages at most 64
         }
     }
-    flush();
-    if (lane == 0) d.range_cnt[r] = flushed;
+    const uint64_t t_stream = d.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0;
+    // the range's last chunk: refractory stage by this wave
+    const uint64_t tb = region + (uint64_t)nch * kChunk;
+    const uint2 c = refrac_chunk<4, kRandom>(d, kp, region, tb, pend, now, pass,
+                                             [&](uint32_t q) { return stage[q]; });
+    if (lane == 0) {
+        if (nch > 0) d.ovf[oslot] = make_uint2(r, nch - 1);
+        d.range_info[r] = make_uint4(nch * kChunk + pend, c.x, c.y, nch);
+        if (d.wave_clock) {  // diagnostics (ABNN_WAVE_CLOCK): 100 MHz wall clock per wave
+            d.wave_clock[4 * r] = t_start;
+            d.wave_clock[4 * r + 1] = t_stream;
+            d.wave_clock[4 * r + 2] = __builtin_amdgcn_s_memrealtime();
+            d.wave_clock[4 * r + 3] = __smid();
+        }
+    }
 }
 
-// k_tiles: one workgroup builds the tile descriptors (build_tiles).
-__global__ __launch_bounds__(kScanThreads) void k_tiles(DeviceState d)
-{
-    __shared__ uint32_t s_scratch[64 + 3 * 256];
-    build_tiles<kScanThreads>(d, s_scratch);
-}
-
-// k_refrac: one wave per tile.  Per pre-gated entry the refractory gate with a
-// real 8-B gather of lastFired[dst] (brain.metal:79-83), the spike-candidate
-// test (brain.metal:91-92) and the homeostasis input isi (brain.metal:116);
-// per tile the two lane masks and, for the events that passed, the entry
-// {offset, dst, w, isi} at the tile's slot.  The gate is done with the filter
-// image, so it is zeroed here for the next k_bitmap.
+// k_refrac: the queued full chunks (k_gate), one wave per chunk; adds each
+// chunk's counts to its range.
 __global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
 {
-    const uint32_t lane = threadIdx.x & 63, gtid = blockIdx.x * 256 + threadIdx.x;
-    for (uint32_t i = gtid; i < d.filter_words; i += gridDim.x * 256) d.filter[i] = 0u;
-    const uint32_t wave = wave_uniform(gtid >> 6), nwaves = gridDim.x * 4;
-    const uint64_t now = *d.clock;
-    const uint32_t T = d.work->total_tiles;
-    const uint32_t nn = (uint32_t)d.n_nrn;
-    const uint64_t pass = *d.pass_index;
-    for (uint32_t tile = wave; tile < T; tile += nwaves) {
-        const uint4 td = d.tile_desc[tile];
-        const uint64_t region = range_begin(td.x, d.iters, d.n_ranges) * d.iter_events;
-        bool valid = lane < td.z;
-        const uint32_t rel = valid ? d.g1idx[region + td.y + lane] : 0u;
-        // the gate kept only the event offset: dst and w come from the record
-        const uint64_t ri = valid ? rec_index(d, region + rel, pass) : 0;
-        const uint32_t dst = valid ? d.syn.dst[ri] : 0u;
-        const float w = valid ? d.syn.w[ri] : 0.0f;
-        valid = valid && dst < nn;  // tombstones (dst = 0xFFFFFFFF) never pass
-        const uint64_t ld = valid ? d.last_fired[dst] : 0ull;
-        const bool g2 = valid && (now - ld) > (uint64_t)kp.refractory;
-        const uint64_t tg = d.syn_offset + region + rel;
-        const bool cand = g2 && spike_candidate(kp, w, tg, now);
-        const uint64_t bg = __ballot(g2), bc = __ballot(cand);
-        if (g2 && tg == 0) d.work->t0_g2 = 1;
-        if (g2) d.g2e[(uint64_t)tile * kTile + lane] = make_uint4(rel, dst, __float_as_uint(w), __float_as_uint((float)(now - ld)));
-        if (g2 && d.g2src) d.g2src[(uint64_t)tile * kTile + lane] = d.syn.src[ri];  // synaptogenesis keeps src
-        if (lane == 0)
-            d.tile_mask[tile] = make_uint4((uint32_t)bg, (uint32_t)(bg >> 32), (uint32_t)bc, (uint32_t)(bc >> 32));
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
+    const uint64_t now = *d.clock, pass = *d.pass_index;
+    const uint32_t n = d.work->n_ovf;
+    for (uint32_t i = wave; i < n; i += nwaves) {
+        const uint2 q = d.ovf[i];
+        const uint64_t region = region_of(d, q.x), base = region + (uint64_t)q.y * kChunk;
+        const uint32_t* rel = d.g1idx + base;
+        const uint2 c = d.mode == ABNN_MODE_RANDOM
+            ? refrac_chunk<kChunk / 64, true>(d, kp, region, base, kChunk, now, pass, [&](uint32_t j) { return rel[j]; })
+            : refrac_chunk<kChunk / 64, false>(d, kp, region, base, kChunk, now, pass, [&](uint32_t j) { return rel[j]; });
+        if (lane == 0) {
+            d.chunk_cnt[chunk_slot(region, q.y)] = c;
+            atomicAdd(&d.range_info[q.x].y, c.x);
+            atomicAdd(&d.range_info[q.x].z, c.y);
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_scan: ordered spike budget over the tiles (one workgroup, in event order).
-// Up to kSuper tiles per round: wave w scans a contiguous block of 64-tile
-// chunks held in registers; rounds carry the prefix (warm-up passes only).
-__global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelParams kp,
-                                                       int32_t* xchg_out)
+// The ordered spike budget of schedule C1 (brain.metal:85-98 without its
+// races): an event that passed both gates is updated iff fewer than
+// max_spikes spike candidates precede it in global event order.  Walked by
+// k_spikes, k_claim and k_apply alike.  Every workgroup first builds the
+// capped exclusive candidate prefix of all ranges in LDS (a few KB read from
+// L2; cheaper than a separate single-workgroup scan launch).  The work items
+// are the last chunk of every range and every queued full chunk, one per wave
+// at a time: an item adds the candidates of its range's lower full chunks,
+// leaves at once if the budget is spent, and otherwise visits its (<= kChunk)
+// survivors in event order, calling f(region, entry, candidate, budget
+// position, g2x index) for each one whose position is below the budget.
+constexpr uint32_t kWalkWaves = kApplyThreads / 64;
+constexpr uint32_t kPrePerThread = kMaxRanges / kApplyThreads;
+
+// s_pre[r] = min(off + candidates of ranges < r, budget), r < n_ranges.
+__device__ void range_prefix(const DeviceState& d, uint64_t off, uint64_t budget, uint32_t* s_pre, uint64_t* s_red)
 {
-    int64_t* summary_out = reinterpret_cast<int64_t*>(xchg_out);
-    constexpr uint32_t NWv = kScanThreads / 64, kCh = 16, kSuper = NWv * kCh * 64;
-    __shared__ uint32_t s_wt[NWv];
-    __shared__ uint64_t s_red[NWv];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = wave_uniform(tid >> 6);
-    const uint32_t T = d.work->total_tiles;
-    const uint64_t budget = kp.max_spikes;
-    uint64_t carry = 0, g2 = 0;
-    for (uint32_t base = 0; base < T; base += kSuper) {
-        const uint32_t n = min(T - base, kSuper);
-        const uint32_t per = ((n + NWv - 1) / NWv + 63) & ~63u, nch = per / 64;
-        uint32_t cg[kCh];  // candidates | passed-refractory << 16, per tile
+    const uint32_t NR = d.n_ranges, per = (NR + kApplyThreads - 1) / kApplyThreads, q0 = threadIdx.x * per;
+    uint32_t c[kPrePerThread];
+    uint64_t sum = 0;
 #pragma unroll
-        for (uint32_t c = 0; c < kCh; ++c) {
-            const uint32_t i = w * per + c * 64 + lane;
-            const uint4 m = (c < nch && i < n) ? d.tile_mask[base + i] : make_uint4(0u, 0u, 0u, 0u);
-            cg[c] = (uint32_t)(__popc(m.z) + __popc(m.w)) | ((uint32_t)(__popc(m.x) + __popc(m.y)) << 16);
-        }
-        uint32_t excl[kCh], run = 0;
-#pragma unroll
-        for (uint32_t c = 0; c < kCh; ++c) {
-            const uint32_t x = cg[c] & 0xFFFFu, inc = wave_incl_scan(x);
-            excl[c] = run + inc - x;
-            run += lane63(inc);
-            g2 += cg[c] >> 16;
-        }
-        if (lane == 0) s_wt[w] = run;
-        __syncthreads();
-        uint64_t off = carry, tot = 0;
-#pragma unroll
-        for (uint32_t v = 0; v < NWv; ++v) {
-            off += v < w ? s_wt[v] : 0u;
-            tot += s_wt[v];
-        }
-#pragma unroll
-        for (uint32_t c = 0; c < kCh; ++c) {
-            const uint32_t i = w * per + c * 64 + lane;
-            if (c < nch && i < n) {
-                const uint64_t pre = off + excl[c];
-                // a tile is applied iff some event in it passed the refractory
-                // gate while the budget lasted; inactive tiles carry the budget
-                d.tile_pre[base + i] = (uint32_t)((cg[c] >> 16) > 0 && pre < budget ? pre : budget);
-            }
-        }
-        carry += tot;
-        __syncthreads();  // s_wt is rewritten by the next round
+    for (uint32_t j = 0; j < kPrePerThread; ++j) {
+        c[j] = (j < per && q0 + j < NR) ? d.range_info[q0 + j].z : 0u;
+        sum += c[j];
     }
-    const uint64_t wg2 = wave_sum(g2);
-    if (lane == 0) s_red[w] = wg2;
+    uint64_t tot;
+    uint64_t run = off + block_exclusive_scan(sum, &tot, s_red);
+#pragma unroll
+    for (uint32_t j = 0; j < kPrePerThread; ++j) {
+        if (j < per && q0 + j < NR) s_pre[q0 + j] = (uint32_t)(run < budget ? run : budget);
+        run += c[j];
+    }
     __syncthreads();
-    if (tid == 0) {
-        uint64_t tg2 = 0;
-        for (uint32_t v = 0; v < NWv; ++v) tg2 += s_red[v];
-        const uint64_t capped = carry < budget ? carry : budget;
-        const uint32_t t0 = d.work->t0_g2;
-        summary_out[0] = (int64_t)capped;
-        summary_out[1] = (int64_t)t0;
+}
+
+template <class F>
+__device__ void budget_walk(const DeviceState& d, uint64_t off, uint64_t budget, uint32_t* s_pre, uint64_t* s_red,
+                            F&& f)
+{
+    range_prefix(d, off, budget, s_pre, s_red);
+    const uint32_t lane = threadIdx.x & 63, w = wave_uniform(threadIdx.x >> 6);
+    const uint32_t NR = d.n_ranges, items = NR + d.work->n_ovf;
+    for (uint32_t i = blockIdx.x * kWalkWaves + w; i < items; i += gridDim.x * kWalkWaves) {
+        uint32_t r, c;
+        if (i < NR) {
+            r = i;
+            c = d.range_info[r].w;  // the last chunk follows the full ones
+        } else {
+            const uint2 q = d.ovf[i - NR];
+            r = q.x;
+            c = q.y;
+        }
+        uint64_t P = s_pre[r];
+        if (P >= budget) continue;
+        const uint4 ri = d.range_info[r];
+        const uint64_t region = region_of(d, r);
+        const bool last = c == ri.w;
+        uint32_t cl = 0, gl = 0;  // candidates / survivors of the lower full chunks
+        for (uint32_t c0 = 0; c0 < c; c0 += 64)
+            if (c0 + lane < c) {
+                const uint2 cc = d.chunk_cnt[chunk_slot(region, c0 + lane)];
+                cl += cc.y;
+                gl += cc.x;
+            }
+        P += wave_sum(cl);
+        if (P >= budget) continue;
+        // survivors of this chunk: the last one holds what the full ones do not
+        const uint32_t n = last ? ri.y - wave_sum(gl) : d.chunk_cnt[chunk_slot(region, c)].x;
+        const uint64_t base = region + (uint64_t)c * kChunk;
+        constexpr uint32_t RW = kChunk / 64;
+        uint4 e[RW];
+#pragma unroll
+        for (uint32_t j = 0; j < RW; ++j)
+            e[j] = j * 64 + lane < n ? d.g2x[base + j * 64 + lane] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (uint32_t j = 0; j < RW; ++j) {
+            if (j * 64 >= n || P >= budget) break;  // wave-uniform
+            const bool v = j * 64 + lane < n, cand = v && (e[j].y >> 31);
+            const uint64_t bc = __ballot(cand);
+            const uint64_t pre = P + mbcnt64(bc);  // spike candidates before this event
+            if (v && pre < budget) f(region, e[j], cand, pre, base + j * 64 + lane);
+            P += (uint64_t)__popcll(bc);
+        }
+    }
+}
+
+// Budget slots taken by the lower ranks of a sharded pass (their gathered
+// exchange summaries), capped at the budget; 0 without an exchange.
+__device__ uint64_t rank_offset(const KernelParams& kp, const int32_t* gathered, uint32_t rank)
+{
+    const uint32_t words = xchg_words(kp.max_spikes);
+    uint64_t off = 0;
+    if (gathered)
+        for (uint32_t q = 0; q < rank; ++q) off += (uint64_t)*reinterpret_cast<const int64_t*>(gathered + q * words);
+    return off < kp.max_spikes ? off : kp.max_spikes;
+}
+
+// ---------------------------------------------------------------------------
+// k_scan (sharded passes): this shard's exchange summary -- candidates capped
+// at the budget, the event-0-updated flag, events visited, refractory passes.
+__global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelParams kp, int32_t* xchg_out)
+{
+    __shared__ uint64_t s_c[kScanThreads / 64], s_g[kScanThreads / 64];
+    int64_t* summary_out = reinterpret_cast<int64_t*>(xchg_out);
+    uint64_t c = 0, g = 0;
+    for (uint32_t q = threadIdx.x; q < d.n_ranges; q += kScanThreads) {
+        const uint4 ri = d.range_info[q];
+        c += ri.z;
+        g += ri.y;
+    }
+    c = wave_sum(c);
+    g = wave_sum(g);
+    if ((threadIdx.x & 63) == 0) {
+        s_c[threadIdx.x >> 6] = c;
+        s_g[threadIdx.x >> 6] = g;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t tc = 0, tg = 0;
+        for (uint32_t v = 0; v < kScanThreads / 64; ++v) {
+            tc += s_c[v];
+            tg += s_g[v];
+        }
+        const uint64_t budget = kp.max_spikes;
+        summary_out[0] = (int64_t)(tc < budget ? tc : budget);
+        summary_out[1] = (int64_t)d.work->t0_g2;
         summary_out[2] = (int64_t)d.events;
-        summary_out[3] = (int64_t)tg2;
-        d.work->t0_g2 = 0;  // re-armed for the next pass
-        d.work->events = d.events;
-        d.work->g2 = tg2;
+        summary_out[3] = (int64_t)tg;
     }
 }
 
 // ---------------------------------------------------------------------------
 // k_spikes (sharded passes only): this shard's spike list in local budget
 // order, written into its exchange record before the all-gather, so that every
-// rank can stamp every rank's spikes in k_finalize.  Same tile walk as k_apply.
-// The single-GPU pass skips it: k_apply writes the list there, in the same
-// order, at no extra launch.
-__global__ __launch_bounds__(256) void k_spikes(DeviceState d, KernelParams kp, int32_t* spikes)
+// rank can stamp every rank's spikes in k_finalize.
+__global__ __launch_bounds__(kApplyThreads) void k_spikes(DeviceState d, KernelParams kp, int32_t* spikes)
 {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
-    const uint64_t budget = kp.max_spikes;
-    const uint32_t T = d.work->total_tiles;
-    for (uint32_t tile = wave; tile < T; tile += nwaves) {
-        const uint64_t P = d.tile_pre[tile];
-        if (P >= budget) continue;
-        const uint4 m = d.tile_mask[tile];
-        const uint64_t bc = m.z | ((uint64_t)m.w << 32);
-        if (!((bc >> lane) & 1u)) continue;
-        const uint64_t pre = P + mbcnt64(bc);
-        if (pre < budget) spikes[pre] = (int32_t)d.g2e[(uint64_t)tile * kTile + lane].y;
-    }
+    extern __shared__ uint32_t s_pre[];
+    __shared__ uint64_t s_red[kWalkWaves];
+    budget_walk(d, 0, kp.max_spikes, s_pre, s_red, [&](uint64_t, const uint4& e, bool cand, uint64_t pre, uint64_t) {
+        if (cand) spikes[pre] = (int32_t)e.w;
+    });
 }
 
 // ---------------------------------------------------------------------------
 // k_claim (random mode): every event that will reach the update raises its
 // record's claim to its event index + 1, so k_apply lets only the highest
-// store (the last writer in event order).  Same tile walk as k_apply.
-__global__ __launch_bounds__(256) void k_claim(DeviceState d, KernelParams kp, const int32_t* gathered,
-                                               uint32_t rank)
+// store (the last writer in event order).
+__global__ __launch_bounds__(kApplyThreads) void k_claim(DeviceState d, KernelParams kp, const int32_t* gathered,
+                                                         uint32_t rank)
 {
-    const uint32_t words = xchg_words(kp.max_spikes);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
-    const uint64_t budget = kp.max_spikes, pass = *d.pass_index;
-    uint64_t off = 0;
-    for (uint32_t q = 0; q < rank; ++q) off += (uint64_t)*reinterpret_cast<const int64_t*>(gathered + q * words);
-    off = off < budget ? off : budget;
-    const uint32_t T = d.work->total_tiles;
-    for (uint32_t tile = wave; tile < T; tile += nwaves) {
-        const uint64_t P = off + d.tile_pre[tile];
-        if (P >= budget) continue;
-        const uint4 m = d.tile_mask[tile];
-        const uint64_t bg = m.x | ((uint64_t)m.y << 32), bc = m.z | ((uint64_t)m.w << 32);
-        if (!((bg >> lane) & 1u) || P + mbcnt64(bc) >= budget) continue;
-        const uint64_t region = range_begin(d.tile_desc[tile].x, d.iters, d.n_ranges) * d.iter_events;
-        const uint64_t t = region + d.g2e[(uint64_t)tile * kTile + lane].x;
-        atomicMax(d.claim + rec_index(d, t, pass), (uint32_t)(t + 1));
-    }
+    extern __shared__ uint32_t s_pre[];
+    __shared__ uint64_t s_red[kWalkWaves];
+    const uint64_t pass = *d.pass_index;
+    budget_walk(d, rank_offset(kp, gathered, rank), kp.max_spikes, s_pre, s_red,
+                [&](uint64_t region, const uint4& e, bool, uint64_t, uint64_t) {
+                    const uint64_t t = region + e.x;
+                    atomicMax(d.claim + rec_index(d, t, pass), (uint32_t)(t + 1));
+                });
 }
 
 // ---------------------------------------------------------------------------
-// k_apply: weight update of the gated events that still had budget; one wave
-// per tile, tiles past the budget skipped on one load.
-__global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
-                                               const int32_t* gathered, uint32_t rank,
-                                               int32_t* spikes)
+// k_apply: weight update (brain.metal:101-122) of the gated events that still
+// had budget.  Single GPU (no exchange): the spikes are stamped here
+// (brain.metal:125-126, deferred to after every lastFired read of the pass);
+// sharded passes stamp from the gathered spike lists in k_finalize.
+__global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelParams kp,
+                                                         const int32_t* gathered, uint32_t rank)
 {
-    const uint32_t words = xchg_words(kp.max_spikes);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
-    const uint64_t budget = kp.max_spikes;
+    extern __shared__ uint32_t s_pre[];
+    __shared__ uint64_t s_red[kWalkWaves];
+    __shared__ uint32_t s_u[kWalkWaves], s_f[kWalkWaves], s_p[kWalkWaves];
+    // every gate workgroup has its copy of the filter image: zero it for the next k_bitmap
+    for (uint32_t i = blockIdx.x * kApplyThreads + threadIdx.x; i < d.filter_words; i += gridDim.x * kApplyThreads)
+        d.filter[i] = 0u;
     const float R = *d.reward, rb = *d.rbar;  // pass-start values (C1), brain.metal:105-106
-    uint64_t off = 0;
-    for (uint32_t q = 0; q < rank; ++q) off += (uint64_t)*reinterpret_cast<const int64_t*>(gathered + q * words);
-    off = off < budget ? off : budget;
-
-    const uint32_t T = d.work->total_tiles;
-    const uint64_t pass = *d.pass_index;
-    const bool random = d.mode == ABNN_MODE_RANDOM;
+    const uint64_t now = *d.clock, pass = *d.pass_index;
+    const bool random = d.mode == ABNN_MODE_RANDOM, stamp = gathered == nullptr;
     const bool prune = kp.w_prune > 0.0f, genesis = d.grown != nullptr && kp.p_new > 0.0f;
     uint32_t upd = 0, nf = 0, npr = 0;
-    for (uint32_t tile = wave; tile < T; tile += nwaves) {
-        const uint64_t P = off + d.tile_pre[tile];
-        if (P >= budget) continue;
-        const uint4 m = d.tile_mask[tile];
-        const uint64_t bg = m.x | ((uint64_t)m.y << 32), bc = m.z | ((uint64_t)m.w << 32);
-        if (!((bg >> lane) & 1u)) continue;   // no entry, or stopped by the refractory gate
-        const uint64_t pre = P + mbcnt64(bc);  // spike candidates before this event
-        if (pre >= budget) continue;           // budget == 0 at this event: brain.metal:85-88
-        const uint64_t region = range_begin(d.tile_desc[tile].x, d.iters, d.n_ranges) * d.iter_events;
-        const uint4 e = d.g2e[(uint64_t)tile * kTile + lane];
-        const bool f = (bc >> lane) & 1u;
-        const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.w));
+    budget_walk(d, rank_offset(kp, gathered, rank), kp.max_spikes, s_pre, s_red,
+                [&](uint64_t region, const uint4& e, bool f, uint64_t pre, uint64_t slot) {
+        const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.y & 0x7FFFFFFFu));
         const uint64_t t = region + e.x, ri = rec_index(d, t, pass);
         // random mode: of the events that updated one synapse this pass, the
         // highest (k_claim) stores its weight; every one of them still counts
@@ -700,37 +709,44 @@ __global__ __launch_bounds__(256) void k_apply(DeviceState d, KernelParams kp,
             __builtin_nontemporal_store(w, d.syn.w + ri);
         }
         ++upd;
-        if (f) {  // its stamp comes from the exchange record (k_finalize)
-            if (spikes) spikes[pre] = (int32_t)e.y;  // single GPU: off == 0, local order
+        if (f) {
+            if (stamp) d.last_fired[e.w] = now;  // brain.metal:125-126
             ++nf;
             if (genesis) {  // README §5 synaptogenesis: slot `pre` of this pass
                 const uint64_t x = splitmix64_at(d.seed ^ ABNN_GENESIS_KEY, (pass << 32) | pre);
                 if (unit24(x) < kp.p_new) {
                     const uint64_t span = d.n_nrn - d.n_input;
                     d.grown[(pass % kp.compact_every) * kp.max_spikes + pre] =
-                        make_uint4(d.g2src[(uint64_t)tile * kTile + lane],
-                                   d.n_input + (uint32_t)(((x & 0xFFFFFFFFull) * span) >> 32),
+                        make_uint4(d.g2src[slot], d.n_input + (uint32_t)(((x & 0xFFFFFFFFull) * span) >> 32),
                                    __float_as_uint(kp.w_init), 1u);
                 }
             }
         }
-    }
+    });
     // per-workgroup partials (atomics from every wave on one address serialise)
-    __shared__ uint32_t s_u[4], s_f[4], s_p[4];
     const uint32_t wu = wave_sum(upd), wf = wave_sum(nf), wp = wave_sum(npr);
-    if (lane == 0) {
+    if ((threadIdx.x & 63) == 0) {
         s_u[threadIdx.x >> 6] = wu;
         s_f[threadIdx.x >> 6] = wf;
         s_p[threadIdx.x >> 6] = wp;
     }
     __syncthreads();
-    if (threadIdx.x == 0)
-        d.apply_partial[blockIdx.x] = make_uint4(s_u[0] + s_u[1] + s_u[2] + s_u[3], s_f[0] + s_f[1] + s_f[2] + s_f[3],
-                                                 s_p[0] + s_p[1] + s_p[2] + s_p[3], 0u);
+    if (threadIdx.x == 0) {
+        uint4 t = make_uint4(0u, 0u, 0u, 0u);
+        for (uint32_t v = 0; v < kWalkWaves; ++v) {
+            t.x += s_u[v];
+            t.y += s_f[v];
+            t.z += s_p[v];
+        }
+        d.apply_partial[blockIdx.x] = t;
+    }
 }
 
 // ---------------------------------------------------------------------------
-// k_finalize: stamps, rBar, clock tick, statistics (one workgroup).
+// k_finalize: rBar (brain.metal:110-113), clock tick (brain.metal:129),
+// statistics; in sharded passes also the deferred stamps of every rank's
+// spikes from the gathered exchange records (brain.metal:125-126).  One
+// workgroup.
 __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, KernelParams kp,
                                                            const int32_t* gathered, uint32_t world)
 {
@@ -738,49 +754,65 @@ __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, Kernel
     const uint32_t tid = threadIdx.x, words = xchg_words(kp.max_spikes);
     const uint64_t now = *d.clock;
     const uint64_t budget = kp.max_spikes;
-    uint64_t events = 0, off = 0;
-    int64_t t0 = 0;
-    for (uint32_t r = 0; r < world; ++r) {
-        const int64_t* sm = reinterpret_cast<const int64_t*>(gathered + r * words);
-        const int32_t* sp = gathered + r * words + 2 * ABNN_SUMMARY_WORDS;
-        events += (uint64_t)sm[2];
-        t0 |= sm[1];
-        // rank r's spikes fill budget slots [off, off + n): brain.metal:125-126, deferred
-        const uint64_t room = budget - off, n = (uint64_t)sm[0] < room ? (uint64_t)sm[0] : room;
-        for (uint64_t i0 = 0; i0 < n; i0 += kU * kScanThreads) {
-            uint32_t nrn[kU];
+    uint64_t events = d.events, off = 0;
+    int64_t t0 = d.work->t0_g2;
+    if (gathered) {
+        events = 0;
+        t0 = 0;
+        for (uint32_t r = 0; r < world; ++r) {
+            const int64_t* sm = reinterpret_cast<const int64_t*>(gathered + r * words);
+            const int32_t* sp = gathered + r * words + 2 * ABNN_SUMMARY_WORDS;
+            events += (uint64_t)sm[2];
+            t0 |= sm[1];
+            // rank r's spikes fill budget slots [off, off + n)
+            const uint64_t room = budget - off, n = (uint64_t)sm[0] < room ? (uint64_t)sm[0] : room;
+            for (uint64_t i0 = 0; i0 < n; i0 += kU * kScanThreads) {
+                uint32_t nrn[kU];
 #pragma unroll
-            for (uint32_t u = 0; u < kU; ++u) {
-                const uint64_t i = i0 + u * kScanThreads + tid;
-                nrn[u] = i < n ? (uint32_t)sp[i] : 0xFFFFFFFFu;
+                for (uint32_t u = 0; u < kU; ++u) {
+                    const uint64_t i = i0 + u * kScanThreads + tid;
+                    nrn[u] = i < n ? (uint32_t)sp[i] : 0xFFFFFFFFu;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kU; ++u)
+                    if (nrn[u] < d.n_nrn) d.last_fired[nrn[u]] = now;
             }
-#pragma unroll
-            for (uint32_t u = 0; u < kU; ++u)
-                if (nrn[u] < d.n_nrn) d.last_fired[nrn[u]] = now;
+            off += n;
         }
-        off += n;
+    }
+    uint64_t g1 = 0, g2 = 0;
+    for (uint32_t q = tid; q < d.n_ranges; q += kScanThreads) {
+        const uint4 ri = d.range_info[q];
+        g1 += ri.x;
+        g2 += ri.y;
     }
     uint32_t upd = 0, nf = 0, npr = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < kTileBlocks / kScanThreads; ++u) {
-        const uint4 v = d.apply_partial[u * kScanThreads + tid];
-        upd += v.x;
-        nf += v.y;
-        npr += v.z;
+    if (tid < kWalkBlocks) {
+        const uint4 v = d.apply_partial[tid];
+        upd = v.x;
+        nf = v.y;
+        npr = v.z;
     }
+    __shared__ uint64_t s_a[kScanThreads / 64], s_b[kScanThreads / 64];
     __shared__ uint32_t s_u[kScanThreads / 64], s_f[kScanThreads / 64], s_p[kScanThreads / 64];
+    g1 = wave_sum(g1);
+    g2 = wave_sum(g2);
     upd = wave_sum(upd);
     nf = wave_sum(nf);
     npr = wave_sum(npr);
     if ((tid & 63) == 0) {
+        s_a[tid >> 6] = g1;
+        s_b[tid >> 6] = g2;
         s_u[tid >> 6] = upd;
         s_f[tid >> 6] = nf;
         s_p[tid >> 6] = npr;
     }
     __syncthreads();
     if (tid == 0) {
-        uint64_t tu = 0, tf = 0, tp = 0;
+        uint64_t ta = 0, tb = 0, tu = 0, tf = 0, tp = 0;
         for (int w = 0; w < kScanThreads / 64; ++w) {
+            ta += s_a[w];
+            tb += s_b[w];
             tu += s_u[w];
             tf += s_f[w];
             tp += s_p[w];
@@ -791,10 +823,12 @@ __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, Kernel
         if (events > 0) *d.clock = now + kp.clock_inc; // brain.metal:129
         *d.pass_index += 1;
         PassWork* w = d.work;
+        w->t0_g2 = 0;  // re-armed for the next pass
+        w->n_ovf = 0;
         w->stats.passes += 1;
-        w->stats.events += w->events;
-        w->stats.pre_gated += w->g1;
-        w->stats.post_gated += w->g2;
+        w->stats.events += d.events;
+        w->stats.pre_gated += ta;
+        w->stats.post_gated += tb;
         w->stats.updated += tu;
         w->stats.fired += tf;
         w->stats.pruned += tp;
@@ -906,6 +940,9 @@ __global__ __launch_bounds__(256) void k_stamp_list(DeviceState d, const uint32_
 
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
+// budget walks: s_pre holds one u32 per range
+inline size_t walk_lds(const DeviceState& d) { return (size_t)std::max(1u, d.n_ranges) * 4; }
+
 template <int BLOCK, int K, int FW>
 hipError_t launch_gate_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
 {
@@ -985,10 +1022,7 @@ hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t 
 
 hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_tiles, dim3(1), dim3(kScanThreads), 0, s, d);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_refrac, dim3(kTileBlocks), dim3(256), 0, s, d, kp);
+    hipLaunchKernelGGL(k_refrac, dim3(kRefracBlocks), dim3(256), 0, s, d, kp);
     return hipGetLastError();
 }
 
@@ -1003,28 +1037,27 @@ hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out,
-                       bool spike_list, hipStream_t s)
+hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out, hipStream_t s)
 {
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, d, kp, xchg_out);
-    if (!spike_list) return hipGetLastError();
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_spikes, dim3(kTileBlocks), dim3(256), 0, s, d, kp,
+    // at least one workgroup: it also zeroes the filter image (no ranges: a no-op walk)
+    hipLaunchKernelGGL(k_spikes, dim3(kWalkBlocks), dim3(kApplyThreads), walk_lds(d), s, d, kp,
                        xchg_out + 2 * ABNN_SUMMARY_WORDS);
     return hipGetLastError();
 }
 
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
-                        uint32_t world, uint32_t rank, int32_t* spikes, hipStream_t s)
+                        uint32_t rank, hipStream_t s)
 {
-    if (spikes && (world != 1 || rank != 0)) return hipErrorInvalidValue;
+    const dim3 g(kWalkBlocks), b(kApplyThreads);
     if (d.mode == ABNN_MODE_RANDOM) {
-        hipLaunchKernelGGL(k_claim, dim3(kTileBlocks), dim3(256), 0, s, d, kp, gathered, rank);
+        hipLaunchKernelGGL(k_claim, g, b, walk_lds(d), s, d, kp, gathered, rank);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_apply, dim3(kTileBlocks), dim3(256), 0, s, d, kp, gathered, rank, spikes);
+    hipLaunchKernelGGL(k_apply, g, b, walk_lds(d), s, d, kp, gathered, rank);
     return hipGetLastError();
 }
 
