@@ -222,8 +222,9 @@ class Brain:
     def reset_stats(self) -> None:
         call("abnn_reset_stats", self._h)
 
-    def enable_timing(self, on: bool = True) -> None:
-        call("abnn_enable_timing", self._h, 1 if on else 0)
+    def enable_timing(self, on: bool | int = True) -> None:
+        """True/1: time every gate launch; n > 1: every n-th; False/0: off."""
+        call("abnn_enable_timing", self._h, int(on))
 
     def kernel_time(self) -> tuple[float, int]:
         ms = C.c_double()

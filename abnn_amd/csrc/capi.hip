@@ -62,7 +62,8 @@ struct abnn_brain {
     uint64_t rng = 0;              // host RNG of inject_inputs
     uint64_t stim_first = 0, stim_count = 0;
     bool pending_renorm = false;   // shard protocol: decided at gate time
-    bool timing = false;
+    int timing = 0;                // time every timing-th gate launch (0: off)
+    uint64_t timing_count = 0;
     std::vector<EventPair> events;
     size_t events_used = 0;
     uint32_t* idx_scratch = nullptr;
@@ -98,11 +99,11 @@ void free_all(abnn_brain* b)
                     b->syn_alt.src, b->syn_alt.dst,  b->syn_alt.w,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->d.bitmap,    b->d.filter,     b->d.range_info,    b->d.g2x,
-                    b->d.g1idx,     b->d.chunk_cnt,  b->d.ovf,
+                    b->d.chunk_cnt,
                     b->d.apply_partial, b->d.claim,  b->d.g2src,      b->d.grown,
                     b->d.dead,      b->compact_offsets,
                     b->d.work,      b->idx_scratch,
-                    b->u64_scratch,  b->d.wave_clock,  const_cast<uint32_t*>(b->d.dummy)};
+                    b->u64_scratch,  b->d.wave_clock,  b->d.range_bounds,  const_cast<uint32_t*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : b->events) {
@@ -221,7 +222,7 @@ void host_tick(abnn_brain* b)
 abnn_status time_begin(abnn_brain* b, hipStream_t s, EventPair** out)
 {
     *out = nullptr;
-    if (!b->timing) return ABNN_OK;
+    if (b->timing <= 0 || (b->timing_count++ % (uint64_t)b->timing) != 0) return ABNN_OK;
     if (b->events_used == b->events.size()) {
         EventPair p;
         HIP_TRY(hipEventCreate(&p.a));
@@ -250,6 +251,17 @@ void configure(abnn_brain* b)
     if (G == 0 && iters > 0) G = 1;
     d.gate_blocks = (uint32_t)G;
     d.n_ranges = (uint32_t)(G * waves);  // <= kMaxGateBlocks * 16 = kMaxRanges
+}
+
+// Uniform sweep partition: range r starts at iteration floor(r * iters / NR)
+// (k_finalize then adapts it pass by pass).
+abnn_status reset_ranges(abnn_brain* b)
+{
+    const DeviceState& d = b->d;
+    std::vector<uint32_t> rb(d.n_ranges + 1);
+    for (uint32_t r = 0; r <= d.n_ranges; ++r) rb[r] = (uint32_t)((uint64_t)r * d.iters / std::max(1u, d.n_ranges));
+    HIP_TRY(hipMemcpy(d.range_bounds, rb.data(), rb.size() * 4, hipMemcpyHostToDevice));
+    return ABNN_OK;
 }
 
 // README §5 structural update (contract in abnn.h): stable removal of the
@@ -309,7 +321,7 @@ abnn_status structural_update(abnn_brain* b)
     grown += added;
     HIP_TRY(hipMemcpy(&d.work->stats.grown, &grown, 8, hipMemcpyHostToDevice));
     configure(b);
-    return ABNN_OK;
+    return reset_ranges(b);
 }
 
 // bitmap + streaming gate (with the refractory stage) [+ the exchange record
@@ -321,7 +333,6 @@ abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
     ST_TRY(time_begin(b, s, &ev));
     HIP_TRY(launch_gate(b->d, b->kp, s));
     if (ev) HIP_TRY(hipEventRecord(ev->b, s));
-    HIP_TRY(launch_refrac(b->d, b->kp, s));
     if (xchg_out) HIP_TRY(launch_scan(b->d, b->kp, xchg_out, s));
     return ABNN_OK;
 }
@@ -417,9 +428,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     const uint64_t E = visited_events(dmax, p.mode);  // the most events a pass can visit
     REQUIRE(p.mode != ABNN_MODE_RANDOM || E < 0xFFFFFFFFull, "random mode: events per pass must fit u32");
     const bool genesis = p.p_new > 0.0f && p.compact_every > 0;
-    // Gate kernel shape: threads per workgroup x events per lane x LDS filter
-    // KiB (ABNN_GATE="512x8f32"; tuning knob, the default is the measured best).
-    uint32_t gate_block = 512, gate_k = 8, filter_kib = 32;
+    // Gate kernel shape: threads per workgroup x events per lane x KiB per LDS
+    // filter image (ABNN_GATE="1024x8f32"; tuning knob, the default is the measured best).
+    uint32_t gate_block = 1024, gate_k = 8, filter_kib = 32;
     if (const char* env = std::getenv("ABNN_GATE")) {
         unsigned gb = 0, gk = 0, fk = 0;
         const int got = std::sscanf(env, "%ux%uf%u", &gb, &gk, &fk);
@@ -484,7 +495,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     const uint64_t max_ranges = (uint64_t)std::min<int>(kMaxGateBlocks, cus * per_cu) * (gate_block / 64);
     d.n_bitmap_words = (uint32_t)(2 * ((n_nrn + 63) / 64));
     d.filter_words = filter_words;
-    d.filter_exact = d.n_bitmap_words <= filter_words ? 1u : 0u;
+    d.filter_log2 = (uint32_t)__builtin_ctz(filter_words);
     abnn_status s;
     // build_buffers, brain.cpp:52-69: allocate and zero every buffer.
     // padded: the gate's last iteration reads up to one iteration past the sweep
@@ -499,14 +510,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.rbar = d.reward + 1;
     d.pass_index = sb + 2;
     if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.filter, kMaxFilterWords)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.filter, 2 * kMaxFilterWords)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_info, max_ranges)) != ABNN_OK) return fail(s);
     // per-range regions of refractory survivors (16 B per event: every event of
     // a range may pass in the warm-up passes)
     if ((s = dalloc(&d.g2x, iters * iter_events)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.g1idx, iters * iter_events)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.chunk_cnt, iters * iter_events / kChunkSlotDiv + 8)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.ovf, iters * iter_events / kChunk + max_ranges)) != ABNN_OK) return fail(s);
     uint32_t* dummy = nullptr;
     if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
     d.dummy = dummy;
@@ -524,7 +533,10 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     }
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
-    if (std::getenv("ABNN_WAVE_CLOCK") && (s = dalloc(&d.wave_clock, 4 * max_ranges)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.wave_clock, 4 * (uint64_t)kMaxRanges + 16)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.range_bounds, max_ranges + 1)) != ABNN_OK) return fail(s);
+    d.adapt_ranges = std::getenv("ABNN_STATIC_RANGES") ? 0u : 1u;
+    if ((s = reset_ranges(b)) != ABNN_OK) return fail(s);
     *out = b;
     return ABNN_OK;
 }
@@ -808,12 +820,22 @@ abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t 
 }
 
 // Diagnostics (not part of abnn.h): the last pass's per-wave gate times
-// {start, stream done, end, hw id} in 100 MHz ticks; needs ABNN_WAVE_CLOCK at create.
+// {start, stream done, end, hw id} in 100 MHz ticks, then the range bounds.
 abnn_status abnn_debug_wave_clock(abnn_brain* b, uint64_t* out, uint64_t n)
 {
-    REQUIRE(b && out && b->d.wave_clock, "wave clock not enabled");
+    REQUIRE(b && out, "null argument");
     ST_TRY(sync_all(b));
-    HIP_TRY(hipMemcpy(out, b->d.wave_clock, std::min<uint64_t>(n, 4ull * b->d.n_ranges) * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out, b->d.wave_clock, std::min<uint64_t>(n, 4ull * kMaxRanges + 16) * 8, hipMemcpyDeviceToHost));
+    return ABNN_OK;
+}
+
+// Diagnostics (not part of abnn.h): the current sweep partition, n_ranges + 1
+// iteration bounds.
+abnn_status abnn_debug_range_bounds(abnn_brain* b, uint32_t* out, uint64_t n)
+{
+    REQUIRE(b && out, "null argument");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(out, b->d.range_bounds, std::min<uint64_t>(n, b->d.n_ranges + 1ull) * 4, hipMemcpyDeviceToHost));
     return ABNN_OK;
 }
 
@@ -833,11 +855,12 @@ abnn_status abnn_reset_stats(abnn_brain* b)
     return ABNN_OK;
 }
 
-abnn_status abnn_enable_timing(abnn_brain* b, int on)
+abnn_status abnn_enable_timing(abnn_brain* b, int every)
 {
-    REQUIRE(b, "null argument");
+    REQUIRE(b && every >= 0, "bad argument");
     ST_TRY(sync_all(b));
-    b->timing = on != 0;
+    b->timing = every;
+    b->timing_count = 0;
     b->events_used = 0;
     return ABNN_OK;
 }

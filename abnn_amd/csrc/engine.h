@@ -10,10 +10,10 @@
 
 namespace abnn {
 
-// Pre-spike filter kept in LDS by every gate workgroup: the exact recent-spike
-// bitmap folded modulo filter_words 32-bit words (16384 words = 512 Ki bits =
-// 32 KiB by default).  When the bitmap itself fits, the filter IS the bitmap.
-constexpr int kMaxFilterWords = 16384;
+// Pre-spike filter kept in LDS by every gate workgroup: two images of the exact
+// recent-spike bitmap, each folded onto filter_words 32-bit words with its own
+// word hash (kernels.hip; 8192 words = 32 KiB each by default).
+constexpr int kMaxFilterWords = 16384;  // per image
 constexpr int kScanThreads = 1024; // k_scan and k_finalize are one workgroup each
 constexpr int kMaxGateBlocks = 1024;
 constexpr int kMaxRanges = 16384;  // kMaxGateBlocks x up to 16 waves (one range per gate wave)
@@ -25,13 +25,11 @@ static_assert(kMaxRanges % kApplyThreads == 0, "range prefix: whole ranges per t
 constexpr int kDummyRecords = 64 * 32;  // >= 64 lanes x max events per lane; also the record-buffer padding
 constexpr uint32_t kChunk = 384;        // pre-gated events per chunk (staged in LDS by a gate wave)
 constexpr uint32_t kChunkSlotDiv = 128; // chunk_cnt index = (region + c * kChunk) / 128 (unique per chunk)
-constexpr int kRefracBlocks = 512;      // k_refrac grid (x 4 waves; one queued chunk per wave at a time)
 
 // Per-pass bookkeeping in device memory (one per handle).
 struct alignas(16) PassWork {
     uint32_t t0_g2;        // global event 0 passed both gates this pass (re-armed by k_finalize)
-    uint32_t n_ovf;        // full chunks queued for k_refrac this pass (re-armed by k_finalize)
-    uint32_t pad[2];
+    uint32_t pad[3];
     abnn_stats stats;      // cumulative (finalize adds)
 };
 
@@ -56,12 +54,10 @@ struct DeviceState {
     float* reward;            // [1]
     float* rbar;              // [1]
     uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
-    uint32_t* filter;         // [filter_words] folded bitmap
+    uint32_t* filter;         // [2 * filter_words] the two folded bitmap images
     uint4* range_info;        // [n_ranges] {pre-gated, passed refractory, candidates, chunks} per gate wave
-    uint32_t* g1idx;          // [iters * iter_events] per-range regions: offsets of full chunks (k_refrac input)
     uint4* g2x;               // [iters * iter_events] per-range regions: {event - region, isi | cand << 31, w, dst}
-    uint2* chunk_cnt;         // [iters * iter_events / kChunkSlotDiv + 8] {survivors, candidates} per chunk
-    uint2* ovf;               // [iters * iter_events / kChunk + n_ranges] queued full chunks {range, chunk}
+    uint4* chunk_cnt;         // [iters * iter_events / kChunkSlotDiv + 8] {pre-gated, survivors, candidates, 0}
     const uint32_t* dummy;    // [kDummyRecords] zeros: target of the stream loads past a range
     uint4* apply_partial;     // [kMaxApplyBlocks] {updated, fired, pruned, 0} per apply workgroup
     uint32_t* g2src;          // genesis on: [iters * iter_events] src of the g2x entry's record
@@ -69,7 +65,9 @@ struct DeviceState {
     uint32_t* dead;           // pruning on: tombstones per kCompactChunk records (structural update)
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     PassWork* work;
-    uint64_t* wave_clock;     // diagnostics only (ABNN_WAVE_CLOCK): [4 * n_ranges] per-wave gate times
+    uint64_t* wave_clock;     // [4 * n_ranges] per-wave gate times {start, stream done, end, hw id} (100 MHz)
+    uint32_t* range_bounds;   // [n_ranges + 1] first iteration of each range (adaptive, k_finalize)
+    uint32_t adapt_ranges;    // rebalance the partition after every pass (default on; ABNN_STATIC_RANGES=1: off)
     uint64_t n_syn;           // local records
     uint64_t n_nrn;
     uint32_t n_input;
@@ -78,8 +76,8 @@ struct DeviceState {
     uint64_t seed;            // random-mode pick key (abnn_params.seed)
     uint32_t mode;            // ABNN_MODE_SWEEP / ABNN_MODE_RANDOM
     uint32_t n_bitmap_words;  // 2 * ceil(n_nrn / 64)
-    uint32_t filter_words;    // LDS filter size (a power of two, compiled per gate shape)
-    uint32_t filter_exact;    // bitmap fits the filter: no global confirmation
+    uint32_t filter_words;    // words per LDS filter image (a power of two, compiled per gate shape)
+    uint32_t filter_log2;     // log2(filter_words)
     uint32_t gate_blocks;     // persistent gate workgroups G
     uint32_t n_ranges;        // G * waves per workgroup: one contiguous range per wave
     uint32_t iters;           // ceil(events / iter_events)
@@ -118,7 +116,6 @@ int gate_blocks_per_cu(uint32_t block, uint32_t k, uint32_t filter_words, bool t
 hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,
                          uint64_t stim_count, hipStream_t s);
 hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s);
-hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream_t s);
 // Sharded passes: this shard's exchange record (summary + local spike list).
 hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out, hipStream_t s);
 // gathered == nullptr: single-GPU pass (no exchange; k_apply stamps the spikes).

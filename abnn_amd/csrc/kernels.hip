@@ -1,35 +1,33 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of one C1 traversal pass.
 //
 // Reference hot path: monte_carlo_traversal (abnn/src/core/kernels/brain.metal:41-130)
-// and renormalise_clock_and_times (brain.metal:135-145).  One pass = seven
-// launches, each doing one HBM-friendly thing:
+// and renormalise_clock_and_times (brain.metal:135-145).  One single-GPU pass =
+// four launches:
 //
 //   k_bitmap   : lastFired (u64, 8 B/neuron, read once) -> exact recent-spike
 //                bitmap, bit i = (now - lastFired[i]) <= WINDOW_PRE, OR-folded
-//                into the LDS filter image; the per-pass stimulus stamp is
-//                fused here.
+//                into the two LDS filter images; the per-pass stimulus stamp
+//                is fused here.
 //   k_gate     : THE streaming kernel.  Persistent workgroups whose waves each
-//                sweep one contiguous range of events, loading only the src
-//                word of every 16-B SynapsePacked record (the same HBM lines,
-//                one VGPR per event in flight).  Pre-spike gate
-//                (brain.metal:73-77) = one LDS filter bit + an L2 bitmap word
-//                on a filter hit; passing events are staged in event order as
-//                4-B offsets and flushed once per range.  Random-edge mode:
-//                the same loop on Philox-picked records.
-//   k_tiles    : one workgroup: 64-entry tiles over the ranges (descriptors).
-//   k_refrac   : per tile: the record re-read, the refractory gate
-//                (brain.metal:79-83) with a real lastFired[dst] gather, the
-//                spike-candidate test (brain.metal:91-92), isi.
-//   k_scan     : one workgroup: exclusive candidate prefix over the tiles =
-//                the ordered global spike budget of schedule C1
-//                (brain.metal:85-98 without its races) + the shard summary.
-//   k_apply    : weight update (brain.metal:101-122) of every gated event that
-//                still had budget (non-temporal stores; pruning, synaptogenesis);
-//                spikes land at their budget position.  k_claim precedes it in
-//                random mode (highest event wins a record).
-//   k_finalize : deferred lastFired stamps (brain.metal:125-126), rBar EWMA
-//                (brain.metal:110-113), one clock tick (brain.metal:129).
+//                sweep one contiguous range of events (adaptive partition),
+//                loading only the src word of every record (4 B per event).
+//                Pre-spike filter (brain.metal:73-77) = two LDS bits per event;
+//                events that pass are staged in LDS and, per chunk, run
+//                through the refractory stage by the same wave: exact pre-gate
+//                on the bitmap, record re-read, lastFired[dst] gather,
+//                refractory gate (brain.metal:79-83), spike-candidate test
+//                (brain.metal:91-92), isi.  Random-edge mode: the same loop on
+//                Philox-picked records.
+//   k_apply    : the ordered spike budget of schedule C1 (brain.metal:85-98
+//                without its races) walked over the chunks, weight update
+//                (brain.metal:101-122, non-temporal stores; pruning,
+//                synaptogenesis) and the deferred stamps (brain.metal:125-126).
+//                k_claim precedes it in random mode (highest event wins).
+//   k_finalize : rBar EWMA (brain.metal:110-113), one clock tick
+//                (brain.metal:129), statistics, the next pass's partition.
 //   k_renorm   : brain.metal:135-145 with the base read once (no race).
+//   Sharded passes add k_scan + k_spikes (the exchange record) after the gate
+//   and stamp every rank's spikes in k_finalize.
 //
 // All fp32 arithmetic is compiled with -ffp-contract=off and written operation
 // for operation like the oracle, so weights are bit-identical to the CPU.
@@ -170,11 +168,31 @@ __device__ __forceinline__ T wave_sum(T v)
     return v;
 }
 
-// Exclusive scan of one u64 per thread over a kScanThreads workgroup.
+// Inclusive wave scan on DPP (row_shr within 16-lane rows, then the gfx9
+// row broadcasts): six VALU ops, no LDS crossbar round trips.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+    int v = (int)x;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return (uint32_t)v;
+}
+
+__device__ __forceinline__ uint32_t wave_total(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(x), 63);
+}
+
+// Exclusive scan of one u64 per thread over an NT-thread workgroup.
+template <int NT = kScanThreads>
 __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total, uint64_t* s_wave)
 {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    constexpr uint32_t nw = kScanThreads / 64;
+    constexpr uint32_t nw = NT / 64;
     uint64_t inc = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -197,6 +215,21 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total, uint64_t* 
 __device__ __forceinline__ uint64_t range_begin(uint32_t b, uint32_t iters, uint32_t G)
 {
     return (uint64_t)b * iters / G;
+}
+
+// ---------------------------------------------------------------------------
+// Pre-spike filter: two LDS images of the exact recent-spike
+// bitmap, each folded onto FW 32-bit words with its own word hash; bit i % 32
+// of word h(i / 32).  A neuron passes the filter iff its bit is set in both
+// (false positives ~0.5 % at config 3 with 2 x 32 KiB, no false negatives);
+// the exact bitmap confirms the staged events in the refractory stage.
+// Word hashes of j = neuron / 32: h1 = j mod FW; h2 mixes in the bits above
+// log2(FW) (those h1 drops) with a 24-bit multiply, so neurons that collide
+// in h1 mostly do not collide in h2.
+__device__ __forceinline__ uint32_t filter_word1(uint32_t j, uint32_t FW) { return j & (FW - 1); }
+__device__ __forceinline__ uint32_t filter_word2(uint32_t j, uint32_t FW, uint32_t lg)
+{
+    return (j ^ __umul24(j >> lg, 0x9E5u)) & (FW - 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -230,33 +263,42 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
         const uint64_t m = __ballot(bit);
         if (lane == 0 && (wave * 4 + q) * 64 < d.n_nrn) {
             reinterpret_cast<uint64_t*>(d.bitmap)[wave * 4 + q] = m;
-            // fold into the LDS filter image: filter[j] |= bitmap[j + m * filter_words]
-            // (zeroed by k_refrac of the previous pass; few words are non-zero)
-            const uint32_t w0 = (uint32_t)(wave * 4 + q) * 2u, fm = d.filter_words - 1u;
-            if ((uint32_t)m) atomicOr(d.filter + (w0 & fm), (uint32_t)m);
-            if ((uint32_t)(m >> 32)) atomicOr(d.filter + ((w0 + 1u) & fm), (uint32_t)(m >> 32));
+            // fold into the two LDS filter images (zeroed by k_apply of the
+            // previous pass; few words are non-zero)
+            const uint32_t w0 = (uint32_t)(wave * 4 + q) * 2u, FW = d.filter_words, lg = d.filter_log2;
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t part = (uint32_t)(m >> (32 * h));
+                if (part) {
+                    atomicOr(d.filter + filter_word1(w0 + h, FW), part);
+                    atomicOr(d.filter + FW + filter_word2(w0 + h, FW, lg), part);
+                }
+            }
         }
     }
 }
 
 // ---------------------------------------------------------------------------
 // Per-range results of the gate.  A range is the contiguous block of events
-// one gate wave sweeps; range order = event order.  The pre-gated events of a
-// range are cut, in event order, into chunks of kChunk: chunk c occupies
-// [region + c kChunk, region + (c + 1) kChunk) of the range's region in g1idx
-// (offsets, full chunks only) and g2x (refractory survivors, compacted to the
-// chunk's start).  g2x entry = {event - region, isi bits | candidate << 31,
-// w bits, dst}, with isi = (float)(now - lastFired[dst]) >= 0 (its sign bit is
-// free) and w, dst as read at pass start (C1).  chunk_cnt[chunk_slot] =
-// {survivors, candidates} of a full chunk (slots of full chunks never
-// collide; the last chunk's survivors are the range's total minus theirs);
-// range_info[r] = {pre-gated, survivors, candidates, full chunks}.  The last (partial) chunk of a range is processed by its gate wave
-// at the end of its range; full chunks (dense parts of the graph, warm-up
-// passes) are queued for k_refrac so that no wave's stream waits on them.
+// one gate wave sweeps; range order = event order.  Events that pass the LDS
+// filter are staged as {offset, src} and cut, in event order, into chunks of
+// kChunk, each run through the refractory stage by the gate wave itself: a
+// full chunk as soon as it fills (dense parts of the graph, warm-up passes;
+// the adaptive partition gives such ranges fewer events), the range's last
+// chunk once its stream is done.  Chunk c's survivors occupy [region + c
+// kChunk, ...) of g2x.  No atomics anywhere near the stream: a same-address
+// atomic per wave stalls every concurrent stream
+// (profiles/r01n_ubench_soa_atomic.txt).
+//   g2x entry       = {event - region, isi bits | candidate << 31, w bits, dst},
+//                     isi = (float)(now - lastFired[dst]) >= 0 (sign bit free),
+//                     w, dst as read at pass start (C1)
+//   range_info[r]   = {pre-gated, survivors, candidates, full chunks}, whole range
+//   chunk_cnt[slot] = {pre-gated, survivors, candidates, 0} of a full chunk;
+//                     slots of full chunks never collide; the last chunk holds
+//                     the range's survivors minus the full chunks'.
 
 __device__ __forceinline__ uint64_t region_of(const DeviceState& d, uint32_t r)
 {
-    return range_begin(r, d.iters, d.n_ranges) * d.iter_events;
+    return (uint64_t)d.range_bounds[r] * d.iter_events;
 }
 
 __device__ __forceinline__ uint64_t chunk_slot(uint64_t region, uint32_t c)
@@ -264,41 +306,54 @@ __device__ __forceinline__ uint64_t chunk_slot(uint64_t region, uint32_t c)
     return (region + (uint64_t)c * kChunk) / kChunkSlotDiv;
 }
 
-// Refractory stage (brain.metal:79-83, 91-92, 116) of n <= kChunk pre-gated
-// offsets of one chunk, by one wave, in event order: dst and w gathered from
-// the record arrays, the 8-B lastFired[dst] gather, the candidate test; the
-// survivors are written compacted from g2x[base] on.  `rel_at(q)` yields the
-// q-th offset.  Batches of R rounds of 64 keep every load of a lane in flight
-// at once.  Returns {survivors, candidates}.
-template <int R, bool kRandom, class RelAt>
-__device__ __forceinline__ uint2 refrac_chunk(const DeviceState& d, const KernelParams& kp, uint64_t region,
-                                              uint64_t base, uint32_t n, uint64_t now, uint64_t pass,
-                                              RelAt&& rel_at)
+// Counts of a whole range (the gate wave sums its chunks).
+__device__ __forceinline__ uint4 range_totals(const DeviceState& d, uint32_t r) { return d.range_info[r]; }
+
+// Refractory stage of n <= kChunk staged events of one chunk, by one wave, in
+// event order: the exact pre-spike gate on the bitmap word of src
+// (brain.metal:73-77; the filter only pre-selected), then for the events that
+// pass: dst and w gathered from the record arrays, the 8-B lastFired[dst]
+// gather, the refractory gate (brain.metal:79-83), the candidate test
+// (brain.metal:91-92) and isi (brain.metal:116); survivors are written
+// compacted from g2x[base] on.  `at(q)` yields the q-th staged {offset, src}.
+// Batches of R rounds of 64 keep every load of a lane in flight at once.
+// Returns {pre-gated, survivors, candidates, 0}.
+template <int R, bool kRandom, class At>
+__device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const KernelParams& kp, uint64_t region,
+                                              uint64_t base, uint32_t n, uint64_t now, uint64_t pass, At&& at)
 {
     const uint32_t lane = threadIdx.x & 63, nn = (uint32_t)d.n_nrn;
-    uint32_t n_g2 = 0, n_cand = 0;
+    uint32_t n_g1 = 0, n_g2 = 0, n_cand = 0;
     auto record_of = [&](uint32_t rel) -> uint64_t {
         const uint64_t t = region + rel;
         return kRandom ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : t;
     };
     for (uint32_t b0 = 0; b0 < n; b0 += R * 64) {
-        uint32_t rel[R], dst[R];
+        uint32_t rel[R], src[R], bw[R], dst[R];
         float w[R];
         uint64_t ld[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             const uint32_t q = b0 + j * 64 + lane;
-            const bool v = q < n;
-            rel[j] = v ? rel_at(q) : 0u;
-            const uint64_t ri = v ? record_of(rel[j]) : 0;
-            dst[j] = v ? d.syn.dst[ri] : 0xFFFFFFFFu;  // tombstones (dst = 0xFFFFFFFF) never pass
-            w[j] = v ? d.syn.w[ri] : 0.0f;
+            const uint2 e = q < n ? at(q) : make_uint2(0u, 0xFFFFFFFFu);
+            rel[j] = e.x;
+            src[j] = e.y;
+            bw[j] = src[j] < nn ? d.bitmap[src[j] >> 5] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const bool g1 = (bw[j] >> (src[j] & 31u)) & 1u;  // brain.metal:73-77, exact
+            bw[j] = g1;
+            const uint64_t ri = g1 ? record_of(rel[j]) : 0;
+            dst[j] = g1 ? d.syn.dst[ri] : 0xFFFFFFFFu;  // tombstones (dst = 0xFFFFFFFF) never pass
+            w[j] = g1 ? d.syn.w[ri] : 0.0f;
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) ld[j] = dst[j] < nn ? d.last_fired[dst[j]] : 0ull;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             if (b0 + (uint32_t)j * 64 >= n) break;  // wave-uniform
+            n_g1 += (uint32_t)__popcll(__ballot(bw[j] != 0u));
             const bool g2 = dst[j] < nn && (now - ld[j]) > (uint64_t)kp.refractory;  // brain.metal:79-83
             const uint64_t tg = d.syn_offset + region + rel[j];
             const bool cand = g2 && spike_candidate(kp, w[j], tg, now);
@@ -307,14 +362,14 @@ __device__ __forceinline__ uint2 refrac_chunk(const DeviceState& d, const Kernel
                 const uint64_t o = base + n_g2 + mbcnt64(bg);
                 const uint32_t isi = __float_as_uint((float)(now - ld[j])) | (cand ? 0x80000000u : 0u);
                 d.g2x[o] = make_uint4(rel[j], isi, __float_as_uint(w[j]), dst[j]);
-                if (d.g2src) d.g2src[o] = d.syn.src[record_of(rel[j])];  // synaptogenesis keeps src
+                if (d.g2src) d.g2src[o] = src[j];  // synaptogenesis keeps src
                 if (tg == 0) d.work->t0_g2 = 1u;
             }
             n_g2 += (uint32_t)__popcll(bg);
             n_cand += (uint32_t)__popcll(__ballot(cand));
         }
     }
-    return make_uint2(n_g2, n_cand);
+    return make_uint4(n_g1, n_g2, n_cand, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -322,39 +377,46 @@ __device__ __forceinline__ uint2 refrac_chunk(const DeviceState& d, const Kernel
 // contiguous range of events.  The pre-spike gate needs only the src of each
 // record, and the records are held as arrays (SynArrays), so the sweep
 // streams 4 B per event: a wave keeps K events per lane in flight in K VGPRs,
-// each load one coalesced 256-B line segment.  Loads use a wave-uniform base:
-// the arrays are padded by kDummyRecords, so the sweep's last iteration reads
-// past its end instead of masking lanes, and the prefetch after a range's
-// last iteration reads the zero dummy block.  Pre-gated events (~0.2 % in
-// steady state) are staged in LDS as 4-B event offsets; a full chunk goes to
-// g1idx and onto the k_refrac queue, and the range's last chunk is run
-// through the refractory stage by the wave itself once its stream is done.
-// (vmcnt retires in issue order, stores included: a store between the
-// prefetch and its wait delays the whole stream, so chunks are rare.)
+// each load one coalesced 256-B line segment; the next iteration's loads are
+// issued before this one is examined.  Loads use a wave-uniform base: the
+// arrays are padded by kDummyRecords, so the sweep's last iteration reads past
+// its end instead of masking lanes, and the prefetch after a range's last
+// iteration reads the zero dummy block.  Per event: two LDS filter reads and a
+// few VALU ops, no global load; events that pass both filters (~0.7 % at
+// config 3 in steady state, a third of them real) are staged in LDS as
+// {offset, src}; every chunk of them goes through the refractory stage in
+// the wave itself (a full one at once, the last one after the stream).
+// Instruction-issue priority (s_setprio takes an immediate).
+__device__ __forceinline__ void set_priority(uint32_t p)
+{
+    switch (p & 3u) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+
 template <int BLOCK, int K, int FW, bool kTrack, bool kRandom>
-__global__ __launch_bounds__(BLOCK, 4) void k_gate(DeviceState d, KernelParams kp)  // >= 4 waves per SIMD: <= 128 VGPRs
+__global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
     constexpr int NW = BLOCK / 64;
     constexpr uint32_t IE = 64 * K;
     constexpr int KD = kTrack ? K : 1;                 // dst words in flight (track_visits)
+    constexpr uint32_t LG = __builtin_ctz(FW);
+    constexpr uint32_t SE = kChunk + 64;               // a chunk + one k-step
     static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
-    __shared__ uint32_t s_filter[FW];
-    __shared__ uint32_t s_stage[NW][kChunk + 64];      // a chunk + one k-step
+    __shared__ uint32_t s_f1[FW], s_f2[FW];
+    __shared__ uint32_t s_off[NW][SE], s_src[NW][SE];
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wid = wave_uniform(tid >> 6);
     const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
-    const uint64_t it_begin = range_begin(r, d.iters, NR), it_end = range_begin(r + 1, d.iters, NR);
+    const uint64_t it_begin = d.range_bounds[r], it_end = d.range_bounds[r + 1];  // adaptive partition
     const uint64_t region = it_begin * IE;
     const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
-    const bool exact = d.filter_exact != 0;
-    uint32_t* stage = s_stage[wid];
-
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(d.filter);
-        uint4* dst = reinterpret_cast<uint4*>(s_filter);
-        for (int i = tid; i < FW / 4; i += BLOCK) dst[i] = src[i];
-    }
+    uint32_t* st_off = s_off[wid];
+    uint32_t* st_src = s_src[wid];
 
     uint32_t nxs[K], nxd[KD];
     const uint64_t pass = kRandom ? *d.pass_index : 0;
@@ -380,26 +442,37 @@ __global__ __launch_bounds__(BLOCK, 4) void k_gate(DeviceState d, KernelParams k
             }
         }
     };
-    const uint64_t t_start = d.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0;
     issue(it_begin, it_begin < it_end);
+    {
+        const uint4* f = reinterpret_cast<const uint4*>(d.filter);
+        uint4* l1 = reinterpret_cast<uint4*>(s_f1);
+        uint4* l2 = reinterpret_cast<uint4*>(s_f2);
+        for (int i = tid; i < FW / 4; i += BLOCK) {
+            l1[i] = f[i];
+            l2[i] = f[FW / 4 + i];
+        }
+    }
     __syncthreads();
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 
     const uint32_t nn = (uint32_t)d.n_nrn;  // N_NRN < 2^32 (checked at create)
-    uint32_t pend = 0, nch = 0, oslot = 0;
-    // wave-uniform: a full chunk of staged offsets to g1idx and the k_refrac
-    // queue; the (< 64) entries past it move to the front of the stage
+    uint32_t pend = 0, nch = 0;
+    uint4 tot = make_uint4(0u, 0u, 0u, 0u);
+    auto stage_at = [&](uint32_t q) { return make_uint2(st_off[q], st_src[q]); };
+    // wave-uniform: a full chunk through the refractory stage now; the (< 64)
+    // entries past it move to the front of the stage
     auto chunk_out = [&]() {
-        const uint64_t base = region + (uint64_t)nch * kChunk;
-#pragma unroll
-        for (uint32_t q = 0; q < kChunk; q += 64) __builtin_nontemporal_store(stage[q + lane], d.g1idx + base + q + lane);
+        const uint4 c = refrac_chunk<kChunk / 64, kRandom>(d, kp, region, region + (uint64_t)nch * kChunk, kChunk,
+                                                           now, pass, stage_at);
+        if (lane == 0) d.chunk_cnt[chunk_slot(region, nch)] = c;
+        tot.x += c.x;
+        tot.y += c.y;
+        tot.z += c.z;
         const uint32_t rest = pend - kChunk;
-        const uint32_t x = lane < rest ? stage[kChunk + lane] : 0u;
-        if (lane < rest) stage[lane] = x;
-        // queue slot: claimed now, written at the next chunk or the range's
-        // end, so the stream never waits on the atomic's return
-        if (lane == 0) {
-            if (nch > 0) d.ovf[oslot] = make_uint2(r, nch - 1);
-            oslot = atomicAdd(&d.work->n_ovf, 1u);
+        const uint32_t xo = lane < rest ? st_off[kChunk + lane] : 0u, xs = lane < rest ? st_src[kChunk + lane] : 0u;
+        if (lane < rest) {
+            st_off[lane] = xo;
+            st_src[lane] = xs;
         }
         ++nch;
         pend = rest;
@@ -409,8 +482,14 @@ __global__ __launch_bounds__(BLOCK, 4) void k_gate(DeviceState d, KernelParams k
         uint32_t dst[KD];
 #pragma unroll
         for (int k = 0; k < K; ++k) src[k] = nxs[k];
+        // The SIMD arbiter issues strictly by priority, then age: with a fixed
+        // order the last of a SIMD's four waves streams ~15 % slower than the
+        // first.  Rotating every wave through the four ranks every four
+        // iterations equalises them (tools/ubench_soa.hip, profiles/r01p_*).
+        if (((it - it_begin) & 3u) == 0) set_priority((uint32_t)((it - it_begin) >> 2) + wid / 4u);
 #pragma unroll
         for (int k = 0; k < KD; ++k) dst[k] = kTrack ? nxd[k] : 0u;
+        issue(it + 1, it + 1 < it_end);  // next iteration's records in flight first
         const uint64_t base = it * IE;
         uint32_t vmask = (K == 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);  // events of this lane that exist
         if (base + IE > d.events) {  // only the sweep's last iteration
@@ -420,106 +499,109 @@ __global__ __launch_bounds__(BLOCK, 4) void k_gate(DeviceState d, KernelParams k
                 if (base + k * 64 + lane < d.events) vmask |= 1u << k;
         }
 
-        // Pre-spike gate, brain.metal:73-77, first on the LDS filter: all K
-        // reads issued back to back (the word index is masked, so always in
-        // bounds), no branches.
-        uint32_t fw[K];
+        // Pre-spike filter (brain.metal:73-77 pre-selection): both LDS words of
+        // every event read back to back; the word indices are masked, so any
+        // src (tombstones included) stays in bounds.
+        uint32_t f1[K], f2[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) fw[k] = s_filter[(src[k] >> 5) & (FW - 1)];
+        for (int k = 0; k < K; ++k) {
+            f1[k] = s_f1[src[k] >> 5 & (FW - 1)];
+            f2[k] = s_f2[((src[k] >> 5) ^ __umul24(src[k] >> (5 + LG), 0x9E5u)) & (FW - 1)];
+        }
         uint32_t fm = 0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const bool hit = ((fw[k] >> (src[k] & 31u)) & 1u) && src[k] < nn;
-            fm |= (hit ? 1u : 0u) << k;
-        }
+        for (int k = 0; k < K; ++k)
+            fm |= (__builtin_amdgcn_ubfe(f1[k], src[k], 1) & __builtin_amdgcn_ubfe(f2[k], src[k], 1)) << k;
         fm &= vmask;
-        // Filter hits are confirmed on the exact bitmap word (L2-resident);
-        // issued before the next iteration's stream loads.
-        uint32_t cw[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            cw[k] = 0xFFFFFFFFu;
-            if (!exact && ((fm >> k) & 1u)) cw[k] = d.bitmap[src[k] >> 5];
-        }
-        issue(it + 1, it + 1 < it_end);  // next iteration's records in flight
-        // keep every prefetch load ahead of the first use of a confirmation
-        // (otherwise the scheduler interleaves them and waits mid-prefetch)
-        __builtin_amdgcn_sched_barrier(0);
 
         if constexpr (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 if (((vmask >> k) & 1u) && dst[k] < nn) d.last_visited[dst[k]] = now;
         }
-        uint32_t g1m = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            g1m |= ((((fm >> k) & 1u) && ((cw[k] >> (src[k] & 31u)) & 1u)) ? 1u : 0u) << k;
-        if (__ballot(g1m != 0) == 0) continue;  // ~a third of the wave-iterations: nothing to stage
+        if (__ballot(fm != 0) == 0) continue;
         const uint32_t rel = (uint32_t)(base - region);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const bool g1 = (g1m >> k) & 1u;
-            const uint64_t b1 = __ballot(g1);
-            if (g1) stage[pend + mbcnt64(b1)] = rel + k * 64 + lane;
+            const bool h = (fm >> k) & 1u;
+            const uint64_t b1 = __ballot(h);
+            if (h) {
+                const uint32_t q = pend + mbcnt64(b1);
+                st_off[q] = rel + k * 64 + lane;
+                st_src[q] = src[k];
+            }
             pend += (uint32_t)__popcll(b1);
             if (pend >= kChunk) chunk_out();  // a k-step stages at most 64
         }
     }
-    const uint64_t t_stream = d.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t t_stream = __builtin_amdgcn_s_memrealtime();
     // the range's last chunk: refractory stage by this wave
     const uint64_t tb = region + (uint64_t)nch * kChunk;
-    const uint2 c = refrac_chunk<4, kRandom>(d, kp, region, tb, pend, now, pass,
-                                             [&](uint32_t q) { return stage[q]; });
+    const uint4 c = refrac_chunk<kChunk / 64, kRandom>(d, kp, region, tb, pend, now, pass, stage_at);
     if (lane == 0) {
-        if (nch > 0) d.ovf[oslot] = make_uint2(r, nch - 1);
-        d.range_info[r] = make_uint4(nch * kChunk + pend, c.x, c.y, nch);
-        if (d.wave_clock) {  // diagnostics (ABNN_WAVE_CLOCK): 100 MHz wall clock per wave
-            d.wave_clock[4 * r] = t_start;
-            d.wave_clock[4 * r + 1] = t_stream;
-            d.wave_clock[4 * r + 2] = __builtin_amdgcn_s_memrealtime();
-            d.wave_clock[4 * r + 3] = __smid();
-        }
+        d.range_info[r] = make_uint4(tot.x + c.x, tot.y + c.y, tot.z + c.z, nch);
+        // this wave's stream time drives the next pass's partition (k_finalize);
+        // 100 MHz wall clock
+        d.wave_clock[4 * r] = t_start;
+        d.wave_clock[4 * r + 1] = t_stream;
+        d.wave_clock[4 * r + 2] = __builtin_amdgcn_s_memrealtime();
+        d.wave_clock[4 * r + 3] = __smid();
     }
 }
 
-// k_refrac: the queued full chunks (k_gate), one wave per chunk; adds each
-// chunk's counts to its range.
-__global__ __launch_bounds__(256) void k_refrac(DeviceState d, KernelParams kp)
+// ---------------------------------------------------------------------------
+// Work items of the full chunks.  s_cpre[r] = full chunks of the ranges
+// before r (exclusive prefix of range_info[].w, one workgroup, in LDS);
+// item j belongs to the last range r with s_cpre[r] <= j.
+constexpr uint32_t kPrePerThread = kMaxRanges / kApplyThreads;
+
+template <int NT>
+__device__ uint32_t chunk_prefix(const DeviceState& d, uint32_t* s_cpre, uint64_t* s_red)
 {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = wave_uniform((blockIdx.x * 256 + threadIdx.x) >> 6), nwaves = gridDim.x * 4;
-    const uint64_t now = *d.clock, pass = *d.pass_index;
-    const uint32_t n = d.work->n_ovf;
-    for (uint32_t i = wave; i < n; i += nwaves) {
-        const uint2 q = d.ovf[i];
-        const uint64_t region = region_of(d, q.x), base = region + (uint64_t)q.y * kChunk;
-        const uint32_t* rel = d.g1idx + base;
-        const uint2 c = d.mode == ABNN_MODE_RANDOM
-            ? refrac_chunk<kChunk / 64, true>(d, kp, region, base, kChunk, now, pass, [&](uint32_t j) { return rel[j]; })
-            : refrac_chunk<kChunk / 64, false>(d, kp, region, base, kChunk, now, pass, [&](uint32_t j) { return rel[j]; });
-        if (lane == 0) {
-            d.chunk_cnt[chunk_slot(region, q.y)] = c;
-            atomicAdd(&d.range_info[q.x].y, c.x);
-            atomicAdd(&d.range_info[q.x].z, c.y);
-        }
+    const uint32_t NR = d.n_ranges, per = (NR + NT - 1) / NT, q0 = threadIdx.x * per;
+    uint32_t c[kMaxRanges / NT];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kMaxRanges / NT; ++j) {
+        c[j] = (j < per && q0 + j < NR) ? d.range_info[q0 + j].w : 0u;
+        sum += c[j];
     }
+    uint64_t tot;
+    uint32_t run = (uint32_t)block_exclusive_scan<NT>(sum, &tot, s_red);
+#pragma unroll
+    for (uint32_t j = 0; j < kMaxRanges / NT; ++j) {
+        if (j < per && q0 + j < NR) s_cpre[q0 + j] = run;
+        run += c[j];
+    }
+    __syncthreads();
+    return (uint32_t)tot;
+}
+
+__device__ __forceinline__ uint32_t chunk_range(const uint32_t* s_cpre, uint32_t NR, uint32_t j)
+{
+    uint32_t lo = 0, hi = NR;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_cpre[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    return lo;
 }
 
 // ---------------------------------------------------------------------------
 // The ordered spike budget of schedule C1 (brain.metal:85-98 without its
 // races): an event that passed both gates is updated iff fewer than
 // max_spikes spike candidates precede it in global event order.  Walked by
-// k_spikes, k_claim and k_apply alike.  Every workgroup first builds the
-// capped exclusive candidate prefix of all ranges in LDS (a few KB read from
-// L2; cheaper than a separate single-workgroup scan launch).  The work items
-// are the last chunk of every range and every queued full chunk, one per wave
-// at a time: an item adds the candidates of its range's lower full chunks,
-// leaves at once if the budget is spent, and otherwise visits its (<= kChunk)
-// survivors in event order, calling f(region, entry, candidate, budget
-// position, g2x index) for each one whose position is below the budget.
+// k_spikes, k_claim and k_apply alike.  Every workgroup first builds, in LDS,
+// the capped exclusive candidate prefix of all ranges and the full-chunk
+// prefix (a few KB read from L2; cheaper than a separate single-workgroup scan
+// launch).  The work items are the last chunk of every range and every full
+// chunk, one per wave at a time: an item adds the candidates of its range's
+// lower full chunks, leaves at once if the budget is spent, and otherwise
+// visits its (<= kChunk) survivors in event order, calling f(region, entry,
+// candidate, budget position, g2x index) for each one whose position is below
+// the budget.
 constexpr uint32_t kWalkWaves = kApplyThreads / 64;
-constexpr uint32_t kPrePerThread = kMaxRanges / kApplyThreads;
 
 // s_pre[r] = min(off + candidates of ranges < r, budget), r < n_ranges.
 __device__ void range_prefix(const DeviceState& d, uint64_t off, uint64_t budget, uint32_t* s_pre, uint64_t* s_red)
@@ -529,11 +611,11 @@ __device__ void range_prefix(const DeviceState& d, uint64_t off, uint64_t budget
     uint64_t sum = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kPrePerThread; ++j) {
-        c[j] = (j < per && q0 + j < NR) ? d.range_info[q0 + j].z : 0u;
+        c[j] = (j < per && q0 + j < NR) ? range_totals(d, q0 + j).z : 0u;
         sum += c[j];
     }
     uint64_t tot;
-    uint64_t run = off + block_exclusive_scan(sum, &tot, s_red);
+    uint64_t run = off + block_exclusive_scan<kApplyThreads>(sum, &tot, s_red);
 #pragma unroll
     for (uint32_t j = 0; j < kPrePerThread; ++j) {
         if (j < per && q0 + j < NR) s_pre[q0 + j] = (uint32_t)(run < budget ? run : budget);
@@ -543,38 +625,39 @@ __device__ void range_prefix(const DeviceState& d, uint64_t off, uint64_t budget
 }
 
 template <class F>
-__device__ void budget_walk(const DeviceState& d, uint64_t off, uint64_t budget, uint32_t* s_pre, uint64_t* s_red,
+__device__ void budget_walk(const DeviceState& d, uint64_t off, uint64_t budget, uint32_t* s_lds, uint64_t* s_red,
                             F&& f)
 {
+    const uint32_t NR = d.n_ranges;
+    uint32_t* s_pre = s_lds;
+    uint32_t* s_cpre = s_lds + NR;
     range_prefix(d, off, budget, s_pre, s_red);
+    const uint32_t items = NR + chunk_prefix<kApplyThreads>(d, s_cpre, s_red);
     const uint32_t lane = threadIdx.x & 63, w = wave_uniform(threadIdx.x >> 6);
-    const uint32_t NR = d.n_ranges, items = NR + d.work->n_ovf;
     for (uint32_t i = blockIdx.x * kWalkWaves + w; i < items; i += gridDim.x * kWalkWaves) {
         uint32_t r, c;
         if (i < NR) {
             r = i;
             c = d.range_info[r].w;  // the last chunk follows the full ones
         } else {
-            const uint2 q = d.ovf[i - NR];
-            r = q.x;
-            c = q.y;
+            r = chunk_range(s_cpre, NR, i - NR);
+            c = i - NR - s_cpre[r];
         }
         uint64_t P = s_pre[r];
         if (P >= budget) continue;
-        const uint4 ri = d.range_info[r];
         const uint64_t region = region_of(d, r);
-        const bool last = c == ri.w;
         uint32_t cl = 0, gl = 0;  // candidates / survivors of the lower full chunks
         for (uint32_t c0 = 0; c0 < c; c0 += 64)
             if (c0 + lane < c) {
-                const uint2 cc = d.chunk_cnt[chunk_slot(region, c0 + lane)];
-                cl += cc.y;
-                gl += cc.x;
+                const uint4 x = d.chunk_cnt[chunk_slot(region, c0 + lane)];
+                cl += x.z;
+                gl += x.y;
             }
         P += wave_sum(cl);
         if (P >= budget) continue;
+        const uint4 ri = d.range_info[r];
         // survivors of this chunk: the last one holds what the full ones do not
-        const uint32_t n = last ? ri.y - wave_sum(gl) : d.chunk_cnt[chunk_slot(region, c)].x;
+        const uint32_t n = c == ri.w ? ri.y - wave_sum(gl) : d.chunk_cnt[chunk_slot(region, c)].y;
         const uint64_t base = region + (uint64_t)c * kChunk;
         constexpr uint32_t RW = kChunk / 64;
         uint4 e[RW];
@@ -613,7 +696,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelPara
     int64_t* summary_out = reinterpret_cast<int64_t*>(xchg_out);
     uint64_t c = 0, g = 0;
     for (uint32_t q = threadIdx.x; q < d.n_ranges; q += kScanThreads) {
-        const uint4 ri = d.range_info[q];
+        const uint4 ri = range_totals(d, q);
         c += ri.z;
         g += ri.y;
     }
@@ -680,7 +763,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     __shared__ uint64_t s_red[kWalkWaves];
     __shared__ uint32_t s_u[kWalkWaves], s_f[kWalkWaves], s_p[kWalkWaves];
     // every gate workgroup has its copy of the filter image: zero it for the next k_bitmap
-    for (uint32_t i = blockIdx.x * kApplyThreads + threadIdx.x; i < d.filter_words; i += gridDim.x * kApplyThreads)
+    for (uint32_t i = blockIdx.x * kApplyThreads + threadIdx.x; i < 2 * d.filter_words; i += gridDim.x * kApplyThreads)
         d.filter[i] = 0u;
     const float R = *d.reward, rb = *d.rbar;  // pass-start values (C1), brain.metal:105-106
     const uint64_t now = *d.clock, pass = *d.pass_index;
@@ -746,14 +829,65 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
 // k_finalize: rBar (brain.metal:110-113), clock tick (brain.metal:129),
 // statistics; in sharded passes also the deferred stamps of every rank's
 // spikes from the gathered exchange records (brain.metal:125-126).  One
-// workgroup.
+// workgroup; every global load is issued up front (the kernel is a chain of
+// round trips otherwise).
+//
+// It also sets the next pass's sweep partition.  Equal ranges do not finish
+// together: a wave's stream rate depends on its age rank on its SIMD (the
+// oldest of four waves per SIMD streams ~20 % faster than the youngest,
+// profiles/r01o_wave_slots.txt) and dense parts of the graph stage more
+// events.  So range r's measured gate time (wave_clock), spread evenly over its
+// iterations, gives a cumulative cost curve, and boundary k moves halfway from
+// its old place towards the iteration where the curve reaches k / NR of the
+// total.  Results do not depend on the partition (event order is global, C1).
 __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, KernelParams kp,
                                                            const int32_t* gathered, uint32_t world)
 {
-    constexpr uint32_t kU = 4;
-    const uint32_t tid = threadIdx.x, words = xchg_words(kp.max_spikes);
+    extern __shared__ uint32_t s_lds[];
+    constexpr uint32_t NWv = kScanThreads / 64, kU = 4, kRound = 4;
+    __shared__ uint32_t s_w[6][NWv];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, words = xchg_words(kp.max_spikes);
+    const uint32_t NR = d.n_ranges;
+    uint64_t* fin_clock = d.wave_clock + 4 * (uint64_t)kMaxRanges;  // diagnostics: phase times
+    if (tid == 0) fin_clock[0] = __builtin_amdgcn_s_memrealtime();
     const uint64_t now = *d.clock;
     const uint64_t budget = kp.max_spikes;
+    // ---- loads, all issued before any is used: ranges (counts, bounds, wave
+    // times; kRound consecutive ranges per thread per round), apply partials
+    const uint32_t per = (NR + kScanThreads - 1) / kScanThreads, q0 = tid * per;
+    uint32_t g1 = 0, g2 = 0, csum = 0;
+    uint32_t rb[kMaxRanges / kScanThreads], cost[kMaxRanges / kScanThreads];
+    for (uint32_t j0 = 0; j0 < per; j0 += kRound) {
+        uint4 ri[kRound];
+        uint32_t b0[kRound], b1[kRound];
+        uint64_t ts[kRound], te[kRound];
+#pragma unroll
+        for (uint32_t u = 0; u < kRound; ++u) {
+            const uint32_t q = min(q0 + j0 + u, NR - 1);  // clamped: loads never depend on a branch
+            ri[u] = range_totals(d, q);
+            b0[u] = d.range_bounds[q];
+            b1[u] = d.range_bounds[q + 1];
+            ts[u] = d.wave_clock[4 * q];
+            te[u] = d.wave_clock[4 * q + 2];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kRound; ++u) {
+            const uint32_t j = j0 + u;
+            const bool in = j < per && q0 + j < NR;
+            // gate time of the range in 40-ns units, clamped (<= 2.6 ms)
+            const uint64_t t = (te[u] - ts[u]) >> 2;
+            const uint32_t c = in && b1[u] > b0[u] ? (uint32_t)(t < 1 ? 1 : (t > 0xFFFFu ? 0xFFFFu : t)) : 0u;
+            if (j < kMaxRanges / kScanThreads) {
+                rb[j] = b0[u];
+                cost[j] = c;
+            }
+            g1 += in ? ri[u].x : 0u;
+            g2 += in ? ri[u].y : 0u;
+            csum += c;
+        }
+    }
+    uint4 ap = make_uint4(0u, 0u, 0u, 0u);
+    if (tid < kWalkBlocks) ap = d.apply_partial[tid];
     uint64_t events = d.events, off = 0;
     int64_t t0 = d.work->t0_g2;
     if (gathered) {
@@ -780,59 +914,79 @@ __global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, Kernel
             off += n;
         }
     }
-    uint64_t g1 = 0, g2 = 0;
-    for (uint32_t q = tid; q < d.n_ranges; q += kScanThreads) {
-        const uint4 ri = d.range_info[q];
-        g1 += ri.x;
-        g2 += ri.y;
+    if (tid == 0) fin_clock[1] = __builtin_amdgcn_s_memrealtime();
+    // ---- one barrier round on DPP: the cost scan and the statistics sums
+    // (u32: per-pass counts of one rank stay below 2^32, costs below 2^30)
+    const uint32_t cin = wave_incl_scan(csum);
+    const uint32_t v[6] = {(uint32_t)__builtin_amdgcn_readlane((int)cin, 63), wave_total(g1), wave_total(g2),
+                           wave_total(ap.x), wave_total(ap.y), wave_total(ap.z)};
+    if (lane == 0)
+        for (int i = 0; i < 6; ++i) s_w[i][wv] = v[i];
+    __syncthreads();
+    uint32_t before = 0, t[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t w = 0; w < NWv; ++w) {
+        before += w < wv ? s_w[0][w] : 0u;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) t[i] += s_w[i][w];
     }
-    uint32_t upd = 0, nf = 0, npr = 0;
-    if (tid < kWalkBlocks) {
-        const uint4 v = d.apply_partial[tid];
-        upd = v.x;
-        nf = v.y;
-        npr = v.z;
+    const uint32_t total_cost = t[0];
+    uint32_t* s_cc = s_lds;           // [NR + 1] exclusive cumulative cost
+    uint32_t* s_rb = s_lds + NR + 1;  // [NR + 1] current bounds
+    uint32_t run = before + cin - csum;
+#pragma unroll
+    for (uint32_t j = 0; j < kMaxRanges / kScanThreads; ++j) {
+        if (j < per && q0 + j < NR) {
+            s_cc[q0 + j] = run;
+            s_rb[q0 + j] = rb[j];
+            run += cost[j];
+        }
     }
-    __shared__ uint64_t s_a[kScanThreads / 64], s_b[kScanThreads / 64];
-    __shared__ uint32_t s_u[kScanThreads / 64], s_f[kScanThreads / 64], s_p[kScanThreads / 64];
-    g1 = wave_sum(g1);
-    g2 = wave_sum(g2);
-    upd = wave_sum(upd);
-    nf = wave_sum(nf);
-    npr = wave_sum(npr);
-    if ((tid & 63) == 0) {
-        s_a[tid >> 6] = g1;
-        s_b[tid >> 6] = g2;
-        s_u[tid >> 6] = upd;
-        s_f[tid >> 6] = nf;
-        s_p[tid >> 6] = npr;
+    if (tid == 0) {
+        s_cc[NR] = total_cost;
+        s_rb[NR] = d.iters;
     }
     __syncthreads();
+    if (tid == 0) fin_clock[2] = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) {
-        uint64_t ta = 0, tb = 0, tu = 0, tf = 0, tp = 0;
-        for (int w = 0; w < kScanThreads / 64; ++w) {
-            ta += s_a[w];
-            tb += s_b[w];
-            tu += s_u[w];
-            tf += s_f[w];
-            tp += s_p[w];
-        }
-        const float R = *d.reward, rb = *d.rbar;
-        if (t0 != 0 && budget > 0)
-            *d.rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
-        if (events > 0) *d.clock = now + kp.clock_inc; // brain.metal:129
-        *d.pass_index += 1;
+        // every load before every store (the pointers may alias as far as the
+        // compiler knows: interleaved, each read-modify-write is a round trip)
+        const float R = *d.reward, rbar = *d.rbar;
+        const uint64_t pi = *d.pass_index;
         PassWork* w = d.work;
+        abnn_stats st = w->stats;
+        st.passes += 1;
+        st.events += d.events;
+        st.pre_gated += t[1];
+        st.post_gated += t[2];
+        st.updated += t[3];
+        st.fired += t[4];
+        st.pruned += t[5];
+        if (t0 != 0 && budget > 0)
+            *d.rbar = rbar + kp.alpha_rbar * (R - rbar);  // brain.metal:110-113
+        if (events > 0) *d.clock = now + kp.clock_inc;     // brain.metal:129
+        *d.pass_index = pi + 1;
         w->t0_g2 = 0;  // re-armed for the next pass
-        w->n_ovf = 0;
-        w->stats.passes += 1;
-        w->stats.events += d.events;
-        w->stats.pre_gated += ta;
-        w->stats.post_gated += tb;
-        w->stats.updated += tu;
-        w->stats.fired += tf;
-        w->stats.pruned += tp;
+        w->stats = st;
+        fin_clock[3] = __builtin_amdgcn_s_memrealtime();
     }
+    // ---- the next pass's partition
+    if (!d.adapt_ranges || NR < 2 || total_cost == 0) return;
+    for (uint32_t k = tid + 1; k < NR; k += kScanThreads) {
+        const uint32_t T = (uint32_t)((uint64_t)k * total_cost / NR);
+        uint32_t lo = 0, hi = NR;  // last range with s_cc <= T (its cost is > 0)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_cc[mid] <= T) lo = mid;
+            else hi = mid;
+        }
+        // integer floors keep the bounds monotonic in k (ranges never overlap)
+        const uint32_t cr = s_cc[lo + 1] - s_cc[lo];
+        const uint32_t target =
+            s_rb[lo] + (cr ? (uint32_t)((uint64_t)(T - s_cc[lo]) * (s_rb[lo + 1] - s_rb[lo]) / cr) : 0u);
+        d.range_bounds[k] = (target + s_rb[k]) >> 1;
+    }
+    if (tid == 0) fin_clock[4] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------------------
@@ -940,8 +1094,8 @@ __global__ __launch_bounds__(256) void k_stamp_list(DeviceState d, const uint32_
 
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
-// budget walks: s_pre holds one u32 per range
-inline size_t walk_lds(const DeviceState& d) { return (size_t)std::max(1u, d.n_ranges) * 4; }
+// budget walks: the candidate and full-chunk prefixes, one u32 each per range
+inline size_t walk_lds(const DeviceState& d) { return (size_t)std::max(1u, d.n_ranges) * 8; }
 
 template <int BLOCK, int K, int FW>
 hipError_t launch_gate_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
@@ -974,18 +1128,12 @@ int occupancy_shape(bool track, bool random)
 
 // Compiled gate shapes: threads per workgroup x events per lane x filter words.
 #define ABNN_GATE_SHAPES(X) \
-    X(512, 8, 16384)        \
-    X(512, 16, 16384)       \
-    X(512, 4, 16384)        \
+    X(1024, 8, 8192)        \
+    X(1024, 16, 8192)       \
     X(512, 8, 8192)         \
     X(512, 16, 8192)        \
-    X(1024, 8, 8192)        \
-    X(1024, 4, 8192)        \
-    X(256, 16, 8192)        \
-    X(256, 8, 8192)         \
-    X(512, 32, 8192)        \
-    X(256, 32, 8192)        \
-    X(1024, 16, 8192)
+    X(512, 8, 16384)        \
+    X(256, 16, 8192)
 
 constexpr uint64_t shape_key(uint32_t b, uint32_t k, uint32_t fw) { return ((uint64_t)b << 40) | ((uint64_t)k << 32) | fw; }
 
@@ -1017,12 +1165,6 @@ hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t 
     if (d.n_nrn == 0) return hipSuccess;
     hipLaunchKernelGGL(k_bitmap, dim3((uint32_t)((d.n_nrn + 1023) / 1024)), dim3(256), 0, s, d, kp,
                        stim_first, stim_count);
-    return hipGetLastError();
-}
-
-hipError_t launch_refrac(const DeviceState& d, const KernelParams& kp, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_refrac, dim3(kRefracBlocks), dim3(256), 0, s, d, kp);
     return hipGetLastError();
 }
 
@@ -1064,7 +1206,8 @@ hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int3
 hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
                            uint32_t world, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kScanThreads), 0, s, d, kp, gathered, world);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kScanThreads), (size_t)(d.n_ranges + 1) * 8, s, d, kp, gathered,
+                       world);
     return hipGetLastError();
 }
 

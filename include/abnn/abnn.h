@@ -297,10 +297,12 @@ abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t 
 /* ---- statistics / timing ---------------------------------------------------- */
 abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out);   /* synchronises */
 abnn_status abnn_reset_stats(abnn_brain* b);
-/* When on, every pass records HIP events around the gate (streaming) kernel on
- * the stream it is launched on; abnn_get_kernel_time returns the summed
- * milliseconds and the launch count since the last reset.                  */
-abnn_status abnn_enable_timing(abnn_brain* b, int on);
+/* every > 0: every `every`-th pass records HIP events around the gate
+ * (streaming) kernel on the stream it is launched on (an event pair costs
+ * ~11 us of stream time per pass, so sampling keeps it out of the rate);
+ * 0: off.  abnn_get_kernel_time returns the summed milliseconds and the count
+ * of timed launches since the last call.                                    */
+abnn_status abnn_enable_timing(abnn_brain* b, int every);
 abnn_status abnn_get_kernel_time(abnn_brain* b, double* ms_total, uint64_t* launches);
 
 /* ---- persistence ------------------------------------------------------------

@@ -31,7 +31,18 @@
 enum { F_FILTER = 1, F_CONFIRM = 2, F_LOOP = 4, F_BLOOM = 8, F_STAGE = 16, F_EARLY = 32, F_OPT = 64,
        F_SEQ = 128 /* conflict-free LDS addresses */, F_BCAST = 256 /* one LDS address */,
        F_NOCOPY = 512 /* filter not loaded into LDS */, F_NOLOOK = 1024 /* copy only, no lookups */,
-       F_GUARD = 2048 /* no prefetch past the range */, F_NOSYNC = 4096, F_NOATOM = 8192 };
+       F_GUARD = 2048 /* no prefetch past the range */, F_NOSYNC = 4096, F_NOATOM = 8192,
+       F_PRIO = 16384 /* s_setprio: younger waves of a SIMD get higher issue priority */,
+       F_ROT = 32768 /* priority rotates with the iteration count: every wave spends equal time at every rank */ };
+__device__ __forceinline__ void setprio_rt(uint32_t p)
+{
+    switch (p & 3) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
 constexpr uint32_t N_NRN = 5000512;
 
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
@@ -40,7 +51,7 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
 }
 __host__ __device__ __forceinline__ uint32_t hash2(uint32_t x) { return (x * 0x9E3779B1u) >> 17; }  // 15 high bits
 
-template <int BLOCK, int K, int FW, int FLAGS>
+template <int BLOCK, int K, int FW, int FLAGS, int PM = 0xE4 /* prio per age group, 2 bits each */, int ROTM = 7>
 __global__ __launch_bounds__(BLOCK) void k_var(const uint32_t* src, uint64_t events, uint32_t iters,
                                                const uint32_t* bitmap, const uint32_t* filt, const uint32_t* filt2,
                                                uint32_t* tot, uint64_t* clk)
@@ -90,6 +101,13 @@ __global__ __launch_bounds__(BLOCK) void k_var(const uint32_t* src, uint64_t eve
             __builtin_amdgcn_sched_barrier(0);  // keep ascending address order
         }
     };
+    if (FLAGS & F_PRIO) {
+        const uint32_t age = wid / 4 > 3 ? 3 : wid / 4;  // waves of a workgroup go round-robin over the 4 SIMDs
+        const uint32_t pr = (PM >> (2 * age)) & 3;
+        if (pr == 1) __builtin_amdgcn_s_setprio(1);
+        if (pr == 2) __builtin_amdgcn_s_setprio(2);
+        if (pr == 3) __builtin_amdgcn_s_setprio(3);
+    }
     issue(itb);
     if (!(FLAGS & F_NOSYNC)) __syncthreads();
     uint32_t acc = 0, pend = 0;
@@ -97,6 +115,7 @@ __global__ __launch_bounds__(BLOCK) void k_var(const uint32_t* src, uint64_t eve
         uint32_t s[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) s[k] = nx[k];
+        if ((FLAGS & F_ROT) && ((it - itb) & ROTM) == 0) setprio_rt((uint32_t)((it - itb) / (ROTM + 1)) + wid / 4);
         if (FLAGS & F_EARLY) issue(it + 1);
         if (!(FLAGS & (F_FILTER | F_BLOOM)) || (FLAGS & F_NOLOOK)) {
             if (!(FLAGS & F_EARLY)) issue(it + 1);
@@ -225,11 +244,11 @@ __global__ void k_fill(uint32_t* src, uint64_t n, uint64_t seed)
 
 typedef void (*Fn)(const uint32_t*, uint64_t, uint32_t, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t*,
                    uint64_t*, int);
-template <int B, int K, int FW, int FL>
+template <int B, int K, int FW, int FL, int PM = 0xE4, int ROTM = 7>
 void run(const uint32_t* s, uint64_t e, uint32_t it, const uint32_t* bm, const uint32_t* f, const uint32_t* f2,
          uint32_t* t, uint64_t* c, int grid)
 {
-    hipLaunchKernelGGL((k_var<B, K, FW, FL>), dim3(grid), dim3(B), 0, 0, s, e, it, bm, f, f2, t, c);
+    hipLaunchKernelGGL((k_var<B, K, FW, FL, PM, ROTM>), dim3(grid), dim3(B), 0, 0, s, e, it, bm, f, f2, t, c);
 }
 
 int main(int argc, char** argv)
@@ -267,48 +286,15 @@ int main(int argc, char** argv)
     int cus = 256;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     struct V { const char* name; Fn fn; int block, k, fw, per_cu; };
+    constexpr int BOGF = F_BLOOM | F_EARLY | F_OPT | F_STAGE | F_GUARD;
     std::vector<V> vs = {
-        {"S  512x8", run<512, 8, 8192, 0>, 512, 8, 8192, 2},
-        {"FO 512x8 f32", run<512, 8, 8192, F_FILTER | F_EARLY | F_OPT>, 512, 8, 8192, 2},
-        {"FOseq 512x8", run<512, 8, 8192, F_FILTER | F_EARLY | F_OPT | F_SEQ>, 512, 8, 8192, 2},
-        {"FOnocopy 512x8", run<512, 8, 8192, F_FILTER | F_EARLY | F_OPT | F_NOCOPY>, 512, 8, 8192, 2},
-        {"Fcopy-nolook", run<512, 8, 8192, F_FILTER | F_EARLY | F_NOLOOK>, 512, 8, 8192, 2},
-        {"Gen-nolds", run<512, 8, 8192, F_EARLY>, 512, 8, 8192, 2},
-        {"Gen guard", run<512, 8, 8192, F_EARLY | F_GUARD>, 512, 8, 8192, 2},
-        {"Gen nosync", run<512, 8, 8192, F_EARLY | F_NOSYNC>, 512, 8, 8192, 2},
-        {"Gen noatom", run<512, 8, 8192, F_EARLY | F_NOATOM>, 512, 8, 8192, 2},
-        {"Gen all3", run<512, 8, 8192, F_EARLY | F_GUARD | F_NOSYNC | F_NOATOM>, 512, 8, 8192, 2},
-        {"FO all3", run<512, 8, 8192, F_FILTER | F_EARLY | F_OPT | F_GUARD | F_NOATOM>, 512, 8, 8192, 2},
-        {"FObc 512x8", run<512, 8, 8192, F_FILTER | F_EARLY | F_OPT | F_BCAST>, 512, 8, 8192, 2},
-        {"FO 256x8 f32", run<256, 8, 8192, F_FILTER | F_EARLY | F_OPT>, 256, 8, 8192, 4},
-        {"FO 512x4 f32", run<512, 4, 8192, F_FILTER | F_EARLY | F_OPT>, 512, 4, 8192, 2},
-        {"FO 512x8 f8", run<512, 8, 2048, F_FILTER | F_EARLY | F_OPT>, 512, 8, 2048, 2},
-        {"FOG 512x8 f32", run<512, 8, 8192, F_FILTER | F_EARLY | F_OPT | F_STAGE>, 512, 8, 8192, 2},
-        {"FOG 1024x8 f128", run<1024, 8, 32768, F_FILTER | F_EARLY | F_OPT | F_STAGE>, 1024, 8, 32768, 1},
-        {"BO 512x8 2x32", run<512, 8, 8192, F_BLOOM | F_EARLY | F_OPT>, 512, 8, 8192, 2},
-        {"BOG 512x8 2x32", run<512, 8, 8192, F_BLOOM | F_EARLY | F_OPT | F_STAGE>, 512, 8, 8192, 2},
-        {"BOG 1024x8 2x64", run<1024, 8, 16384, F_BLOOM | F_EARLY | F_OPT | F_STAGE>, 1024, 8, 16384, 1},
-        {"BOG 1024x16 2x64", run<1024, 16, 16384, F_BLOOM | F_EARLY | F_OPT | F_STAGE>, 1024, 16, 16384, 1},
-        {"FE 512x8 f32", run<512, 8, 8192, F_FILTER | F_EARLY>, 512, 8, 8192, 2},
-        {"BE 512x8 2x32", run<512, 8, 8192, F_BLOOM | F_EARLY>, 512, 8, 8192, 2},
-        {"BEG 512x8 2x32", run<512, 8, 8192, F_BLOOM | F_EARLY | F_STAGE>, 512, 8, 8192, 2},
-        {"BEG 512x16 2x32", run<512, 16, 8192, F_BLOOM | F_EARLY | F_STAGE>, 512, 16, 8192, 2},
-        {"BEG 1024x8 2x64", run<1024, 8, 16384, F_BLOOM | F_EARLY | F_STAGE>, 1024, 8, 16384, 1},
-        {"CEG 512x8 f32", run<512, 8, 8192, F_FILTER | F_CONFIRM | F_EARLY | F_STAGE>, 512, 8, 8192, 2},
-        {"F  512x8 f32", run<512, 8, 8192, F_FILTER>, 512, 8, 8192, 2},
-        {"C  512x8 f32", run<512, 8, 8192, F_FILTER | F_CONFIRM>, 512, 8, 8192, 2},
-        {"CG 512x8 f32", run<512, 8, 8192, F_FILTER | F_CONFIRM | F_STAGE>, 512, 8, 8192, 2},
-        {"L  512x8 f32", run<512, 8, 8192, F_FILTER | F_LOOP>, 512, 8, 8192, 2},
-        {"LG 512x8 f32", run<512, 8, 8192, F_FILTER | F_LOOP | F_STAGE>, 512, 8, 8192, 2},
-        {"B  512x8 2x32", run<512, 8, 8192, F_BLOOM>, 512, 8, 8192, 2},
-        {"BC 512x8 2x32", run<512, 8, 8192, F_BLOOM | F_CONFIRM>, 512, 8, 8192, 2},
-        {"BCG 512x8 2x32", run<512, 8, 8192, F_BLOOM | F_CONFIRM | F_STAGE>, 512, 8, 8192, 2},
-        {"BLG 512x8 2x32", run<512, 8, 8192, F_BLOOM | F_LOOP | F_STAGE>, 512, 8, 8192, 2},
-        {"CG 512x8 f64", run<512, 8, 16384, F_FILTER | F_CONFIRM | F_STAGE>, 512, 8, 16384, 2},
-        {"CG 1024x8 f128", run<1024, 8, 32768, F_FILTER | F_CONFIRM | F_STAGE>, 1024, 8, 32768, 1},
         {"S  1024x8", run<1024, 8, 8192, 0>, 1024, 8, 8192, 1},
-        {"S  512x16", run<512, 16, 8192, 0>, 512, 16, 8192, 2},
-        {"CG 512x16 f32", run<512, 16, 8192, F_FILTER | F_CONFIRM | F_STAGE>, 512, 16, 8192, 2},
+        {"BOG 1024x8", run<1024, 8, 8192, BOGF>, 1024, 8, 8192, 1},
+        {"BOG prio 0123", run<1024, 8, 8192, BOGF | F_PRIO, 0xE4>, 1024, 8, 8192, 1},
+        {"BOG rot 1", run<1024, 8, 8192, BOGF | F_ROT, 0, 0>, 1024, 8, 8192, 1},
+        {"BOG rot 4", run<1024, 8, 8192, BOGF | F_ROT, 0, 3>, 1024, 8, 8192, 1},
+        {"BOG rot 8", run<1024, 8, 8192, BOGF | F_ROT, 0, 7>, 1024, 8, 8192, 1},
+        {"BOG rot 16", run<1024, 8, 8192, BOGF | F_ROT, 0, 15>, 1024, 8, 8192, 1},
     };
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -337,13 +323,22 @@ int main(int argc, char** argv)
         }
         const int nw = grid * v.block / 64;
         CK(hipMemcpy(hc.data(), clk, nw * 8, hipMemcpyDeviceToHost));
-        std::vector<double> d(nw);
-        for (int i = 0; i < nw; ++i) d[i] = hc[i] * 0.01;
+        std::vector<double> d(nw), gm(4, 0.0);
+        std::vector<int> gn(4, 0);
+        const int NWb = v.block / 64;
+        for (int i = 0; i < nw; ++i) {
+            d[i] = hc[i] * 0.01;
+            const int g = std::min(3, (i % NWb) / 4);
+            gm[g] += d[i];
+            gn[g]++;
+        }
         std::sort(d.begin(), d.end());
         std::sort(t.begin(), t.end());
         printf("%-16s median %.4f ms  (%.0f GB/s)  wave us p10 %.1f p50 %.1f p90 %.1f max %.1f  count %u\n", v.name,
                t[t.size() / 2], E * 4.0 / (t[t.size() / 2] * 1e-3) / 1e9, d[nw / 10], d[nw / 2], d[nw * 9 / 10],
                d[nw - 1], ht[1] / 2);
+        printf("    age-group mean us: %.1f %.1f %.1f %.1f\n", gn[0] ? gm[0] / gn[0] : 0, gn[1] ? gm[1] / gn[1] : 0,
+               gn[2] ? gm[2] / gn[2] : 0, gn[3] ? gm[3] / gn[3] : 0);
     }
     return 0;
 }

@@ -25,12 +25,14 @@ for p in range(passes):
     b.encode_traversal(1)
     b.synchronize()
     nr = 16384
-    buf = np.zeros(4 * nr, dtype=np.uint64)
+    buf = np.zeros(4 * nr + 16, dtype=np.uint64)
     f = b._lib.abnn_debug_wave_clock
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     f.restype = ctypes.c_int
     assert f(b._h, buf.ctypes.data, buf.size) == 0
-    w = buf.reshape(-1, 4)
+    fin = buf[4 * nr:4 * nr + 5].astype(np.int64)
+    print("  k_finalize phases (us):", ((fin[1:] - fin[0]) * 0.01).round(2).tolist())
+    w = buf[:4 * nr].reshape(-1, 4)
     w = w[w[:, 0] > 0]
     t0 = w[:, 0].min()
     st, se, en = (w[:, 0] - t0) * 10e-3, (w[:, 1] - t0) * 10e-3, (w[:, 2] - t0) * 10e-3  # us
@@ -42,6 +44,16 @@ for p in range(passes):
     print(f"  stream dur  {q(se - st)}")
     print(f"  tail dur    {q(en - se)}")
     np.save(os.path.join(os.environ.get("OUT", "gpurun_out"), f"wave_clock_p{p}.npy"), buf.reshape(-1, 4)[:len(w)])
+    rb = np.zeros(len(w) + 1, dtype=np.uint32)
+    g = b._lib.abnn_debug_range_bounds
+    g.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    g.restype = ctypes.c_int
+    assert g(b._h, rb.ctypes.data, rb.size) == 0
+    ln = np.diff(rb.astype(np.int64))  # bounds for the NEXT pass
+    wid = np.arange(len(w)) % 16
+    print("  next lengths r0..11:", ln[:12].tolist(), " per age group mean len:",
+          [round(float(ln[(wid // 4) == a].mean()), 1) for a in range(4)],
+          " per age group mean end:", [round(float(en[(wid // 4) == a].mean()), 1) for a in range(4)])
     late = np.argsort(en)[-6:]
     print("  latest waves (range: start/stream-end/end us):",
           "  ".join(f"{i}:{st[i]:.1f}/{se[i]:.1f}/{en[i]:.1f}" for i in late))
