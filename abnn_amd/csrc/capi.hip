@@ -100,7 +100,7 @@ void free_all(abnn_brain* b)
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->d.bitmap,    b->d.filter,     b->d.range_info,    b->d.g2x,
                     b->d.chunk_cnt,
-                    b->d.apply_partial, b->d.claim,  b->d.g2src,      b->d.grown,
+                    b->d.wg_stats, b->d.claim,  b->d.g2src,      b->d.grown,
                     b->d.dead,      b->compact_offsets,
                     b->d.work,      b->idx_scratch,
                     b->u64_scratch,  b->d.wave_clock,  b->d.range_bounds,  const_cast<uint32_t*>(b->d.dummy)};
@@ -340,7 +340,6 @@ abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
 abnn_status run_commit(abnn_brain* b, const int32_t* gathered, uint32_t world, bool renorm,
                        hipStream_t s)
 {
-    HIP_TRY(launch_finalize(b->d, b->kp, gathered, world, s));
     host_tick(b);
     if (renorm) {  // renormalise_if_needed, brain.cpp:125-141; kernel brain.metal:135-145
         HIP_TRY(launch_renorm(b->d, b->clock_host, s));
@@ -519,7 +518,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     uint32_t* dummy = nullptr;
     if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
     d.dummy = dummy;
-    if ((s = dalloc(&d.apply_partial, kMaxApplyBlocks)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.wg_stats, kWalkBlocks)) != ABNN_OK) return fail(s);
     if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, cap)) != ABNN_OK) return fail(s);
     if (p.compact_every > 0) {  // structural updates: the compaction's second buffer + scratch
         const uint64_t nb = (cap + kCompactChunk - 1) / kCompactChunk;
@@ -768,7 +767,7 @@ abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream)
         // the host reads the clock at encode time, before the pass (brain.cpp:127-128)
         const bool renorm = b->clock_host > b->params.renorm_thresh;
         ST_TRY(run_gate(b, nullptr, s));
-        HIP_TRY(launch_apply(b->d, b->kp, nullptr, 0, s));
+        HIP_TRY(launch_apply(b->d, b->kp, nullptr, 1, 0, s));
         ST_TRY(run_commit(b, nullptr, 1, renorm, s));
     }
     return ABNN_OK;
@@ -804,7 +803,7 @@ abnn_status abnn_shard_apply(abnn_brain* b, const void* gathered_dev, uint32_t w
     REQUIRE(world >= 1 && rank < world, "bad world/rank");
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
-    HIP_TRY(launch_apply(b->d, b->kp, static_cast<const int32_t*>(gathered_dev), rank, s));
+    HIP_TRY(launch_apply(b->d, b->kp, static_cast<const int32_t*>(gathered_dev), world, rank, s));
     return ABNN_OK;
 }
 
@@ -844,6 +843,18 @@ abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out)
     REQUIRE(b && out, "null argument");
     ST_TRY(sync_all(b));
     HIP_TRY(hipMemcpy(out, &b->d.work->stats, sizeof(abnn_stats), hipMemcpyDeviceToHost));
+    std::vector<abnn_stats> wg(kWalkBlocks);
+    HIP_TRY(hipMemcpy(wg.data(), b->d.wg_stats, kWalkBlocks * sizeof(abnn_stats), hipMemcpyDeviceToHost));
+    for (const abnn_stats& x : wg) {
+        out->passes += x.passes;
+        out->events += x.events;
+        out->pre_gated += x.pre_gated;
+        out->post_gated += x.post_gated;
+        out->updated += x.updated;
+        out->fired += x.fired;
+        out->pruned += x.pruned;
+        out->grown += x.grown;
+    }
     return ABNN_OK;
 }
 
@@ -852,6 +863,7 @@ abnn_status abnn_reset_stats(abnn_brain* b)
     REQUIRE(b, "null argument");
     ST_TRY(sync_all(b));
     HIP_TRY(hipMemset(&b->d.work->stats, 0, sizeof(abnn_stats)));
+    HIP_TRY(hipMemset(b->d.wg_stats, 0, kWalkBlocks * sizeof(abnn_stats)));
     return ABNN_OK;
 }
 

@@ -20,7 +20,7 @@ constexpr int kMaxRanges = 16384;  // kMaxGateBlocks x up to 16 waves (one range
 constexpr int kApplyThreads = 1024;  // budget-walk workgroups (k_spikes, k_claim, k_apply)
 constexpr uint32_t kWalkBlocks = 256; // their grid: 4096 waves, one work item (chunk) per wave at a time
 constexpr int kMaxApplyBlocks = kWalkBlocks;
-static_assert(kMaxApplyBlocks <= kScanThreads, "k_finalize reads one apply partial per thread");
+static_assert(kMaxApplyBlocks <= kApplyThreads, "the finalizing workgroup reads one apply partial per thread");
 static_assert(kMaxRanges % kApplyThreads == 0, "range prefix: whole ranges per thread");
 constexpr int kDummyRecords = 64 * 32;  // >= 64 lanes x max events per lane; also the record-buffer padding
 constexpr uint32_t kChunk = 384;        // pre-gated events per chunk (staged in LDS by a gate wave)
@@ -29,8 +29,9 @@ constexpr uint32_t kChunkSlotDiv = 128; // chunk_cnt index = (region + c * kChun
 // Per-pass bookkeeping in device memory (one per handle).
 struct alignas(16) PassWork {
     uint32_t t0_g2;        // global event 0 passed both gates this pass (re-armed by k_finalize)
-    uint32_t pad[3];
-    abnn_stats stats;      // cumulative (finalize adds)
+    uint32_t ticket;       // k_apply workgroups done this pass (the last one finalizes, re-arms it)
+    uint32_t pad[2];
+    abnn_stats stats;      // host-kept counters (grown); the device ones live in DeviceState::wg_stats
 };
 
 // Synapse records on the device, structure of arrays: record i is
@@ -59,7 +60,7 @@ struct DeviceState {
     uint4* g2x;               // [iters * iter_events] per-range regions: {event - region, isi | cand << 31, w, dst}
     uint4* chunk_cnt;         // [iters * iter_events / kChunkSlotDiv + 8] {pre-gated, survivors, candidates, 0}
     const uint32_t* dummy;    // [kDummyRecords] zeros: target of the stream loads past a range
-    uint4* apply_partial;     // [kMaxApplyBlocks] {updated, fired, pruned, 0} per apply workgroup
+    abnn_stats* wg_stats;     // [kWalkBlocks] statistics, one slot per k_apply workgroup (summed by abnn_get_stats)
     uint32_t* g2src;          // genesis on: [iters * iter_events] src of the g2x entry's record
     uint4* grown;             // genesis on: [compact_every * max_spikes] grown records (w = 1: used)
     uint32_t* dead;           // pruning on: tombstones per kCompactChunk records (structural update)
@@ -118,11 +119,11 @@ hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t 
 hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s);
 // Sharded passes: this shard's exchange record (summary + local spike list).
 hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out, hipStream_t s);
-// gathered == nullptr: single-GPU pass (no exchange; k_apply stamps the spikes).
+// The rest of the pass: budget walk, weight update, stamps and, in its last
+// workgroup, the pass's end (rBar, clock, statistics, next partition).
+// gathered == nullptr: single-GPU pass (no exchange).
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
-                        uint32_t rank, hipStream_t s);
-hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
-                           uint32_t world, hipStream_t s);
+                        uint32_t world, uint32_t rank, hipStream_t s);
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);
 // Structural update: stable compaction into `dst`, block b of kCompactChunk
 // records starting at offsets[b] (live counts from the k_apply tombstone tally).

@@ -23,11 +23,12 @@
 //                (brain.metal:101-122, non-temporal stores; pruning,
 //                synaptogenesis) and the deferred stamps (brain.metal:125-126).
 //                k_claim precedes it in random mode (highest event wins).
-//   k_finalize : rBar EWMA (brain.metal:110-113), one clock tick
-//                (brain.metal:129), statistics, the next pass's partition.
+//                Its last workgroup ends the pass: rBar EWMA
+//                (brain.metal:110-113), one clock tick (brain.metal:129),
+//                statistics, the next pass's partition.
 //   k_renorm   : brain.metal:135-145 with the base read once (no race).
-//   Sharded passes add k_scan + k_spikes (the exchange record) after the gate
-//   and stamp every rank's spikes in k_finalize.
+//   Sharded passes add k_scan + k_spikes (the exchange record) after the gate;
+//   k_apply then stamps every rank's spikes from the gathered records.
 //
 // All fp32 arithmetic is compiled with -ffp-contract=off and written operation
 // for operation like the oracle, so weights are bit-identical to the CPU.
@@ -185,6 +186,20 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 __device__ __forceinline__ uint32_t wave_total(uint32_t x)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(x), 63);
+}
+
+// Sum of one u64 per thread over an NT-thread workgroup (every thread gets it).
+template <int NT>
+__device__ uint64_t block_sum(uint64_t v, uint64_t* s_wave)
+{
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t t = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NT / 64; ++w) t += s_wave[w];
+    __syncthreads();
+    return t;
 }
 
 // Exclusive scan of one u64 per thread over an NT-thread workgroup.
@@ -540,7 +555,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     const uint4 c = refrac_chunk<kChunk / 64, kRandom>(d, kp, region, tb, pend, now, pass, stage_at);
     if (lane == 0) {
         d.range_info[r] = make_uint4(tot.x + c.x, tot.y + c.y, tot.z + c.z, nch);
-        // this wave's stream time drives the next pass's partition (k_finalize);
+        // this wave's gate time drives the next pass's partition (finalize_pass);
         // 100 MHz wall clock
         d.wave_clock[4 * r] = t_start;
         d.wave_clock[4 * r + 1] = t_stream;
@@ -550,114 +565,130 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 }
 
 // ---------------------------------------------------------------------------
-// Work items of the full chunks.  s_cpre[r] = full chunks of the ranges
-// before r (exclusive prefix of range_info[].w, one workgroup, in LDS);
-// item j belongs to the last range r with s_cpre[r] <= j.
+// The ordered spike budget of schedule C1 (brain.metal:85-98 without its
+// races): an event that passed both gates is updated iff fewer than
+// max_spikes spike candidates precede it in global event order.  Walked by
+// k_spikes, k_claim and k_apply alike.  Every workgroup first builds, in LDS,
+// per range: the capped exclusive candidate prefix, the exclusive prefix of
+// full chunks and the survivor count (one packed scan over range_info, a few
+// KB read from L2 -- cheaper than a separate single-workgroup scan launch).
+// The work items are the last chunk of every range and every full chunk, one
+// per wave at a time: an item adds the candidates of its range's lower full
+// chunks, leaves at once if the budget is spent, and otherwise visits its
+// (<= kChunk) survivors in event order, calling f(region, entry, candidate,
+// budget position, g2x index) for each one whose position is below the budget.
+// A range without full chunks costs its item one global round trip (g2x).
+constexpr uint32_t kWalkWaves = kApplyThreads / 64;
 constexpr uint32_t kPrePerThread = kMaxRanges / kApplyThreads;
 
-template <int NT>
-__device__ uint32_t chunk_prefix(const DeviceState& d, uint32_t* s_cpre, uint64_t* s_red)
+struct WalkLds {
+    uint32_t* pre;   // [NR]     min(off + candidates of ranges < r, budget)
+    uint32_t* cpre;  // [NR + 1] full chunks of ranges < r
+    uint32_t* surv;  // [NR]     refractory survivors of range r
+};
+
+__device__ __forceinline__ WalkLds walk_lds_view(uint32_t* s, uint32_t NR)
 {
-    const uint32_t NR = d.n_ranges, per = (NR + NT - 1) / NT, q0 = threadIdx.x * per;
-    uint32_t c[kMaxRanges / NT];
-    uint64_t sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kMaxRanges / NT; ++j) {
-        c[j] = (j < per && q0 + j < NR) ? d.range_info[q0 + j].w : 0u;
-        sum += c[j];
-    }
-    uint64_t tot;
-    uint32_t run = (uint32_t)block_exclusive_scan<NT>(sum, &tot, s_red);
-#pragma unroll
-    for (uint32_t j = 0; j < kMaxRanges / NT; ++j) {
-        if (j < per && q0 + j < NR) s_cpre[q0 + j] = run;
-        run += c[j];
-    }
-    __syncthreads();
-    return (uint32_t)tot;
+    return WalkLds{s, s + NR, s + 2 * NR + 1};
 }
 
-__device__ __forceinline__ uint32_t chunk_range(const uint32_t* s_cpre, uint32_t NR, uint32_t j)
+// Builds the WalkLds arrays; returns the number of full chunks.  With totals,
+// also the pass's pre-gated and survivor counts (every thread gets them).
+__device__ uint32_t walk_prefix(const DeviceState& d, uint64_t off, uint64_t budget, const WalkLds& L, uint64_t* s_red,
+                                uint64_t* tot_g1, uint64_t* tot_g2)
+{
+    constexpr uint32_t kRound = 4;
+    const uint32_t NR = d.n_ranges, per = (NR + kApplyThreads - 1) / kApplyThreads, q0 = threadIdx.x * per;
+    uint64_t v[kPrePerThread];  // candidates | full chunks << 32
+    uint64_t sum = 0, g1 = 0, g2 = 0;
+    for (uint32_t j0 = 0; j0 < per; j0 += kRound) {
+        uint4 ri[kRound];
+#pragma unroll
+        for (uint32_t u = 0; u < kRound; ++u) ri[u] = range_totals(d, min(q0 + j0 + u, NR - 1));  // clamped
+#pragma unroll
+        for (uint32_t u = 0; u < kRound; ++u) {
+            const uint32_t j = j0 + u, q = q0 + j;
+            const bool in = j < per && q < NR;
+            const uint64_t x = in ? (uint64_t)ri[u].z | ((uint64_t)ri[u].w << 32) : 0u;
+            if (j < kPrePerThread) v[j] = x;
+            if (in) L.surv[q] = ri[u].y;
+            sum += x;
+            g1 += in ? ri[u].x : 0u;
+            g2 += in ? ri[u].y : 0u;
+        }
+    }
+    uint64_t tot;
+    uint64_t run = block_exclusive_scan<kApplyThreads>(sum, &tot, s_red);
+    uint64_t cand = off + (uint32_t)run;
+    uint32_t chunks = (uint32_t)(run >> 32);
+#pragma unroll
+    for (uint32_t j = 0; j < kPrePerThread; ++j) {
+        if (j < per && q0 + j < NR) {
+            L.pre[q0 + j] = (uint32_t)(cand < budget ? cand : budget);
+            L.cpre[q0 + j] = chunks;
+            cand += (uint32_t)v[j];
+            chunks += (uint32_t)(v[j] >> 32);
+        }
+    }
+    if (threadIdx.x == 0) L.cpre[NR] = (uint32_t)(tot >> 32);
+    if (tot_g1) {  // workgroup-uniform
+        *tot_g1 = block_sum<kApplyThreads>(g1, s_red);
+        *tot_g2 = block_sum<kApplyThreads>(g2, s_red);
+    }
+    __syncthreads();
+    return (uint32_t)(tot >> 32);
+}
+
+// item j of the full chunks belongs to the last range r with cpre[r] <= j
+__device__ __forceinline__ uint32_t chunk_range(const uint32_t* cpre, uint32_t NR, uint32_t j)
 {
     uint32_t lo = 0, hi = NR;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (s_cpre[mid] <= j) lo = mid;
+        if (cpre[mid] <= j) lo = mid;
         else hi = mid;
     }
     return lo;
 }
 
-// ---------------------------------------------------------------------------
-// The ordered spike budget of schedule C1 (brain.metal:85-98 without its
-// races): an event that passed both gates is updated iff fewer than
-// max_spikes spike candidates precede it in global event order.  Walked by
-// k_spikes, k_claim and k_apply alike.  Every workgroup first builds, in LDS,
-// the capped exclusive candidate prefix of all ranges and the full-chunk
-// prefix (a few KB read from L2; cheaper than a separate single-workgroup scan
-// launch).  The work items are the last chunk of every range and every full
-// chunk, one per wave at a time: an item adds the candidates of its range's
-// lower full chunks, leaves at once if the budget is spent, and otherwise
-// visits its (<= kChunk) survivors in event order, calling f(region, entry,
-// candidate, budget position, g2x index) for each one whose position is below
-// the budget.
-constexpr uint32_t kWalkWaves = kApplyThreads / 64;
-
-// s_pre[r] = min(off + candidates of ranges < r, budget), r < n_ranges.
-__device__ void range_prefix(const DeviceState& d, uint64_t off, uint64_t budget, uint32_t* s_pre, uint64_t* s_red)
-{
-    const uint32_t NR = d.n_ranges, per = (NR + kApplyThreads - 1) / kApplyThreads, q0 = threadIdx.x * per;
-    uint32_t c[kPrePerThread];
-    uint64_t sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kPrePerThread; ++j) {
-        c[j] = (j < per && q0 + j < NR) ? range_totals(d, q0 + j).z : 0u;
-        sum += c[j];
-    }
-    uint64_t tot;
-    uint64_t run = off + block_exclusive_scan<kApplyThreads>(sum, &tot, s_red);
-#pragma unroll
-    for (uint32_t j = 0; j < kPrePerThread; ++j) {
-        if (j < per && q0 + j < NR) s_pre[q0 + j] = (uint32_t)(run < budget ? run : budget);
-        run += c[j];
-    }
-    __syncthreads();
-}
-
 template <class F>
 __device__ void budget_walk(const DeviceState& d, uint64_t off, uint64_t budget, uint32_t* s_lds, uint64_t* s_red,
-                            F&& f)
+                            F&& f, uint64_t* tot_g1 = nullptr, uint64_t* tot_g2 = nullptr)
 {
     const uint32_t NR = d.n_ranges;
-    uint32_t* s_pre = s_lds;
-    uint32_t* s_cpre = s_lds + NR;
-    range_prefix(d, off, budget, s_pre, s_red);
-    const uint32_t items = NR + chunk_prefix<kApplyThreads>(d, s_cpre, s_red);
+    const WalkLds L = walk_lds_view(s_lds, NR);
+    const uint32_t items = NR + walk_prefix(d, off, budget, L, s_red, tot_g1, tot_g2);
     const uint32_t lane = threadIdx.x & 63, w = wave_uniform(threadIdx.x >> 6);
     for (uint32_t i = blockIdx.x * kWalkWaves + w; i < items; i += gridDim.x * kWalkWaves) {
         uint32_t r, c;
         if (i < NR) {
             r = i;
-            c = d.range_info[r].w;  // the last chunk follows the full ones
+            c = L.cpre[r + 1] - L.cpre[r];  // the last chunk follows the full ones
         } else {
-            r = chunk_range(s_cpre, NR, i - NR);
-            c = i - NR - s_cpre[r];
+            r = chunk_range(L.cpre, NR, i - NR);
+            c = i - NR - L.cpre[r];
         }
-        uint64_t P = s_pre[r];
+        uint64_t P = L.pre[r];
         if (P >= budget) continue;
         const uint64_t region = region_of(d, r);
-        uint32_t cl = 0, gl = 0;  // candidates / survivors of the lower full chunks
-        for (uint32_t c0 = 0; c0 < c; c0 += 64)
-            if (c0 + lane < c) {
-                const uint4 x = d.chunk_cnt[chunk_slot(region, c0 + lane)];
-                cl += x.z;
-                gl += x.y;
-            }
-        P += wave_sum(cl);
-        if (P >= budget) continue;
-        const uint4 ri = d.range_info[r];
-        // survivors of this chunk: the last one holds what the full ones do not
-        const uint32_t n = c == ri.w ? ri.y - wave_sum(gl) : d.chunk_cnt[chunk_slot(region, c)].y;
+        const uint32_t nfull = L.cpre[r + 1] - L.cpre[r];
+        uint32_t n = 0;
+        if (nfull) {  // candidates of the lower full chunks; survivors of this one
+            uint32_t cl = 0, gl = 0, own = 0;
+            for (uint32_t c0 = 0; c0 < nfull; c0 += 64)
+                if (c0 + lane < nfull && c0 + lane <= c) {
+                    const uint4 x = d.chunk_cnt[chunk_slot(region, c0 + lane)];
+                    if (c0 + lane < c) cl += x.z;
+                    else own = x.y;
+                    gl += x.y;
+                }
+            P += wave_sum(cl);
+            if (P >= budget) continue;
+            // the last chunk holds what the full ones do not
+            n = c == nfull ? L.surv[r] - wave_sum(gl) : wave_sum(own);
+        } else {
+            n = L.surv[r];
+        }
         const uint64_t base = region + (uint64_t)c * kChunk;
         constexpr uint32_t RW = kChunk / 64;
         uint4 e[RW];
@@ -685,6 +716,139 @@ __device__ uint64_t rank_offset(const KernelParams& kp, const int32_t* gathered,
     if (gathered)
         for (uint32_t q = 0; q < rank; ++q) off += (uint64_t)*reinterpret_cast<const int64_t*>(gathered + q * words);
     return off < kp.max_spikes ? off : kp.max_spikes;
+}
+
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+// Sharded passes: stamp rank r's first min(count_r, budget - offset_r) spikes
+// (the gathered exchange records, rank order); workgroups take slices.
+__device__ void stamp_gathered(const DeviceState& d, const KernelParams& kp, const int32_t* gathered, uint32_t world,
+                               uint64_t now)
+{
+    const uint32_t words = xchg_words(kp.max_spikes);
+    const uint64_t budget = kp.max_spikes;
+    uint64_t off = 0;
+    for (uint32_t r = 0; r < world && off < budget; ++r) {
+        const int64_t cnt = *reinterpret_cast<const int64_t*>(gathered + r * words);
+        const int32_t* sp = gathered + r * words + 2 * ABNN_SUMMARY_WORDS;
+        const uint64_t room = budget - off, n = (uint64_t)cnt < room ? (uint64_t)cnt : room;
+        for (uint64_t i = (uint64_t)blockIdx.x * kApplyThreads + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kApplyThreads) {
+            const uint32_t nrn = (uint32_t)sp[i];
+            if (nrn < d.n_nrn) d.last_fired[nrn] = now;
+        }
+        off += n;
+    }
+}
+
+// The end of a pass, by the last k_apply workgroup (every other one has read
+// the pass-start scalars and is done with the partition): rBar
+// (brain.metal:110-113), clock tick (brain.metal:129) and the next pass's
+// sweep partition.  Equal ranges do not finish together: a wave's stream rate
+// depends on how the SIMD arbiter treats it (the gate rotates priorities) and
+// dense parts of the graph stage more events.  So range r's measured gate time
+// (wave_clock), spread evenly over its iterations, gives a cumulative cost
+// curve, and boundary k moves halfway from its old place towards the
+// iteration where the curve reaches k / NR of the total.  Results do not
+// depend on the partition (event order is global, C1).
+__device__ void finalize_pass(const DeviceState& d, const KernelParams& kp, const int32_t* gathered, uint32_t world,
+                              uint64_t now, float R, float rbar, uint64_t pass, uint32_t* s_lds)
+{
+    constexpr uint32_t NWv = kApplyThreads / 64, kRound = 4;
+    __shared__ uint32_t s_w[NWv];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, NR = d.n_ranges;
+    if (tid == 0) {
+        uint64_t events = d.events;
+        int64_t t0 = d.work->t0_g2;
+        if (gathered) {
+            const uint32_t words = xchg_words(kp.max_spikes);
+            events = 0;
+            t0 = 0;
+            for (uint32_t r = 0; r < world; ++r) {
+                const int64_t* sm = reinterpret_cast<const int64_t*>(gathered + r * words);
+                events += (uint64_t)sm[2];
+                t0 |= sm[1];
+            }
+        }
+        if (t0 != 0 && kp.max_spikes > 0)
+            *d.rbar = rbar + kp.alpha_rbar * (R - rbar);  // brain.metal:110-113
+        if (events > 0) *d.clock = now + kp.clock_inc;     // brain.metal:129
+        *d.pass_index = pass + 1;
+        d.work->t0_g2 = 0;  // re-armed for the next pass
+        __hip_atomic_store((gu32*)(&d.work->ticket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- the next pass's partition
+    if (!d.adapt_ranges || NR < 2) return;
+    const uint32_t per = (NR + kApplyThreads - 1) / kApplyThreads, q0 = tid * per;
+    uint32_t csum = 0;
+    uint32_t rb[kMaxRanges / kApplyThreads], cost[kMaxRanges / kApplyThreads];
+    for (uint32_t j0 = 0; j0 < per; j0 += kRound) {
+        uint32_t b0[kRound], b1[kRound];
+        uint64_t ts[kRound], te[kRound];
+#pragma unroll
+        for (uint32_t u = 0; u < kRound; ++u) {
+            const uint32_t q = min(q0 + j0 + u, NR - 1);  // clamped: loads never depend on a branch
+            b0[u] = d.range_bounds[q];
+            b1[u] = d.range_bounds[q + 1];
+            ts[u] = d.wave_clock[4 * q];
+            te[u] = d.wave_clock[4 * q + 2];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kRound; ++u) {
+            const uint32_t j = j0 + u;
+            const bool in = j < per && q0 + j < NR;
+            // gate time of the range in 40-ns units, clamped (<= 2.6 ms)
+            const uint64_t t = (te[u] - ts[u]) >> 2;
+            const uint32_t c = in && b1[u] > b0[u] ? (uint32_t)(t < 1 ? 1 : (t > 0xFFFFu ? 0xFFFFu : t)) : 0u;
+            if (j < kMaxRanges / kApplyThreads) {
+                rb[j] = b0[u];
+                cost[j] = c;
+            }
+            csum += c;
+        }
+    }
+    // cost scan on DPP (u32: costs below 2^30)
+    const uint32_t cin = wave_incl_scan(csum);
+    if (lane == 63) s_w[wv] = cin;
+    __syncthreads();
+    uint32_t before = 0, total_cost = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NWv; ++w) {
+        before += w < wv ? s_w[w] : 0u;
+        total_cost += s_w[w];
+    }
+    uint32_t* s_cc = s_lds;           // [NR + 1] exclusive cumulative cost (reuses the walk's LDS)
+    uint32_t* s_rb = s_lds + NR + 1;  // [NR + 1] current bounds
+    uint32_t run = before + cin - csum;
+#pragma unroll
+    for (uint32_t j = 0; j < kMaxRanges / kApplyThreads; ++j) {
+        if (j < per && q0 + j < NR) {
+            s_cc[q0 + j] = run;
+            s_rb[q0 + j] = rb[j];
+            run += cost[j];
+        }
+    }
+    if (tid == 0) {
+        s_cc[NR] = total_cost;
+        s_rb[NR] = d.iters;
+    }
+    __syncthreads();
+    if (total_cost == 0) return;
+    for (uint32_t k = tid + 1; k < NR; k += kApplyThreads) {
+        const uint32_t T = (uint32_t)((uint64_t)k * total_cost / NR);
+        uint32_t lo = 0, hi = NR;  // last range with s_cc <= T (its cost is > 0)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_cc[mid] <= T) lo = mid;
+            else hi = mid;
+        }
+        // integer floors keep the bounds monotonic in k (ranges never overlap)
+        const uint32_t cr = s_cc[lo + 1] - s_cc[lo];
+        const uint32_t target =
+            s_rb[lo] + (cr ? (uint32_t)((uint64_t)(T - s_cc[lo]) * (s_rb[lo + 1] - s_rb[lo]) / cr) : 0u);
+        d.range_bounds[k] = (target + s_rb[k]) >> 1;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -724,7 +888,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(DeviceState d, KernelPara
 // ---------------------------------------------------------------------------
 // k_spikes (sharded passes only): this shard's spike list in local budget
 // order, written into its exchange record before the all-gather, so that every
-// rank can stamp every rank's spikes in k_finalize.
+// rank can stamp every rank's spikes in k_apply.
 __global__ __launch_bounds__(kApplyThreads) void k_spikes(DeviceState d, KernelParams kp, int32_t* spikes)
 {
     extern __shared__ uint32_t s_pre[];
@@ -755,22 +919,36 @@ __global__ __launch_bounds__(kApplyThreads) void k_claim(DeviceState d, KernelPa
 // k_apply: weight update (brain.metal:101-122) of the gated events that still
 // had budget.  Single GPU (no exchange): the spikes are stamped here
 // (brain.metal:125-126, deferred to after every lastFired read of the pass);
-// sharded passes stamp from the gathered spike lists in k_finalize.
+// sharded passes stamp from the gathered spike lists (stamp_gathered).
 __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelParams kp,
-                                                         const int32_t* gathered, uint32_t rank)
+                                                         const int32_t* gathered, uint32_t world, uint32_t rank)
 {
-    extern __shared__ uint32_t s_pre[];
+    extern __shared__ uint32_t s_lds[];
     __shared__ uint64_t s_red[kWalkWaves];
     __shared__ uint32_t s_u[kWalkWaves], s_f[kWalkWaves], s_p[kWalkWaves];
+    __shared__ uint64_t s_now, s_pass;
+    __shared__ float s_R, s_rb;
+    __shared__ uint32_t s_last;
+    // pass-start scalars (C1, brain.metal:105-106), read by one lane and used
+    // through LDS only: the last workgroup rewrites them
+    if (threadIdx.x == 0) {
+        s_R = *d.reward;
+        s_rb = *d.rbar;
+        s_now = *d.clock;
+        s_pass = *d.pass_index;
+    }
     // every gate workgroup has its copy of the filter image: zero it for the next k_bitmap
     for (uint32_t i = blockIdx.x * kApplyThreads + threadIdx.x; i < 2 * d.filter_words; i += gridDim.x * kApplyThreads)
         d.filter[i] = 0u;
-    const float R = *d.reward, rb = *d.rbar;  // pass-start values (C1), brain.metal:105-106
-    const uint64_t now = *d.clock, pass = *d.pass_index;
+    __syncthreads();
+    const float R = s_R, rb = s_rb;
+    const uint64_t now = s_now, pass = s_pass;
     const bool random = d.mode == ABNN_MODE_RANDOM, stamp = gathered == nullptr;
     const bool prune = kp.w_prune > 0.0f, genesis = d.grown != nullptr && kp.p_new > 0.0f;
     uint32_t upd = 0, nf = 0, npr = 0;
-    budget_walk(d, rank_offset(kp, gathered, rank), kp.max_spikes, s_pre, s_red,
+    uint64_t g1 = 0, g2 = 0;
+    const bool first = blockIdx.x == 0;  // workgroup 0 also counts the pass's gate totals
+    budget_walk(d, rank_offset(kp, gathered, rank), kp.max_spikes, s_lds, s_red,
                 [&](uint64_t region, const uint4& e, bool f, uint64_t pre, uint64_t slot) {
         const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.y & 0x7FFFFFFFu));
         const uint64_t t = region + e.x, ri = rec_index(d, t, pass);
@@ -805,8 +983,13 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
                 }
             }
         }
-    });
-    // per-workgroup partials (atomics from every wave on one address serialise)
+    }, first ? &g1 : nullptr, first ? &g2 : nullptr);
+    // sharded passes: every rank's spikes from the gathered exchange records,
+    // budget order across ranks = global event order (brain.metal:125-126);
+    // nothing of this kernel reads lastFired
+    if (gathered) stamp_gathered(d, kp, gathered, world, now);
+    // statistics: every workgroup adds into its own slot (no cross-workgroup
+    // sum; abnn_get_stats adds the slots)
     const uint32_t wu = wave_sum(upd), wf = wave_sum(nf), wp = wave_sum(npr);
     if ((threadIdx.x & 63) == 0) {
         s_u[threadIdx.x >> 6] = wu;
@@ -815,178 +998,32 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint4 t = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t tu = 0, tf = 0, tp = 0;
         for (uint32_t v = 0; v < kWalkWaves; ++v) {
-            t.x += s_u[v];
-            t.y += s_f[v];
-            t.z += s_p[v];
+            tu += s_u[v];
+            tf += s_f[v];
+            tp += s_p[v];
         }
-        d.apply_partial[blockIdx.x] = t;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_finalize: rBar (brain.metal:110-113), clock tick (brain.metal:129),
-// statistics; in sharded passes also the deferred stamps of every rank's
-// spikes from the gathered exchange records (brain.metal:125-126).  One
-// workgroup; every global load is issued up front (the kernel is a chain of
-// round trips otherwise).
-//
-// It also sets the next pass's sweep partition.  Equal ranges do not finish
-// together: a wave's stream rate depends on its age rank on its SIMD (the
-// oldest of four waves per SIMD streams ~20 % faster than the youngest,
-// profiles/r01o_wave_slots.txt) and dense parts of the graph stage more
-// events.  So range r's measured gate time (wave_clock), spread evenly over its
-// iterations, gives a cumulative cost curve, and boundary k moves halfway from
-// its old place towards the iteration where the curve reaches k / NR of the
-// total.  Results do not depend on the partition (event order is global, C1).
-__global__ __launch_bounds__(kScanThreads) void k_finalize(DeviceState d, KernelParams kp,
-                                                           const int32_t* gathered, uint32_t world)
-{
-    extern __shared__ uint32_t s_lds[];
-    constexpr uint32_t NWv = kScanThreads / 64, kU = 4, kRound = 4;
-    __shared__ uint32_t s_w[6][NWv];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, words = xchg_words(kp.max_spikes);
-    const uint32_t NR = d.n_ranges;
-    uint64_t* fin_clock = d.wave_clock + 4 * (uint64_t)kMaxRanges;  // diagnostics: phase times
-    if (tid == 0) fin_clock[0] = __builtin_amdgcn_s_memrealtime();
-    const uint64_t now = *d.clock;
-    const uint64_t budget = kp.max_spikes;
-    // ---- loads, all issued before any is used: ranges (counts, bounds, wave
-    // times; kRound consecutive ranges per thread per round), apply partials
-    const uint32_t per = (NR + kScanThreads - 1) / kScanThreads, q0 = tid * per;
-    uint32_t g1 = 0, g2 = 0, csum = 0;
-    uint32_t rb[kMaxRanges / kScanThreads], cost[kMaxRanges / kScanThreads];
-    for (uint32_t j0 = 0; j0 < per; j0 += kRound) {
-        uint4 ri[kRound];
-        uint32_t b0[kRound], b1[kRound];
-        uint64_t ts[kRound], te[kRound];
-#pragma unroll
-        for (uint32_t u = 0; u < kRound; ++u) {
-            const uint32_t q = min(q0 + j0 + u, NR - 1);  // clamped: loads never depend on a branch
-            ri[u] = range_totals(d, q);
-            b0[u] = d.range_bounds[q];
-            b1[u] = d.range_bounds[q + 1];
-            ts[u] = d.wave_clock[4 * q];
-            te[u] = d.wave_clock[4 * q + 2];
+        abnn_stats* st = d.wg_stats + blockIdx.x;
+        abnn_stats x = *st;
+        x.updated += tu;
+        x.fired += tf;
+        x.pruned += tp;
+        if (first) {
+            x.passes += 1;
+            x.events += d.events;
+            x.pre_gated += g1;
+            x.post_gated += g2;
         }
-#pragma unroll
-        for (uint32_t u = 0; u < kRound; ++u) {
-            const uint32_t j = j0 + u;
-            const bool in = j < per && q0 + j < NR;
-            // gate time of the range in 40-ns units, clamped (<= 2.6 ms)
-            const uint64_t t = (te[u] - ts[u]) >> 2;
-            const uint32_t c = in && b1[u] > b0[u] ? (uint32_t)(t < 1 ? 1 : (t > 0xFFFFu ? 0xFFFFu : t)) : 0u;
-            if (j < kMaxRanges / kScanThreads) {
-                rb[j] = b0[u];
-                cost[j] = c;
-            }
-            g1 += in ? ri[u].x : 0u;
-            g2 += in ? ri[u].y : 0u;
-            csum += c;
-        }
-    }
-    uint4 ap = make_uint4(0u, 0u, 0u, 0u);
-    if (tid < kWalkBlocks) ap = d.apply_partial[tid];
-    uint64_t events = d.events, off = 0;
-    int64_t t0 = d.work->t0_g2;
-    if (gathered) {
-        events = 0;
-        t0 = 0;
-        for (uint32_t r = 0; r < world; ++r) {
-            const int64_t* sm = reinterpret_cast<const int64_t*>(gathered + r * words);
-            const int32_t* sp = gathered + r * words + 2 * ABNN_SUMMARY_WORDS;
-            events += (uint64_t)sm[2];
-            t0 |= sm[1];
-            // rank r's spikes fill budget slots [off, off + n)
-            const uint64_t room = budget - off, n = (uint64_t)sm[0] < room ? (uint64_t)sm[0] : room;
-            for (uint64_t i0 = 0; i0 < n; i0 += kU * kScanThreads) {
-                uint32_t nrn[kU];
-#pragma unroll
-                for (uint32_t u = 0; u < kU; ++u) {
-                    const uint64_t i = i0 + u * kScanThreads + tid;
-                    nrn[u] = i < n ? (uint32_t)sp[i] : 0xFFFFFFFFu;
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < kU; ++u)
-                    if (nrn[u] < d.n_nrn) d.last_fired[nrn[u]] = now;
-            }
-            off += n;
-        }
-    }
-    if (tid == 0) fin_clock[1] = __builtin_amdgcn_s_memrealtime();
-    // ---- one barrier round on DPP: the cost scan and the statistics sums
-    // (u32: per-pass counts of one rank stay below 2^32, costs below 2^30)
-    const uint32_t cin = wave_incl_scan(csum);
-    const uint32_t v[6] = {(uint32_t)__builtin_amdgcn_readlane((int)cin, 63), wave_total(g1), wave_total(g2),
-                           wave_total(ap.x), wave_total(ap.y), wave_total(ap.z)};
-    if (lane == 0)
-        for (int i = 0; i < 6; ++i) s_w[i][wv] = v[i];
-    __syncthreads();
-    uint32_t before = 0, t[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (uint32_t w = 0; w < NWv; ++w) {
-        before += w < wv ? s_w[0][w] : 0u;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) t[i] += s_w[i][w];
-    }
-    const uint32_t total_cost = t[0];
-    uint32_t* s_cc = s_lds;           // [NR + 1] exclusive cumulative cost
-    uint32_t* s_rb = s_lds + NR + 1;  // [NR + 1] current bounds
-    uint32_t run = before + cin - csum;
-#pragma unroll
-    for (uint32_t j = 0; j < kMaxRanges / kScanThreads; ++j) {
-        if (j < per && q0 + j < NR) {
-            s_cc[q0 + j] = run;
-            s_rb[q0 + j] = rb[j];
-            run += cost[j];
-        }
-    }
-    if (tid == 0) {
-        s_cc[NR] = total_cost;
-        s_rb[NR] = d.iters;
+        *st = x;
+        // the last workgroup to arrive ends the pass; every workgroup's
+        // pass-start scalar loads are complete (used above through LDS)
+        const uint32_t ticket = __hip_atomic_fetch_add((gu32*)(&d.work->ticket), 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        s_last = ticket == gridDim.x - 1;
     }
     __syncthreads();
-    if (tid == 0) fin_clock[2] = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0) {
-        // every load before every store (the pointers may alias as far as the
-        // compiler knows: interleaved, each read-modify-write is a round trip)
-        const float R = *d.reward, rbar = *d.rbar;
-        const uint64_t pi = *d.pass_index;
-        PassWork* w = d.work;
-        abnn_stats st = w->stats;
-        st.passes += 1;
-        st.events += d.events;
-        st.pre_gated += t[1];
-        st.post_gated += t[2];
-        st.updated += t[3];
-        st.fired += t[4];
-        st.pruned += t[5];
-        if (t0 != 0 && budget > 0)
-            *d.rbar = rbar + kp.alpha_rbar * (R - rbar);  // brain.metal:110-113
-        if (events > 0) *d.clock = now + kp.clock_inc;     // brain.metal:129
-        *d.pass_index = pi + 1;
-        w->t0_g2 = 0;  // re-armed for the next pass
-        w->stats = st;
-        fin_clock[3] = __builtin_amdgcn_s_memrealtime();
-    }
-    // ---- the next pass's partition
-    if (!d.adapt_ranges || NR < 2 || total_cost == 0) return;
-    for (uint32_t k = tid + 1; k < NR; k += kScanThreads) {
-        const uint32_t T = (uint32_t)((uint64_t)k * total_cost / NR);
-        uint32_t lo = 0, hi = NR;  // last range with s_cc <= T (its cost is > 0)
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_cc[mid] <= T) lo = mid;
-            else hi = mid;
-        }
-        // integer floors keep the bounds monotonic in k (ranges never overlap)
-        const uint32_t cr = s_cc[lo + 1] - s_cc[lo];
-        const uint32_t target =
-            s_rb[lo] + (cr ? (uint32_t)((uint64_t)(T - s_cc[lo]) * (s_rb[lo + 1] - s_rb[lo]) / cr) : 0u);
-        d.range_bounds[k] = (target + s_rb[k]) >> 1;
-    }
-    if (tid == 0) fin_clock[4] = __builtin_amdgcn_s_memrealtime();
+    if (s_last) finalize_pass(d, kp, gathered, world, now, R, rb, pass, s_lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1094,8 +1131,8 @@ __global__ __launch_bounds__(256) void k_stamp_list(DeviceState d, const uint32_
 
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
-// budget walks: the candidate and full-chunk prefixes, one u32 each per range
-inline size_t walk_lds(const DeviceState& d) { return (size_t)std::max(1u, d.n_ranges) * 8; }
+// budget walks: WalkLds (three u32 per range; the finalizing workgroup reuses two)
+inline size_t walk_lds(const DeviceState& d) { return ((size_t)std::max(1u, d.n_ranges) + 1) * 12; }
 
 template <int BLOCK, int K, int FW>
 hipError_t launch_gate_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
@@ -1191,7 +1228,7 @@ hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xc
 }
 
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
-                        uint32_t rank, hipStream_t s)
+                        uint32_t world, uint32_t rank, hipStream_t s)
 {
     const dim3 g(kWalkBlocks), b(kApplyThreads);
     if (d.mode == ABNN_MODE_RANDOM) {
@@ -1199,15 +1236,7 @@ hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int3
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_apply, g, b, walk_lds(d), s, d, kp, gathered, rank);
-    return hipGetLastError();
-}
-
-hipError_t launch_finalize(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
-                           uint32_t world, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kScanThreads), (size_t)(d.n_ranges + 1) * 8, s, d, kp, gathered,
-                       world);
+    hipLaunchKernelGGL(k_apply, g, b, walk_lds(d), s, d, kp, gathered, world, rank);
     return hipGetLastError();
 }
 

@@ -30,8 +30,6 @@ for p in range(passes):
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     f.restype = ctypes.c_int
     assert f(b._h, buf.ctypes.data, buf.size) == 0
-    fin = buf[4 * nr:4 * nr + 5].astype(np.int64)
-    print("  k_finalize phases (us):", ((fin[1:] - fin[0]) * 0.01).round(2).tolist())
     w = buf[:4 * nr].reshape(-1, 4)
     w = w[w[:, 0] > 0]
     t0 = w[:, 0].min()
