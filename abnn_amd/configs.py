@@ -33,7 +33,7 @@ CONFIGS = {
                    "N_NRN=100k, N_SYN=10M, 10M events/pass"),
     # configs[2]: constants.h defaults -- the headline single-GPU workload
     "c3": Workload("c3", 256, 256, 5_000_000, 1_000_000_000, 150_000_000,
-                   "N_NRN=5,000,512, N_SYN=1B (16 GB SynapsePacked), 150M events/pass"),
+                   "N_NRN=5,000,512, N_SYN=1B (16 GB as SynapsePacked; 12 GB src/dst/w arrays in HBM), 150M events/pass"),
     # configs[3]: the same graph sharded across GPUs (150M events/pass/GPU, capped by shard)
     "c4": Workload("c4", 256, 256, 5_000_000, 1_000_000_000, 150_000_000,
                    "N_SYN=1B sharded N ways, 150M events/pass/GPU"),

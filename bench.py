@@ -201,16 +201,19 @@ def main():
         value = total_events / dt
         avg_gate_ms = gate_ms / max(1, launches)
         track = bool(brain.params.track_visits)
-        bytes_per_launch = algorithmic_bytes(stats, track) / max(1, launches)
+        # one gate launch per pass; HIP events time a sample of them (every
+        # TIMING_EVERY-th), so bytes per launch come from the pass count
+        passes = max(1, stats["passes"])
+        bytes_per_launch = algorithmic_bytes(stats, track) / passes
         achieved = bytes_per_launch / (avg_gate_ms * 1e-3) / 1e9
-        survey_per_launch = survey_bytes(stats, track) / max(1, launches)
+        survey_per_launch = survey_bytes(stats, track) / passes
         default_run = mode == 0 and events == wl.events
         traffic = load_traffic(args.config) if world == 1 and default_run else None
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
-            "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4),
+            "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": launches,
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "bytes_formula": ("4*E (src-array stream; E visited events) -- DESIGN.md §5" if mode == 0 else
                               "4*E (one random src word per pick; HBM moves >= 64 B per "
