@@ -103,7 +103,8 @@ void free_all(abnn_brain* b)
                     b->d.wg_stats, b->d.claim,  b->d.g2src,      b->d.grown,
                     b->d.dead,      b->compact_offsets,
                     b->d.work,      b->idx_scratch,
-                    b->u64_scratch,  b->d.wave_clock,  b->d.range_bounds,  const_cast<uint32_t*>(b->d.dummy)};
+                    b->u64_scratch,  b->d.wave_clock,  b->d.range_bounds,  b->d.range_bounds_next,
+                    const_cast<uint32_t*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& e : b->events) {
@@ -254,7 +255,7 @@ void configure(abnn_brain* b)
 }
 
 // Uniform sweep partition: range r starts at iteration floor(r * iters / NR)
-// (k_finalize then adapts it pass by pass).
+// (k_bitmap then adapts it pass by pass, adapt_partition).
 abnn_status reset_ranges(abnn_brain* b)
 {
     const DeviceState& d = b->d;
@@ -334,6 +335,16 @@ abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
     HIP_TRY(launch_gate(b->d, b->kp, s));
     if (ev) HIP_TRY(hipEventRecord(ev->b, s));
     if (xchg_out) HIP_TRY(launch_scan(b->d, b->kp, xchg_out, s));
+    return ABNN_OK;
+}
+
+// budget walk, weight update, stamps, pass end; k_apply writes the next
+// pass's partition into range_bounds_next, which becomes current here
+// (kernel arguments are captured at launch)
+abnn_status run_apply(abnn_brain* b, const int32_t* gathered, uint32_t world, uint32_t rank, hipStream_t s)
+{
+    HIP_TRY(launch_apply(b->d, b->kp, gathered, world, rank, s));
+    std::swap(b->d.range_bounds, b->d.range_bounds_next);
     return ABNN_OK;
 }
 
@@ -534,6 +545,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.wave_clock, 4 * (uint64_t)kMaxRanges + 16)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_bounds, max_ranges + 1)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.range_bounds_next, max_ranges + 1)) != ABNN_OK) return fail(s);
     d.adapt_ranges = std::getenv("ABNN_STATIC_RANGES") ? 0u : 1u;
     if ((s = reset_ranges(b)) != ABNN_OK) return fail(s);
     *out = b;
@@ -767,7 +779,7 @@ abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream)
         // the host reads the clock at encode time, before the pass (brain.cpp:127-128)
         const bool renorm = b->clock_host > b->params.renorm_thresh;
         ST_TRY(run_gate(b, nullptr, s));
-        HIP_TRY(launch_apply(b->d, b->kp, nullptr, 1, 0, s));
+        ST_TRY(run_apply(b, nullptr, 1, 0, s));
         ST_TRY(run_commit(b, nullptr, 1, renorm, s));
     }
     return ABNN_OK;
@@ -803,8 +815,7 @@ abnn_status abnn_shard_apply(abnn_brain* b, const void* gathered_dev, uint32_t w
     REQUIRE(world >= 1 && rank < world, "bad world/rank");
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
-    HIP_TRY(launch_apply(b->d, b->kp, static_cast<const int32_t*>(gathered_dev), world, rank, s));
-    return ABNN_OK;
+    return run_apply(b, static_cast<const int32_t*>(gathered_dev), world, rank, s);
 }
 
 abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t world, void* stream)

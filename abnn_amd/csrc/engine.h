@@ -14,7 +14,7 @@ namespace abnn {
 // recent-spike bitmap, each folded onto filter_words 32-bit words with its own
 // word hash (kernels.hip; 8192 words = 32 KiB each by default).
 constexpr int kMaxFilterWords = 16384;  // per image
-constexpr int kScanThreads = 1024; // k_scan and k_finalize are one workgroup each
+constexpr int kScanThreads = 1024; // k_scan is one workgroup
 constexpr int kMaxGateBlocks = 1024;
 constexpr int kMaxRanges = 16384;  // kMaxGateBlocks x up to 16 waves (one range per gate wave)
 constexpr int kApplyThreads = 1024;  // budget-walk workgroups (k_spikes, k_claim, k_apply)
@@ -28,7 +28,7 @@ constexpr uint32_t kChunkSlotDiv = 128; // chunk_cnt index = (region + c * kChun
 
 // Per-pass bookkeeping in device memory (one per handle).
 struct alignas(16) PassWork {
-    uint32_t t0_g2;        // global event 0 passed both gates this pass (re-armed by k_finalize)
+    uint32_t t0_g2;        // global event 0 passed both gates this pass (re-armed by finalize_pass)
     uint32_t ticket;       // k_apply workgroups done this pass (the last one finalizes, re-arms it)
     uint32_t pad[2];
     abnn_stats stats;      // host-kept counters (grown); the device ones live in DeviceState::wg_stats
@@ -67,7 +67,8 @@ struct DeviceState {
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     PassWork* work;
     uint64_t* wave_clock;     // [4 * n_ranges] per-wave gate times {start, stream done, end, hw id} (100 MHz)
-    uint32_t* range_bounds;   // [n_ranges + 1] first iteration of each range (adaptive, k_finalize)
+    uint32_t* range_bounds;   // [n_ranges + 1] first iteration of each range (this pass)
+    uint32_t* range_bounds_next;  // [n_ranges + 1] the next pass's (adapt_partition in k_apply; the host swaps)
     uint32_t adapt_ranges;    // rebalance the partition after every pass (default on; ABNN_STATIC_RANGES=1: off)
     uint64_t n_syn;           // local records
     uint64_t n_nrn;

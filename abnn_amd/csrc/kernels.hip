@@ -555,7 +555,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     const uint4 c = refrac_chunk<kChunk / 64, kRandom>(d, kp, region, tb, pend, now, pass, stage_at);
     if (lane == 0) {
         d.range_info[r] = make_uint4(tot.x + c.x, tot.y + c.y, tot.z + c.z, nch);
-        // this wave's gate time drives the next pass's partition (finalize_pass);
+        // this wave's gate time drives the next pass's partition (adapt_partition);
         // 100 MHz wall clock
         d.wave_clock[4 * r] = t_start;
         d.wave_clock[4 * r + 1] = t_stream;
@@ -743,43 +743,57 @@ __device__ void stamp_gathered(const DeviceState& d, const KernelParams& kp, con
 }
 
 // The end of a pass, by the last k_apply workgroup (every other one has read
-// the pass-start scalars and is done with the partition): rBar
-// (brain.metal:110-113), clock tick (brain.metal:129) and the next pass's
-// sweep partition.  Equal ranges do not finish together: a wave's stream rate
-// depends on how the SIMD arbiter treats it (the gate rotates priorities) and
-// dense parts of the graph stage more events.  So range r's measured gate time
-// (wave_clock), spread evenly over its iterations, gives a cumulative cost
-// curve, and boundary k moves halfway from its old place towards the
-// iteration where the curve reaches k / NR of the total.  Results do not
-// depend on the partition (event order is global, C1).
+// the pass-start scalars): rBar (brain.metal:110-113), clock tick
+// (brain.metal:129).
 __device__ void finalize_pass(const DeviceState& d, const KernelParams& kp, const int32_t* gathered, uint32_t world,
-                              uint64_t now, float R, float rbar, uint64_t pass, uint32_t* s_lds)
+                              uint64_t now, float R, float rbar, uint64_t pass)
+{
+    if (threadIdx.x != 0) return;
+    uint64_t events = d.events;
+    int64_t t0 = d.work->t0_g2;
+    if (gathered) {
+        const uint32_t words = xchg_words(kp.max_spikes);
+        events = 0;
+        t0 = 0;
+        for (uint32_t r = 0; r < world; ++r) {
+            const int64_t* sm = reinterpret_cast<const int64_t*>(gathered + r * words);
+            events += (uint64_t)sm[2];
+            t0 |= sm[1];
+        }
+    }
+    if (t0 != 0 && kp.max_spikes > 0)
+        *d.rbar = rbar + kp.alpha_rbar * (R - rbar);  // brain.metal:110-113
+    if (events > 0) *d.clock = now + kp.clock_inc;     // brain.metal:129
+    *d.pass_index = pass + 1;
+    d.work->t0_g2 = 0;  // re-armed for the next pass
+    __hip_atomic_store((gu32*)(&d.work->ticket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The next pass's sweep partition, computed by every k_apply workgroup for its
+// own slice of boundaries and written into the other bounds buffer
+// (range_bounds_next; the host swaps the two after the launch), so no
+// workgroup waits for another.  Equal ranges do not finish together: a wave's
+// stream rate depends on how the SIMD arbiter treats it (the gate rotates
+// priorities) and dense parts of the graph (the input->output block: every
+// event pre-gated) stage more events.  So range r's measured gate time
+// (wave_clock, written by this pass's gate: start to stream done, full chunks
+// included; the last chunk's refractory stage after the stream costs every
+// wave about the same and would bias short ranges), spread evenly over its
+// iterations, gives a cumulative cost curve, and boundary k moves halfway from
+// its old place towards the iteration where the curve reaches k / NR of the
+// total.  Results do not depend on the partition (event order is global, C1).
+__device__ void adapt_partition(const DeviceState& d, uint32_t* s_lds)
 {
     constexpr uint32_t NWv = kApplyThreads / 64, kRound = 4;
     __shared__ uint32_t s_w[NWv];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, NR = d.n_ranges;
-    if (tid == 0) {
-        uint64_t events = d.events;
-        int64_t t0 = d.work->t0_g2;
-        if (gathered) {
-            const uint32_t words = xchg_words(kp.max_spikes);
-            events = 0;
-            t0 = 0;
-            for (uint32_t r = 0; r < world; ++r) {
-                const int64_t* sm = reinterpret_cast<const int64_t*>(gathered + r * words);
-                events += (uint64_t)sm[2];
-                t0 |= sm[1];
-            }
-        }
-        if (t0 != 0 && kp.max_spikes > 0)
-            *d.rbar = rbar + kp.alpha_rbar * (R - rbar);  // brain.metal:110-113
-        if (events > 0) *d.clock = now + kp.clock_inc;     // brain.metal:129
-        *d.pass_index = pass + 1;
-        d.work->t0_g2 = 0;  // re-armed for the next pass
-        __hip_atomic_store((gu32*)(&d.work->ticket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // this workgroup's boundaries k in [k0, k1); bounds 0 and NR never move
+    const uint32_t slice = (NR + 1 + gridDim.x - 1) / gridDim.x;
+    const uint32_t k0 = min(blockIdx.x * slice, NR + 1), k1 = min(k0 + slice, NR + 1);
+    if (!d.adapt_ranges || NR < 2) {  // workgroup-uniform: carry the bounds over
+        for (uint32_t k = k0 + tid; k < k1; k += kApplyThreads) d.range_bounds_next[k] = d.range_bounds[k];
+        return;
     }
-    // ---- the next pass's partition
-    if (!d.adapt_ranges || NR < 2) return;
     const uint32_t per = (NR + kApplyThreads - 1) / kApplyThreads, q0 = tid * per;
     uint32_t csum = 0;
     uint32_t rb[kMaxRanges / kApplyThreads], cost[kMaxRanges / kApplyThreads];
@@ -792,7 +806,7 @@ __device__ void finalize_pass(const DeviceState& d, const KernelParams& kp, cons
             b0[u] = d.range_bounds[q];
             b1[u] = d.range_bounds[q + 1];
             ts[u] = d.wave_clock[4 * q];
-            te[u] = d.wave_clock[4 * q + 2];
+            te[u] = d.wave_clock[4 * q + 1];  // stream done (the tail is ~constant per wave)
         }
 #pragma unroll
         for (uint32_t u = 0; u < kRound; ++u) {
@@ -834,20 +848,23 @@ __device__ void finalize_pass(const DeviceState& d, const KernelParams& kp, cons
         s_rb[NR] = d.iters;
     }
     __syncthreads();
-    if (total_cost == 0) return;
-    for (uint32_t k = tid + 1; k < NR; k += kApplyThreads) {
-        const uint32_t T = (uint32_t)((uint64_t)k * total_cost / NR);
-        uint32_t lo = 0, hi = NR;  // last range with s_cc <= T (its cost is > 0)
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_cc[mid] <= T) lo = mid;
-            else hi = mid;
+    for (uint32_t k = k0 + tid; k < k1; k += kApplyThreads) {
+        uint32_t nb = s_rb[k];
+        if (k > 0 && k < NR && total_cost > 0) {
+            const uint32_t T = (uint32_t)((uint64_t)k * total_cost / NR);
+            uint32_t lo = 0, hi = NR;  // last range with s_cc <= T (its cost is > 0)
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_cc[mid] <= T) lo = mid;
+                else hi = mid;
+            }
+            // integer floors keep the bounds monotonic in k (ranges never overlap)
+            const uint32_t cr = s_cc[lo + 1] - s_cc[lo];
+            const uint32_t target =
+                s_rb[lo] + (cr ? (uint32_t)((uint64_t)(T - s_cc[lo]) * (s_rb[lo + 1] - s_rb[lo]) / cr) : 0u);
+            nb = (target + s_rb[k]) >> 1;
         }
-        // integer floors keep the bounds monotonic in k (ranges never overlap)
-        const uint32_t cr = s_cc[lo + 1] - s_cc[lo];
-        const uint32_t target =
-            s_rb[lo] + (cr ? (uint32_t)((uint64_t)(T - s_cc[lo]) * (s_rb[lo + 1] - s_rb[lo]) / cr) : 0u);
-        d.range_bounds[k] = (target + s_rb[k]) >> 1;
+        d.range_bounds_next[k] = nb;
     }
 }
 
@@ -988,6 +1005,8 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     // budget order across ranks = global event order (brain.metal:125-126);
     // nothing of this kernel reads lastFired
     if (gathered) stamp_gathered(d, kp, gathered, world, now);
+    __syncthreads();  // the walk's LDS is reused
+    adapt_partition(d, s_lds);
     // statistics: every workgroup adds into its own slot (no cross-workgroup
     // sum; abnn_get_stats adds the slots)
     const uint32_t wu = wave_sum(upd), wf = wave_sum(nf), wp = wave_sum(npr);
@@ -1023,7 +1042,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
         s_last = ticket == gridDim.x - 1;
     }
     __syncthreads();
-    if (s_last) finalize_pass(d, kp, gathered, world, now, R, rb, pass, s_lds);
+    if (s_last) finalize_pass(d, kp, gathered, world, now, R, rb, pass);
 }
 
 // ---------------------------------------------------------------------------

@@ -4,7 +4,7 @@
 Runs config 3 for `warm` passes, then reads the last pass's per-wave clocks
 {start, stream done, end} (100 MHz s_memrealtime) and prints the spread of
 start, stream-end and end times, the tail (refractory stage) durations and the
-latest waves.  usage: ABNN_WAVE_CLOCK=1 python tools/wave_clock.py [passes]
+latest waves.  usage: ABNN_WAVE_CLOCK=1 python tools/wave_clock.py [passes [first printed]]
 """
 import ctypes
 import os
@@ -21,9 +21,12 @@ b = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, device=0)
 b.build_random_graph(1)
 b.set_auto_stimulus(0, wl.n_input)
 passes = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+first = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # print passes >= first
 for p in range(passes):
     b.encode_traversal(1)
     b.synchronize()
+    if p < first:
+        continue
     nr = 16384
     buf = np.zeros(4 * nr + 16, dtype=np.uint64)
     f = b._lib.abnn_debug_wave_clock
