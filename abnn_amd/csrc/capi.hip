@@ -98,12 +98,12 @@ void free_all(abnn_brain* b)
     void* ptrs[] = {b->d.syn.src,   b->d.syn.dst,    b->d.syn.w,
                     b->syn_alt.src, b->syn_alt.dst,  b->syn_alt.w,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
-                    b->d.bitmap,    b->d.filter,     b->d.range_info,    b->d.g2x,
+                    b->d.bitmap,    b->d.filter,     b->d.range_info,    b->d.range_g1,  b->d.g2x,
                     b->d.chunk_cnt,
                     b->d.wg_stats, b->d.claim,  b->d.g2src,      b->d.grown,
                     b->d.dead,      b->compact_offsets,
                     b->d.work,      b->idx_scratch,
-                    b->u64_scratch,  b->d.wave_clock,  b->d.range_bounds,  b->d.range_bounds_next,
+                    b->u64_scratch,  b->d.wave_clock,  b->d.apply_clock, b->d.range_bounds,  b->d.range_bounds_next,
                     const_cast<uint32_t*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -255,7 +255,7 @@ void configure(abnn_brain* b)
 }
 
 // Uniform sweep partition: range r starts at iteration floor(r * iters / NR)
-// (k_bitmap then adapts it pass by pass, adapt_partition).
+// (k_apply then adapts it pass by pass, partition_bounds).
 abnn_status reset_ranges(abnn_brain* b)
 {
     const DeviceState& d = b->d;
@@ -501,6 +501,10 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (per_cu > 4) per_cu = 4;
     b->cus = cus;
     b->per_cu = per_cu;
+    // partition A-B knobs: wave -> range map, adaptation gain
+    if (const char* env = std::getenv("ABNN_RANGE_MAP")) d.range_map = std::atoi(env) ? 1u : 0u;
+    d.adapt_gain = 2;
+    if (const char* env = std::getenv("ABNN_ADAPT_GAIN")) d.adapt_gain = (uint32_t)std::min(4, std::max(1, std::atoi(env)));
     configure(b);  // sweep partition for the creation size
     const uint64_t max_ranges = (uint64_t)std::min<int>(kMaxGateBlocks, cus * per_cu) * (gate_block / 64);
     d.n_bitmap_words = (uint32_t)(2 * ((n_nrn + 63) / 64));
@@ -522,6 +526,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.filter, 2 * kMaxFilterWords)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_info, max_ranges)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.range_g1, max_ranges)) != ABNN_OK) return fail(s);
     // per-range regions of refractory survivors (16 B per event: every event of
     // a range may pass in the warm-up passes)
     if ((s = dalloc(&d.g2x, iters * iter_events)) != ABNN_OK) return fail(s);
@@ -544,6 +549,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.wave_clock, 4 * (uint64_t)kMaxRanges + 16)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.apply_clock, 8 * (uint64_t)kWalkBlocks)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_bounds, max_ranges + 1)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_bounds_next, max_ranges + 1)) != ABNN_OK) return fail(s);
     d.adapt_ranges = std::getenv("ABNN_STATIC_RANGES") ? 0u : 1u;
@@ -836,6 +842,16 @@ abnn_status abnn_debug_wave_clock(abnn_brain* b, uint64_t* out, uint64_t n)
     REQUIRE(b && out, "null argument");
     ST_TRY(sync_all(b));
     HIP_TRY(hipMemcpy(out, b->d.wave_clock, std::min<uint64_t>(n, 4ull * kMaxRanges + 16) * 8, hipMemcpyDeviceToHost));
+    return ABNN_OK;
+}
+
+// Diagnostics (not part of abnn.h): the last k_apply's per-workgroup timeline,
+// 8 u64 per workgroup (see k_apply), 100 MHz ticks.
+abnn_status abnn_debug_apply_clock(abnn_brain* b, uint64_t* out, uint64_t n)
+{
+    REQUIRE(b && out, "null argument");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(out, b->d.apply_clock, std::min<uint64_t>(n, 8ull * kWalkBlocks) * 8, hipMemcpyDeviceToHost));
     return ABNN_OK;
 }
 

@@ -56,7 +56,8 @@ struct DeviceState {
     float* rbar;              // [1]
     uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
     uint32_t* filter;         // [2 * filter_words] the two folded bitmap images
-    uint4* range_info;        // [n_ranges] {pre-gated, passed refractory, candidates, chunks} per gate wave
+    uint4* range_info;        // [n_ranges] {gate time (40 ns), passed refractory, candidates, chunks} per gate wave
+    uint32_t* range_g1;       // [n_ranges] pre-gated events per gate wave (statistics)
     uint4* g2x;               // [iters * iter_events] per-range regions: {event - region, isi | cand << 31, w, dst}
     uint4* chunk_cnt;         // [iters * iter_events / kChunkSlotDiv + 8] {pre-gated, survivors, candidates, 0}
     const uint32_t* dummy;    // [kDummyRecords] zeros: target of the stream loads past a range
@@ -66,10 +67,13 @@ struct DeviceState {
     uint32_t* dead;           // pruning on: tombstones per kCompactChunk records (structural update)
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     PassWork* work;
-    uint64_t* wave_clock;     // [4 * n_ranges] per-wave gate times {start, stream done, end, hw id} (100 MHz)
+    uint64_t* wave_clock;     // [4 * n_ranges] per-wave gate times {start, stream done, end (100 MHz), quarter costs (4 x u16, 40 ns)}
+    uint64_t* apply_clock;    // [8 * kWalkBlocks] per-workgroup k_apply timeline (diagnostics, 100 MHz)
     uint32_t* range_bounds;   // [n_ranges + 1] first iteration of each range (this pass)
-    uint32_t* range_bounds_next;  // [n_ranges + 1] the next pass's (adapt_partition in k_apply; the host swaps)
+    uint32_t* range_bounds_next;  // [n_ranges + 1] the next pass's (partition_bounds in k_apply; the host swaps)
     uint32_t adapt_ranges;    // rebalance the partition after every pass (default on; ABNN_STATIC_RANGES=1: off)
+    uint32_t adapt_gain;      // a boundary moves adapt_gain / 4 of the way to its target (1..4, ABNN_ADAPT_GAIN; default 2)
+    uint32_t range_map;       // gate wave -> range: 0 blocked (workgroup b: ranges b*NW..), 1 interleaved (ABNN_RANGE_MAP=1)
     uint64_t n_syn;           // local records
     uint64_t n_nrn;
     uint32_t n_input;

@@ -25,7 +25,8 @@
 //                k_claim precedes it in random mode (highest event wins).
 //                Its last workgroup ends the pass: rBar EWMA
 //                (brain.metal:110-113), one clock tick (brain.metal:129),
-//                statistics, the next pass's partition.
+//                statistics; every workgroup also computes a slice of the
+//                next pass's partition.
 //   k_renorm   : brain.metal:135-145 with the base read once (no race).
 //   Sharded passes add k_scan + k_spikes (the exchange record) after the gate;
 //   k_apply then stamps every rank's spikes from the gathered records.
@@ -306,7 +307,8 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
 //   g2x entry       = {event - region, isi bits | candidate << 31, w bits, dst},
 //                     isi = (float)(now - lastFired[dst]) >= 0 (sign bit free),
 //                     w, dst as read at pass start (C1)
-//   range_info[r]   = {pre-gated, survivors, candidates, full chunks}, whole range
+//   range_info[r]   = {gate time, survivors, candidates, full chunks}, whole range;
+//   range_g1[r]     = its pre-gated events (statistics)
 //   chunk_cnt[slot] = {pre-gated, survivors, candidates, 0} of a full chunk;
 //                     slots of full chunks never collide; the last chunk holds
 //                     the range's survivors minus the full chunks'.
@@ -426,7 +428,10 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wid = wave_uniform(tid >> 6);
-    const uint32_t NR = gridDim.x * NW, r = blockIdx.x * NW + wid;
+    // range of this wave: blocked (a workgroup's waves sweep neighbouring
+    // ranges) or interleaved (neighbouring ranges on different CUs / XCDs, so
+    // a dense stretch of the graph does not land on one CU)
+    const uint32_t r = d.range_map ? wid * gridDim.x + blockIdx.x : blockIdx.x * NW + wid;
     const uint64_t it_begin = d.range_bounds[r], it_end = d.range_bounds[r + 1];  // adaptive partition
     const uint64_t region = it_begin * IE;
     const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
@@ -469,6 +474,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     }
     __syncthreads();
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    // clock checkpoints at the range's quarter iterations (diagnostics:
+    // where inside a range the time went, tools/wave_clock.py)
+    const uint64_t len = it_end - it_begin;
+    const uint64_t cp1 = it_begin + (len >> 2), cp2 = it_begin + (len >> 1), cp3 = it_begin + ((len * 3) >> 2);
+    uint64_t t1 = t_start, t2 = t_start, t3 = t_start;
 
     const uint32_t nn = (uint32_t)d.n_nrn;  // N_NRN < 2^32 (checked at create)
     uint32_t pend = 0, nch = 0;
@@ -495,6 +505,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     for (uint64_t it = it_begin; it < it_end; ++it) {
         uint32_t src[K];
         uint32_t dst[KD];
+        if (it == cp1) t1 = __builtin_amdgcn_s_memrealtime();
+        if (it == cp2) t2 = __builtin_amdgcn_s_memrealtime();
+        if (it == cp3) t3 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int k = 0; k < K; ++k) src[k] = nxs[k];
         // The SIMD arbiter issues strictly by priority, then age: with a fixed
@@ -554,13 +567,25 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     const uint64_t tb = region + (uint64_t)nch * kChunk;
     const uint4 c = refrac_chunk<kChunk / 64, kRandom>(d, kp, region, tb, pend, now, pass, stage_at);
     if (lane == 0) {
-        d.range_info[r] = make_uint4(tot.x + c.x, tot.y + c.y, tot.z + c.z, nch);
-        // this wave's gate time drives the next pass's partition (adapt_partition);
-        // 100 MHz wall clock
+        // this wave's gate time (start to stream done, full chunks included;
+        // the last chunk's refractory stage after the stream costs every wave
+        // about the same and would bias short ranges) drives the next pass's
+        // partition (partition_bounds): 40-ns units, clamped to [1, 0xFFFF],
+        // 0 for an empty range
+        const uint64_t gt = (t_stream - t_start) >> 2;
+        const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
+        d.range_info[r] = make_uint4(cost, tot.y + c.y, tot.z + c.z, nch);
+        d.range_g1[r] = tot.x + c.x;
+        // diagnostics (tools/wave_clock.py): 100 MHz wall clock
         d.wave_clock[4 * r] = t_start;
         d.wave_clock[4 * r + 1] = t_stream;
         d.wave_clock[4 * r + 2] = __builtin_amdgcn_s_memrealtime();
-        d.wave_clock[4 * r + 3] = __smid();
+        // the four quarters' stream times, 16 bits each in 40-ns units
+        auto q16 = [](uint64_t a, uint64_t b) -> uint64_t {
+            const uint64_t t = (b - a) >> 2;
+            return t > 0xFFFFu ? 0xFFFFu : t;
+        };
+        d.wave_clock[4 * r + 3] = q16(t_start, t1) | q16(t1, t2) << 16 | q16(t2, t3) << 32 | q16(t3, t_stream) << 48;
     }
 }
 
@@ -570,8 +595,10 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 // max_spikes spike candidates precede it in global event order.  Walked by
 // k_spikes, k_claim and k_apply alike.  Every workgroup first builds, in LDS,
 // per range: the capped exclusive candidate prefix, the exclusive prefix of
-// full chunks and the survivor count (one packed scan over range_info, a few
-// KB read from L2 -- cheaper than a separate single-workgroup scan launch).
+// full chunks and the survivor count (one packed scan over range_info, 64 KB
+// read from L2 per workgroup at 4096 ranges -- cheaper than a separate
+// single-workgroup scan launch, but L2-bandwidth-bound: every byte added per
+// range costs every workgroup).
 // The work items are the last chunk of every range and every full chunk, one
 // per wave at a time: an item adds the candidates of its range's lower full
 // chunks, leaves at once if the budget is spent, and otherwise visits its
@@ -579,7 +606,6 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 // budget position, g2x index) for each one whose position is below the budget.
 // A range without full chunks costs its item one global round trip (g2x).
 constexpr uint32_t kWalkWaves = kApplyThreads / 64;
-constexpr uint32_t kPrePerThread = kMaxRanges / kApplyThreads;
 
 struct WalkLds {
     uint32_t* pre;   // [NR]     min(off + candidates of ranges < r, budget)
@@ -592,50 +618,151 @@ __device__ __forceinline__ WalkLds walk_lds_view(uint32_t* s, uint32_t NR)
     return WalkLds{s, s + NR, s + 2 * NR + 1};
 }
 
-// Builds the WalkLds arrays; returns the number of full chunks.  With totals,
-// also the pass's pre-gated and survivor counts (every thread gets them).
+// The next pass's sweep partition (k_apply only; part = its LDS, else null),
+// computed from the same per-thread slice of ranges as the walk prefix, so
+// its loads share the prefix's round trip and its cost scan the prefix's
+// barriers.  Every k_apply workgroup then computes its own slice of boundaries
+// into the other bounds buffer (range_bounds_next; the host swaps the two
+// after the launch), so no workgroup waits for another.
+//
+// Equal ranges do not finish together: a wave's stream rate depends on how
+// the SIMD arbiter treats it (the gate rotates priorities) and dense parts of
+// the graph (the input->output block: every event pre-gated) stage more
+// events.  So range r's measured gate time (range_info[r].x, written by this
+// pass's gate), spread evenly over its iterations, gives a cumulative
+// cost curve, and boundary k moves adapt_gain / 4 of the way (default half)
+// from its old place towards the iteration where the curve reaches k / NR of
+// the total, rounded to the nearest iteration (a floor never moves a boundary
+// right by one iteration, and in the dense stretch one iteration is ~9 % of a
+// range).  Results do not depend on the partition (event order is global, C1).
+struct PartLds {
+    uint32_t* cc;  // [NR + 1] exclusive cumulative cost
+    uint32_t* rb;  // [NR + 1] current bounds
+};
+
+__device__ void partition_bounds(const DeviceState& d, const PartLds& P, uint32_t total_cost)
+{
+    const uint32_t NR = d.n_ranges;
+    // this workgroup's boundaries k in [k0, k1); bounds 0 and NR never move
+    const uint32_t slice = (NR + 1 + gridDim.x - 1) / gridDim.x;
+    const uint32_t k0 = min(blockIdx.x * slice, NR + 1), k1 = min(k0 + slice, NR + 1);
+    for (uint32_t k = k0 + threadIdx.x; k < k1; k += kApplyThreads) {
+        uint32_t nb = P.rb[k];
+        if (d.adapt_ranges && k > 0 && k < NR && total_cost > 0) {
+            const uint32_t T = (uint32_t)((uint64_t)k * total_cost / NR);
+            uint32_t lo = 0, hi = NR;  // last range with cc <= T (its cost is > 0)
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (P.cc[mid] <= T) lo = mid;
+                else hi = mid;
+            }
+            // target in 1/256 iterations; both terms of the move are monotonic
+            // in k, so ranges never overlap
+            const uint32_t cr = P.cc[lo + 1] - P.cc[lo];
+            const uint64_t tfp = (uint64_t)P.rb[lo] * 256u +
+                                 (cr ? (uint64_t)(T - P.cc[lo]) * (P.rb[lo + 1] - P.rb[lo]) * 256u / cr : 0u);
+            const uint32_t g = d.adapt_gain;
+            nb = (uint32_t)(((uint64_t)P.rb[k] * 256u * (4u - g) + tfp * g + 512u) >> 10);
+        }
+        d.range_bounds_next[k] = nb;
+    }
+}
+
+// Builds the WalkLds arrays (and, with part, the partition curve); returns the
+// number of full chunks.  With totals, also the pass's pre-gated and survivor
+// counts (every thread gets them).
 __device__ uint32_t walk_prefix(const DeviceState& d, uint64_t off, uint64_t budget, const WalkLds& L, uint64_t* s_red,
-                                uint64_t* tot_g1, uint64_t* tot_g2)
+                                uint64_t* tot_g1, uint64_t* tot_g2, const PartLds* part)
 {
     constexpr uint32_t kRound = 4;
+    __shared__ uint32_t s_cw[kApplyThreads / 64];
     const uint32_t NR = d.n_ranges, per = (NR + kApplyThreads - 1) / kApplyThreads, q0 = threadIdx.x * per;
-    uint64_t v[kPrePerThread];  // candidates | full chunks << 32
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const bool adapt = part && d.adapt_ranges && NR >= 2;  // workgroup-uniform
+    // pass 1: this thread's ranges' raw counts into LDS (pre = candidates,
+    // cpre = full chunks, cc = cost), their sums into registers; pass 2 turns
+    // its own LDS entries into exclusive prefixes in place (no per-range
+    // register arrays: k_apply runs at 128 VGPRs)
+    const bool totals = tot_g1 != nullptr;  // workgroup-uniform
     uint64_t sum = 0, g1 = 0, g2 = 0;
+    uint32_t csum = 0;
     for (uint32_t j0 = 0; j0 < per; j0 += kRound) {
         uint4 ri[kRound];
+        uint32_t b0[kRound], x1[kRound];
 #pragma unroll
-        for (uint32_t u = 0; u < kRound; ++u) ri[u] = range_totals(d, min(q0 + j0 + u, NR - 1));  // clamped
+        for (uint32_t u = 0; u < kRound; ++u) {
+            const uint32_t q = min(q0 + j0 + u, NR - 1);  // clamped: loads never depend on a branch
+            ri[u] = range_totals(d, q);
+            if (part) b0[u] = d.range_bounds[q];
+            if (totals) x1[u] = d.range_g1[q];
+        }
 #pragma unroll
         for (uint32_t u = 0; u < kRound; ++u) {
             const uint32_t j = j0 + u, q = q0 + j;
             const bool in = j < per && q < NR;
             const uint64_t x = in ? (uint64_t)ri[u].z | ((uint64_t)ri[u].w << 32) : 0u;
-            if (j < kPrePerThread) v[j] = x;
-            if (in) L.surv[q] = ri[u].y;
+            const uint32_t c = in && adapt ? ri[u].x : 0u;
+            if (in) {
+                L.pre[q] = ri[u].z;
+                L.cpre[q] = ri[u].w;
+                L.surv[q] = ri[u].y;
+                if (part) part->rb[q] = b0[u];
+                if (adapt) part->cc[q] = c;
+            }
             sum += x;
-            g1 += in ? ri[u].x : 0u;
-            g2 += in ? ri[u].y : 0u;
+            csum += c;
+            if (totals) {
+                g1 += in ? x1[u] : 0u;
+                g2 += in ? ri[u].y : 0u;
+            }
         }
     }
+    if (part && threadIdx.x == 0) d.apply_clock[8 * blockIdx.x + 4] = __builtin_amdgcn_s_memrealtime();
+    // the cost scan (DPP, u32: costs below 2^30) shares the prefix's barriers
+    const uint32_t cin = wave_incl_scan(csum);
+    if (lane == 63) s_cw[wv] = cin;
     uint64_t tot;
     uint64_t run = block_exclusive_scan<kApplyThreads>(sum, &tot, s_red);
     uint64_t cand = off + (uint32_t)run;
     uint32_t chunks = (uint32_t)(run >> 32);
+    uint32_t before = 0, total_cost = 0;
+    if (adapt) {
 #pragma unroll
-    for (uint32_t j = 0; j < kPrePerThread; ++j) {
-        if (j < per && q0 + j < NR) {
-            L.pre[q0 + j] = (uint32_t)(cand < budget ? cand : budget);
-            L.cpre[q0 + j] = chunks;
-            cand += (uint32_t)v[j];
-            chunks += (uint32_t)(v[j] >> 32);
+        for (uint32_t w = 0; w < kApplyThreads / 64; ++w) {
+            before += w < wv ? s_cw[w] : 0u;
+            total_cost += s_cw[w];
         }
     }
-    if (threadIdx.x == 0) L.cpre[NR] = (uint32_t)(tot >> 32);
-    if (tot_g1) {  // workgroup-uniform
-        *tot_g1 = block_sum<kApplyThreads>(g1, s_red);
-        *tot_g2 = block_sum<kApplyThreads>(g2, s_red);
+    uint32_t crun = before + cin - csum;
+    for (uint32_t q = q0; q < min(q0 + per, NR); ++q) {
+        const uint32_t nc = L.pre[q], nk = L.cpre[q];
+        L.pre[q] = (uint32_t)(cand < budget ? cand : budget);
+        L.cpre[q] = chunks;
+        cand += nc;
+        chunks += nk;
+        if (adapt) {
+            const uint32_t c = part->cc[q];
+            part->cc[q] = crun;
+            crun += c;
+        }
+    }
+    if (threadIdx.x == 0) {
+        L.cpre[NR] = (uint32_t)(tot >> 32);
+        if (part) {
+            part->cc[NR] = total_cost;
+            part->rb[NR] = d.iters;
+        }
+    }
+    if (totals) {  // LDS targets (a local's address would live in scratch)
+        const uint64_t a = block_sum<kApplyThreads>(g1, s_red), b = block_sum<kApplyThreads>(g2, s_red);
+        if (threadIdx.x == 0) {
+            *tot_g1 = a;
+            *tot_g2 = b;
+        }
     }
     __syncthreads();
+    if (part && threadIdx.x == 0) d.apply_clock[8 * blockIdx.x + 7] = __builtin_amdgcn_s_memrealtime();
+    if (part) partition_bounds(d, *part, adapt ? total_cost : 0u);
     return (uint32_t)(tot >> 32);
 }
 
@@ -653,13 +780,18 @@ __device__ __forceinline__ uint32_t chunk_range(const uint32_t* cpre, uint32_t N
 
 template <class F>
 __device__ void budget_walk(const DeviceState& d, uint64_t off, uint64_t budget, uint32_t* s_lds, uint64_t* s_red,
-                            F&& f, uint64_t* tot_g1 = nullptr, uint64_t* tot_g2 = nullptr)
+                            F&& f, uint64_t* tot_g1 = nullptr, uint64_t* tot_g2 = nullptr, uint64_t* tclock = nullptr,
+                            bool partition = false)
 {
     const uint32_t NR = d.n_ranges;
     const WalkLds L = walk_lds_view(s_lds, NR);
-    const uint32_t items = NR + walk_prefix(d, off, budget, L, s_red, tot_g1, tot_g2);
+    const PartLds P{s_lds + 3 * NR + 1, s_lds + 4 * NR + 2};
+    const uint32_t items = NR + walk_prefix(d, off, budget, L, s_red, tot_g1, tot_g2, partition ? &P : nullptr);
+    if (tclock && threadIdx.x == 0) *tclock = __builtin_amdgcn_s_memrealtime();
     const uint32_t lane = threadIdx.x & 63, w = wave_uniform(threadIdx.x >> 6);
-    for (uint32_t i = blockIdx.x * kWalkWaves + w; i < items; i += gridDim.x * kWalkWaves) {
+    // consecutive items on different workgroups: the ranges that hold the
+    // budget (the first ones) and the first full chunks spread over the chip
+    for (uint32_t i = w * gridDim.x + blockIdx.x; i < items; i += gridDim.x * kWalkWaves) {
         uint32_t r, c;
         if (i < NR) {
             r = i;
@@ -769,105 +901,6 @@ __device__ void finalize_pass(const DeviceState& d, const KernelParams& kp, cons
     __hip_atomic_store((gu32*)(&d.work->ticket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The next pass's sweep partition, computed by every k_apply workgroup for its
-// own slice of boundaries and written into the other bounds buffer
-// (range_bounds_next; the host swaps the two after the launch), so no
-// workgroup waits for another.  Equal ranges do not finish together: a wave's
-// stream rate depends on how the SIMD arbiter treats it (the gate rotates
-// priorities) and dense parts of the graph (the input->output block: every
-// event pre-gated) stage more events.  So range r's measured gate time
-// (wave_clock, written by this pass's gate: start to stream done, full chunks
-// included; the last chunk's refractory stage after the stream costs every
-// wave about the same and would bias short ranges), spread evenly over its
-// iterations, gives a cumulative cost curve, and boundary k moves halfway from
-// its old place towards the iteration where the curve reaches k / NR of the
-// total.  Results do not depend on the partition (event order is global, C1).
-__device__ void adapt_partition(const DeviceState& d, uint32_t* s_lds)
-{
-    constexpr uint32_t NWv = kApplyThreads / 64, kRound = 4;
-    __shared__ uint32_t s_w[NWv];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, NR = d.n_ranges;
-    // this workgroup's boundaries k in [k0, k1); bounds 0 and NR never move
-    const uint32_t slice = (NR + 1 + gridDim.x - 1) / gridDim.x;
-    const uint32_t k0 = min(blockIdx.x * slice, NR + 1), k1 = min(k0 + slice, NR + 1);
-    if (!d.adapt_ranges || NR < 2) {  // workgroup-uniform: carry the bounds over
-        for (uint32_t k = k0 + tid; k < k1; k += kApplyThreads) d.range_bounds_next[k] = d.range_bounds[k];
-        return;
-    }
-    const uint32_t per = (NR + kApplyThreads - 1) / kApplyThreads, q0 = tid * per;
-    uint32_t csum = 0;
-    uint32_t rb[kMaxRanges / kApplyThreads], cost[kMaxRanges / kApplyThreads];
-    for (uint32_t j0 = 0; j0 < per; j0 += kRound) {
-        uint32_t b0[kRound], b1[kRound];
-        uint64_t ts[kRound], te[kRound];
-#pragma unroll
-        for (uint32_t u = 0; u < kRound; ++u) {
-            const uint32_t q = min(q0 + j0 + u, NR - 1);  // clamped: loads never depend on a branch
-            b0[u] = d.range_bounds[q];
-            b1[u] = d.range_bounds[q + 1];
-            ts[u] = d.wave_clock[4 * q];
-            te[u] = d.wave_clock[4 * q + 1];  // stream done (the tail is ~constant per wave)
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kRound; ++u) {
-            const uint32_t j = j0 + u;
-            const bool in = j < per && q0 + j < NR;
-            // gate time of the range in 40-ns units, clamped (<= 2.6 ms)
-            const uint64_t t = (te[u] - ts[u]) >> 2;
-            const uint32_t c = in && b1[u] > b0[u] ? (uint32_t)(t < 1 ? 1 : (t > 0xFFFFu ? 0xFFFFu : t)) : 0u;
-            if (j < kMaxRanges / kApplyThreads) {
-                rb[j] = b0[u];
-                cost[j] = c;
-            }
-            csum += c;
-        }
-    }
-    // cost scan on DPP (u32: costs below 2^30)
-    const uint32_t cin = wave_incl_scan(csum);
-    if (lane == 63) s_w[wv] = cin;
-    __syncthreads();
-    uint32_t before = 0, total_cost = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < NWv; ++w) {
-        before += w < wv ? s_w[w] : 0u;
-        total_cost += s_w[w];
-    }
-    uint32_t* s_cc = s_lds;           // [NR + 1] exclusive cumulative cost (reuses the walk's LDS)
-    uint32_t* s_rb = s_lds + NR + 1;  // [NR + 1] current bounds
-    uint32_t run = before + cin - csum;
-#pragma unroll
-    for (uint32_t j = 0; j < kMaxRanges / kApplyThreads; ++j) {
-        if (j < per && q0 + j < NR) {
-            s_cc[q0 + j] = run;
-            s_rb[q0 + j] = rb[j];
-            run += cost[j];
-        }
-    }
-    if (tid == 0) {
-        s_cc[NR] = total_cost;
-        s_rb[NR] = d.iters;
-    }
-    __syncthreads();
-    for (uint32_t k = k0 + tid; k < k1; k += kApplyThreads) {
-        uint32_t nb = s_rb[k];
-        if (k > 0 && k < NR && total_cost > 0) {
-            const uint32_t T = (uint32_t)((uint64_t)k * total_cost / NR);
-            uint32_t lo = 0, hi = NR;  // last range with s_cc <= T (its cost is > 0)
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_cc[mid] <= T) lo = mid;
-                else hi = mid;
-            }
-            // integer floors keep the bounds monotonic in k (ranges never overlap)
-            const uint32_t cr = s_cc[lo + 1] - s_cc[lo];
-            const uint32_t target =
-                s_rb[lo] + (cr ? (uint32_t)((uint64_t)(T - s_cc[lo]) * (s_rb[lo + 1] - s_rb[lo]) / cr) : 0u);
-            nb = (target + s_rb[k]) >> 1;
-        }
-        d.range_bounds_next[k] = nb;
-    }
-}
-
 // ---------------------------------------------------------------------------
 // k_scan (sharded passes): this shard's exchange summary -- candidates capped
 // at the budget, the event-0-updated flag, events visited, refractory passes.
@@ -946,9 +979,13 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     __shared__ uint64_t s_now, s_pass;
     __shared__ float s_R, s_rb;
     __shared__ uint32_t s_last;
+    // per-workgroup timeline (diagnostics, abnn_debug_apply_clock): entry,
+    // scalars, walk prefix, walk done, partition, ticket, pass end
+    uint64_t* tc = d.apply_clock + 8 * blockIdx.x;
     // pass-start scalars (C1, brain.metal:105-106), read by one lane and used
     // through LDS only: the last workgroup rewrites them
     if (threadIdx.x == 0) {
+        tc[0] = __builtin_amdgcn_s_memrealtime();
         s_R = *d.reward;
         s_rb = *d.rbar;
         s_now = *d.clock;
@@ -958,12 +995,13 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     for (uint32_t i = blockIdx.x * kApplyThreads + threadIdx.x; i < 2 * d.filter_words; i += gridDim.x * kApplyThreads)
         d.filter[i] = 0u;
     __syncthreads();
+    if (threadIdx.x == 0) tc[1] = __builtin_amdgcn_s_memrealtime();
     const float R = s_R, rb = s_rb;
     const uint64_t now = s_now, pass = s_pass;
     const bool random = d.mode == ABNN_MODE_RANDOM, stamp = gathered == nullptr;
     const bool prune = kp.w_prune > 0.0f, genesis = d.grown != nullptr && kp.p_new > 0.0f;
     uint32_t upd = 0, nf = 0, npr = 0;
-    uint64_t g1 = 0, g2 = 0;
+    __shared__ uint64_t s_g1, s_g2;  // the pass's gate totals (workgroup 0)
     const bool first = blockIdx.x == 0;  // workgroup 0 also counts the pass's gate totals
     budget_walk(d, rank_offset(kp, gathered, rank), kp.max_spikes, s_lds, s_red,
                 [&](uint64_t region, const uint4& e, bool f, uint64_t pre, uint64_t slot) {
@@ -1000,13 +1038,12 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
                 }
             }
         }
-    }, first ? &g1 : nullptr, first ? &g2 : nullptr);
+    }, first ? &s_g1 : nullptr, first ? &s_g2 : nullptr, tc + 2, true);
     // sharded passes: every rank's spikes from the gathered exchange records,
     // budget order across ranks = global event order (brain.metal:125-126);
     // nothing of this kernel reads lastFired
     if (gathered) stamp_gathered(d, kp, gathered, world, now);
-    __syncthreads();  // the walk's LDS is reused
-    adapt_partition(d, s_lds);
+    if (threadIdx.x == 0) tc[3] = __builtin_amdgcn_s_memrealtime();
     // statistics: every workgroup adds into its own slot (no cross-workgroup
     // sum; abnn_get_stats adds the slots)
     const uint32_t wu = wave_sum(upd), wf = wave_sum(nf), wp = wave_sum(npr);
@@ -1031,8 +1068,8 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
         if (first) {
             x.passes += 1;
             x.events += d.events;
-            x.pre_gated += g1;
-            x.post_gated += g2;
+            x.pre_gated += s_g1;
+            x.post_gated += s_g2;
         }
         *st = x;
         // the last workgroup to arrive ends the pass; every workgroup's
@@ -1040,9 +1077,13 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
         const uint32_t ticket = __hip_atomic_fetch_add((gu32*)(&d.work->ticket), 1u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT);
         s_last = ticket == gridDim.x - 1;
+        tc[5] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
-    if (s_last) finalize_pass(d, kp, gathered, world, now, R, rb, pass);
+    if (s_last) {
+        finalize_pass(d, kp, gathered, world, now, R, rb, pass);
+        if (threadIdx.x == 0) tc[6] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1151,7 +1192,13 @@ __global__ __launch_bounds__(256) void k_stamp_list(DeviceState d, const uint32_
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
 // budget walks: WalkLds (three u32 per range; the finalizing workgroup reuses two)
-inline size_t walk_lds(const DeviceState& d) { return ((size_t)std::max(1u, d.n_ranges) + 1) * 12; }
+// dynamic LDS of the budget walk (k_spikes, k_claim): its prefix arrays;
+// k_apply adds the partition curve and bounds
+inline size_t walk_lds(const DeviceState& d, bool partition = false)
+{
+    const size_t nr = std::max(1u, d.n_ranges);
+    return (3 * nr + 1 + (partition ? 2 * (nr + 1) : 0)) * 4;
+}
 
 template <int BLOCK, int K, int FW>
 hipError_t launch_gate_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
@@ -1255,7 +1302,7 @@ hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int3
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_apply, g, b, walk_lds(d), s, d, kp, gathered, world, rank);
+    hipLaunchKernelGGL(k_apply, g, b, walk_lds(d, true), s, d, kp, gathered, world, rank);
     return hipGetLastError();
 }
 
