@@ -61,6 +61,20 @@ struct abnn_brain {
     uint64_t clock_host = 0;       // mirror, for the renormalisation decision (brain.cpp:127)
     uint64_t rng = 0;              // host RNG of inject_inputs
     uint64_t stim_first = 0, stim_count = 0;
+    // steady-state bitmap build by k_apply (build_next_ok): consecutive
+    // single-GPU passes whose spike lists are in fired_ring with no clock
+    // discontinuity, the highest lastFired value the host wrote (creation's
+    // zeros included), the stimulus of the last kFiredRing passes, whether
+    // the next pass's bitmap was built (and for which stimulus), borrowed
+    // state pointers handed out.  Bitmap and images are double-buffered by
+    // pass parity.
+    uint64_t clean_passes = 0, max_host_stamp = 0;
+    uint64_t stim_ring[kFiredRing][2] = {};
+    bool next_built = false;
+    uint64_t built_stim[2] = {};
+    bool ext_ptrs = false, force_full_bitmap = false;
+    uint32_t* bitmap_buf[2] = {};
+    uint32_t* filter_buf[2] = {};
     bool pending_renorm = false;   // shard protocol: decided at gate time
     int timing = 0;                // time every timing-th gate launch (0: off)
     uint64_t timing_count = 0;
@@ -98,12 +112,12 @@ void free_all(abnn_brain* b)
     void* ptrs[] = {b->d.syn.src,   b->d.syn.dst,    b->d.syn.w,
                     b->syn_alt.src, b->syn_alt.dst,  b->syn_alt.w,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
-                    b->d.bitmap,    b->d.filter,     b->d.range_info,    b->d.range_g1,  b->d.g2x,
+                    b->bitmap_buf[0], b->bitmap_buf[1], b->filter_buf[0], b->filter_buf[1], b->d.range_info,    b->d.range_g1,  b->d.g2x,
                     b->d.chunk_cnt,
                     b->d.wg_stats, b->d.claim,  b->d.g2src,      b->d.grown,
                     b->d.dead,      b->compact_offsets,
                     b->d.work,      b->idx_scratch,
-                    b->u64_scratch,  b->d.wave_clock,  b->d.apply_clock, b->d.range_bounds,  b->d.range_bounds_next,
+                    b->u64_scratch,  b->d.wave_clock,  b->d.apply_clock, b->d.fired_ring, b->d.n_fired_ring, b->d.range_bounds,  b->d.range_bounds_next,
                     const_cast<uint32_t*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -325,11 +339,46 @@ abnn_status structural_update(abnn_brain* b)
     return reset_ranges(b);
 }
 
+// A host write to lastFired (or a clock change) up to `stamp`: the recent-spike
+// bitmap is rebuilt from all of lastFired (k_bitmap) until k_apply's build is
+// exact again.
+void state_written(abnn_brain* b, uint64_t stamp)
+{
+    b->clean_passes = 0;
+    b->max_host_stamp = std::max(b->max_host_stamp, stamp);
+    b->next_built = false;
+}
+
+// k_apply of pass p may build pass p+1's bitmap from the spike lists
+// (kernels.hip, build_next_lists) iff: the clock advances by one per pass; the
+// last window_pre - 1 passes were single-GPU passes after the last
+// discontinuity, so their spike lists are in fired_ring; and no value the
+// host wrote is recent at pass p+1 (clock >= max_host_stamp + window_pre).
+bool build_next_ok(const abnn_brain* b)
+{
+    const uint64_t W = b->params.window_pre;
+    return !b->ext_ptrs && !b->force_full_bitmap && b->params.clock_inc == 1 && W >= 1 && W < kFiredRing &&
+           b->clean_passes + 1 >= W && b->clock_host >= b->max_host_stamp + W;
+}
+
 // bitmap + streaming gate (with the refractory stage) [+ the exchange record
 // of a sharded pass]: the first half of every pass.
 abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
 {
-    HIP_TRY(launch_bitmap(b->d, b->kp, b->stim_first, b->stim_count, s));
+    DeviceState& d = b->d;
+    const uint64_t p = b->pass_host;
+    d.bitmap = b->bitmap_buf[p & 1];
+    d.filter = b->filter_buf[p & 1];
+    d.bitmap_next = b->bitmap_buf[(p + 1) & 1];
+    d.filter_next = b->filter_buf[(p + 1) & 1];
+    d.stim_first = b->stim_first;
+    d.stim_count = b->stim_count;
+    const bool prebuilt = !xchg_out && b->next_built && b->built_stim[0] == b->stim_first &&
+                          b->built_stim[1] == b->stim_count;
+    b->next_built = false;
+    if (!prebuilt) HIP_TRY(launch_bitmap(d, b->kp, b->stim_first, b->stim_count, s));
+    b->stim_ring[b->pass_host % kFiredRing][0] = b->stim_first;
+    b->stim_ring[b->pass_host % kFiredRing][1] = b->stim_count;
     EventPair* ev = nullptr;
     ST_TRY(time_begin(b, s, &ev));
     HIP_TRY(launch_gate(b->d, b->kp, s));
@@ -343,7 +392,25 @@ abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
 // (kernel arguments are captured at launch)
 abnn_status run_apply(abnn_brain* b, const int32_t* gathered, uint32_t world, uint32_t rank, hipStream_t s)
 {
-    HIP_TRY(launch_apply(b->d, b->kp, gathered, world, rank, s));
+    DeviceState& d = b->d;
+    d.build_next = !gathered && build_next_ok(b) ? 1u : 0u;
+    d.n_next_stim = 0;
+    if (d.build_next) {  // distinct stimulus ranges of passes p+1-W .. p+1 (p+1: the current one)
+        const uint64_t W = b->params.window_pre, p = b->pass_host;
+        auto add = [&](uint64_t f, uint64_t c) {
+            if (c == 0) return;
+            for (uint32_t r = 0; r < d.n_next_stim; ++r)
+                if (d.next_stim[r][0] == f && d.next_stim[r][1] == c) return;
+            d.next_stim[d.n_next_stim][0] = f;
+            d.next_stim[d.n_next_stim++][1] = c;
+        };
+        for (uint64_t q = p + 1 - W; q <= p; ++q) add(b->stim_ring[q % kFiredRing][0], b->stim_ring[q % kFiredRing][1]);
+        add(b->stim_first, b->stim_count);
+    }
+    HIP_TRY(launch_apply(d, b->kp, gathered, world, rank, s));
+    b->next_built = d.build_next != 0;
+    b->built_stim[0] = b->stim_first;
+    b->built_stim[1] = b->stim_count;
     std::swap(b->d.range_bounds, b->d.range_bounds_next);
     return ABNN_OK;
 }
@@ -352,8 +419,14 @@ abnn_status run_commit(abnn_brain* b, const int32_t* gathered, uint32_t world, b
                        hipStream_t s)
 {
     host_tick(b);
+    // sharded passes stamp from the gathered lists, not fired_ring
+    b->clean_passes = gathered ? 0 : b->clean_passes + 1;
     if (renorm) {  // renormalise_if_needed, brain.cpp:125-141; kernel brain.metal:135-145
         HIP_TRY(launch_renorm(b->d, b->clock_host, s));
+        const uint64_t base = b->clock_host;
+        b->max_host_stamp = b->max_host_stamp > base ? b->max_host_stamp - base : 0;
+        b->clean_passes = 0;  // the clock jumps back
+        b->next_built = false;
         b->clock_host = 0;
     }
     b->pass_host += 1;
@@ -523,8 +596,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.reward = reinterpret_cast<float*>(sb + 1);
     d.rbar = d.reward + 1;
     d.pass_index = sb + 2;
-    if ((s = dalloc(&d.bitmap, (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.filter, 2 * kMaxFilterWords)) != ABNN_OK) return fail(s);
+    for (int i = 0; i < 2; ++i) {
+        if ((s = dalloc(&b->bitmap_buf[i], (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
+        if ((s = dalloc(&b->filter_buf[i], 2 * kMaxFilterWords)) != ABNN_OK) return fail(s);
+    }
+    d.bitmap = b->bitmap_buf[0];
+    d.filter = b->filter_buf[0];
     if ((s = dalloc(&d.range_info, max_ranges)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_g1, max_ranges)) != ABNN_OK) return fail(s);
     // per-range regions of refractory survivors (16 B per event: every event of
@@ -550,6 +627,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.wave_clock, 4 * (uint64_t)kMaxRanges + 16)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.apply_clock, 8 * (uint64_t)kWalkBlocks)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.fired_ring, (uint64_t)kFiredRing * std::max(1u, p.max_spikes))) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.n_fired_ring, kFiredRing)) != ABNN_OK) return fail(s);
+    b->force_full_bitmap = std::getenv("ABNN_FULL_BITMAP") != nullptr;
     if ((s = dalloc(&d.range_bounds, max_ranges + 1)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_bounds_next, max_ranges + 1)) != ABNN_OK) return fail(s);
     d.adapt_ranges = std::getenv("ABNN_STATIC_RANGES") ? 0u : 1u;
@@ -585,6 +665,9 @@ abnn_status abnn_get_params(const abnn_brain* b, abnn_params* out)
 abnn_status abnn_state_ptrs(abnn_brain* b, abnn_state* out)
 {
     REQUIRE(b && out, "null argument");
+    // the caller may write lastFired or the clock behind the handle's back:
+    // rebuild the recent-spike bitmap from lastFired every pass from now on
+    b->ext_ptrs = true;
     out->syn_src = b->d.syn.src;
     out->syn_dst = b->d.syn.dst;
     out->syn_w = b->d.syn.w;
@@ -654,6 +737,7 @@ abnn_status abnn_set_last_fired(abnn_brain* b, uint64_t first, const uint64_t* s
     REQUIRE(first <= b->n_nrn && n <= b->n_nrn - first, "range out of bounds");
     ST_TRY(sync_all(b));
     HIP_TRY(hipMemcpy(b->d.last_fired + first, src, n * 8, hipMemcpyHostToDevice));
+    state_written(b, n ? *std::max_element(src, src + n) : 0);
     return ABNN_OK;
 }
 
@@ -684,6 +768,7 @@ abnn_status abnn_set_timestamps(abnn_brain* b, const uint32_t* idx, uint64_t n, 
     HIP_TRY(hipMemcpy(b->idx_scratch, idx, n * 4, hipMemcpyHostToDevice));
     HIP_TRY(launch_stamp_list(b->d, b->idx_scratch, n, nullptr, value, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    state_written(b, value);
     return ABNN_OK;
 }
 
@@ -710,6 +795,7 @@ abnn_status abnn_set_scalars(abnn_brain* b, const abnn_scalars* in)
     std::memcpy(reinterpret_cast<char*>(blk) + 12, &in->rbar, 4);
     blk[2] = in->pass_index;
     HIP_TRY(hipMemcpy(b->scalar_block, blk, sizeof(blk), hipMemcpyHostToDevice));
+    state_written(b, b->clock_host);  // every stamp so far is <= the old clock
     b->clock_host = in->clock;
     b->pass_host = in->pass_index;
     return ABNN_OK;
@@ -747,6 +833,7 @@ abnn_status abnn_inject_inputs(abnn_brain* b, const float* v, uint32_t n, float 
     // lastFired[i] = clock, read on the device
     HIP_TRY(launch_stamp_list(b->d, b->idx_scratch, idx.size(), b->d.clock, 0, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    state_written(b, b->clock_host);
     return ABNN_OK;
 }
 
@@ -852,6 +939,18 @@ abnn_status abnn_debug_apply_clock(abnn_brain* b, uint64_t* out, uint64_t n)
     REQUIRE(b && out, "null argument");
     ST_TRY(sync_all(b));
     HIP_TRY(hipMemcpy(out, b->d.apply_clock, std::min<uint64_t>(n, 8ull * kWalkBlocks) * 8, hipMemcpyDeviceToHost));
+    return ABNN_OK;
+}
+
+// Diagnostics (not part of abnn.h): the recent-spike bitmap of the last pass
+// (n_bitmap_words u32; bit i = neuron i was recent at that pass's start) and
+// whether k_apply built the next pass's (no k_bitmap launch).
+abnn_status abnn_debug_bitmap(abnn_brain* b, uint32_t* out, uint64_t n, int* incremental_next)
+{
+    REQUIRE(b && out, "null argument");
+    ST_TRY(sync_all(b));
+    HIP_TRY(hipMemcpy(out, b->d.bitmap, std::min<uint64_t>(n, b->d.n_bitmap_words) * 4, hipMemcpyDeviceToHost));
+    if (incremental_next) *incremental_next = b->next_built ? 1 : 0;
     return ABNN_OK;
 }
 
@@ -1108,6 +1207,7 @@ abnn_status abnn_load_flat(abnn_brain* b, const char* path)
         uint64_t* dst = arr == 0 ? b->d.last_fired : b->d.last_visited;
         if (ok && b->n_nrn)
             ok = hipMemcpy(dst, ts.data(), b->n_nrn * 8, hipMemcpyHostToDevice) == hipSuccess;
+        if (ok && arr == 0) state_written(b, b->n_nrn ? *std::max_element(ts.begin(), ts.end()) : 0);
     }
     std::fclose(f);
     if (!ok) {

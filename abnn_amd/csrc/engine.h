@@ -23,6 +23,7 @@ constexpr int kMaxApplyBlocks = kWalkBlocks;
 static_assert(kMaxApplyBlocks <= kApplyThreads, "the finalizing workgroup reads one apply partial per thread");
 static_assert(kMaxRanges % kApplyThreads == 0, "range prefix: whole ranges per thread");
 constexpr int kDummyRecords = 64 * 32;  // >= 64 lanes x max events per lane; also the record-buffer padding
+constexpr uint32_t kFiredRing = 8;     // spike lists kept (the bitmap build needs window_pre < kFiredRing)
 constexpr uint32_t kChunk = 384;        // pre-gated events per chunk (staged in LDS by a gate wave)
 constexpr uint32_t kChunkSlotDiv = 128; // chunk_cnt index = (region + c * kChunk) / 128 (unique per chunk)
 
@@ -54,8 +55,14 @@ struct DeviceState {
     uint64_t* pass_index;     // [1] passes run (keys the random-mode picks)
     float* reward;            // [1]
     float* rbar;              // [1]
-    uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap
-    uint32_t* filter;         // [2 * filter_words] the two folded bitmap images
+    uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap of this pass
+    uint32_t* filter;         // [2 * filter_words] the two folded bitmap images of this pass
+    uint32_t* bitmap_next;    // the next pass's (double-buffered by pass parity; zeroed by the gate)
+    uint32_t* filter_next;
+    uint64_t stim_first, stim_count;  // this pass's stimulus range (stamped `now` at pass start)
+    uint32_t build_next;      // k_apply builds bitmap_next / filter_next (steady state)
+    uint32_t n_next_stim;     // stimulus ranges of passes p+1-W..p+1 (distinct), for the build
+    uint64_t next_stim[kFiredRing][2];
     uint4* range_info;        // [n_ranges] {gate time (40 ns), passed refractory, candidates, chunks} per gate wave
     uint32_t* range_g1;       // [n_ranges] pre-gated events per gate wave (statistics)
     uint4* g2x;               // [iters * iter_events] per-range regions: {event - region, isi | cand << 31, w, dst}
@@ -68,6 +75,8 @@ struct DeviceState {
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     PassWork* work;
     uint64_t* wave_clock;     // [4 * n_ranges] per-wave gate times {start, stream done, end (100 MHz), quarter costs (4 x u16, 40 ns)}
+    uint32_t* fired_ring;     // [kFiredRing * max_spikes] spike list of pass q at (q % kFiredRing), budget order
+    uint32_t* n_fired_ring;   // [kFiredRing] their lengths (k_apply workgroup 0)
     uint64_t* apply_clock;    // [8 * kWalkBlocks] per-workgroup k_apply timeline (diagnostics, 100 MHz)
     uint32_t* range_bounds;   // [n_ranges + 1] first iteration of each range (this pass)
     uint32_t* range_bounds_next;  // [n_ranges + 1] the next pass's (partition_bounds in k_apply; the host swaps)

@@ -7,7 +7,9 @@
 //   k_bitmap   : lastFired (u64, 8 B/neuron, read once) -> exact recent-spike
 //                bitmap, bit i = (now - lastFired[i]) <= WINDOW_PRE, OR-folded
 //                into the two LDS filter images; the per-pass stimulus stamp
-//                is fused here.
+//                is fused here.  Only after host writes and in the first
+//                passes: in steady state k_apply builds the next pass's bitmap
+//                from the last passes' spike lists (one pass = two launches).
 //   k_gate     : THE streaming kernel.  Persistent workgroups whose waves each
 //                sweep one contiguous range of events (adaptive partition),
 //                loading only the src word of every record (4 B per event).
@@ -294,6 +296,83 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
 }
 
 // ---------------------------------------------------------------------------
+// Steady state: the next pass's bitmap and filter images are
+// built by k_apply instead of k_bitmap.  With the clock advancing by one per
+// pass and no host-written stamp recent (the host checks, capi.hip
+// build_next_ok), neuron n is recent at pass p+1 iff it was stamped by a spike
+// of passes p+1-W..p (the spike lists: fired_ring, and this pass's spikes as
+// k_apply stamps them) or by the stimulus of passes p+1-W..p+1 (W =
+// window_pre).  Both buffers of pass p+1 were zeroed by the gate of pass p,
+// so the build only sets bits: the order of the word atomics does not matter.
+__device__ __forceinline__ void recent_set_next_word(const DeviceState& d, uint32_t j, uint32_t bits)
+{
+    const uint32_t FW = d.filter_words, lg = d.filter_log2;
+    atomicOr(d.bitmap_next + j, bits);
+    atomicOr(d.filter_next + filter_word1(j, FW), bits);
+    atomicOr(d.filter_next + FW + filter_word2(j, FW, lg), bits);
+}
+
+// Wave-converged form: the lanes with act set neuron n.  The spike lists
+// repeat neurons (a neuron fires from many synapses, and the dense
+// input->output block makes the 256 outputs fire over and over in the first
+// passes), and same-address atomics serialise (~12 ns each): the lanes that
+// share the first active lane's bitmap word are merged into one set of three
+// atomics, for up to kMerge rounds while merging pays (a group of one ends it).
+__device__ __forceinline__ void wave_set_next(const DeviceState& d, bool act, uint32_t n)
+{
+    constexpr int kMerge = 8;
+    const uint32_t lane = threadIdx.x & 63, j = n >> 5;
+    for (int it = 0; it < kMerge; ++it) {
+        const uint64_t m = __ballot(act);
+        if (m == 0) return;
+        const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+        const uint32_t jl = (uint32_t)__builtin_amdgcn_readlane((int)j, (int)lead);
+        const bool same = act && j == jl;
+        const uint64_t g = __ballot(same);
+        if (__popcll(g) == 1) break;  // no repeats at the head: plain atomics
+        uint32_t bits = same ? 1u << (n & 31u) : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) bits |= __shfl_xor(bits, o, 64);
+        if (lane == lead) recent_set_next_word(d, jl, bits);
+        act = act && !same;
+    }
+    if (act) recent_set_next_word(d, j, 1u << (n & 31u));
+}
+
+// The items of the build that do not depend on this pass: the spike lists of
+// passes p+1-W..p-1 and the stimulus ranges.  Item x of k_apply thread t of
+// workgroup g is x = t * gridDim + g (every workgroup gets a few), its loads
+// issued at kernel entry (next_item_load, both at once: the list entry is read
+// whether or not it is below the list's length) so they land during the walk
+// prefix; the atomics follow the walk (next_item_set).  Items beyond one per
+// thread (more than 256 K) are walked after it.
+struct NextItem {
+    uint32_t n, lim, i;  // neuron; valid iff i < lim
+};
+
+__device__ __forceinline__ uint64_t next_items(const DeviceState& d, const KernelParams& kp)
+{
+    const uint32_t W = kp.window_pre, nl = W > 0 ? W - 1 : 0;
+    uint64_t items = (uint64_t)nl * kp.max_spikes;
+    for (uint32_t r = 0; r < d.n_next_stim; ++r) items += d.next_stim[r][1];
+    return items;
+}
+
+__device__ __forceinline__ NextItem next_item_load(const DeviceState& d, const KernelParams& kp, uint64_t pass, uint64_t x)
+{
+    const uint32_t M = kp.max_spikes, W = kp.window_pre, nl = W > 0 ? W - 1 : 0;
+    if (x < (uint64_t)nl * M) {
+        const uint32_t k = (uint32_t)(x / M), i = (uint32_t)(x - (uint64_t)k * M);
+        const uint64_t q = (pass - nl + k) & (kFiredRing - 1);  // passes p+1-W .. p-1
+        return NextItem{d.fired_ring[q * M + i], d.n_fired_ring[q], i};
+    }
+    uint64_t y = x - (uint64_t)nl * M;
+    uint32_t r = 0;
+    while (y >= d.next_stim[r][1]) y -= d.next_stim[r++][1];
+    return NextItem{(uint32_t)(d.next_stim[r][0] + y), 1u, 0u};
+}
+
+// ---------------------------------------------------------------------------
 // Per-range results of the gate.  A range is the contiguous block of events
 // one gate wave sweeps; range order = event order.  Events that pass the LDS
 // filter are staged as {offset, src} and cut, in event order, into chunks of
@@ -366,7 +445,10 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
             w[j] = g1 ? d.syn.w[ri] : 0.0f;
         }
 #pragma unroll
-        for (int j = 0; j < R; ++j) ld[j] = dst[j] < nn ? d.last_fired[dst[j]] : 0ull;
+        // the stimulus of this pass is stamped `now` (brain.cpp:82) by k_bitmap
+        // or, in steady state, by the gate itself at some point of the pass
+        for (int j = 0; j < R; ++j)
+            ld[j] = dst[j] - d.stim_first < d.stim_count ? now : (dst[j] < nn ? d.last_fired[dst[j]] : 0ull);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             if (b0 + (uint32_t)j * 64 >= n) break;  // wave-uniform
@@ -471,6 +553,16 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             l1[i] = f[i];
             l2[i] = f[FW / 4 + i];
         }
+        // the next pass's bitmap and images are zeroed here (k_apply or
+        // k_bitmap builds them), a slice per workgroup; this pass's stimulus
+        // is stamped by workgroup 0 (the refractory stage reads it as now)
+        const uint32_t nz = d.n_bitmap_words + 2 * FW, per = (nz + gridDim.x - 1) / gridDim.x;
+        for (uint32_t i = blockIdx.x * per + tid; i < min(nz, (blockIdx.x + 1) * per); i += BLOCK) {
+            if (i < d.n_bitmap_words) d.bitmap_next[i] = 0u;
+            else d.filter_next[i - d.n_bitmap_words] = 0u;
+        }
+        if (blockIdx.x == 0)
+            for (uint64_t i = tid; i < d.stim_count; i += BLOCK) d.last_fired[d.stim_first + i] = now;
     }
     __syncthreads();
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -672,7 +764,7 @@ __device__ void partition_bounds(const DeviceState& d, const PartLds& P, uint32_
 // number of full chunks.  With totals, also the pass's pre-gated and survivor
 // counts (every thread gets them).
 __device__ uint32_t walk_prefix(const DeviceState& d, uint64_t off, uint64_t budget, const WalkLds& L, uint64_t* s_red,
-                                uint64_t* tot_g1, uint64_t* tot_g2, const PartLds* part)
+                                uint64_t* tot_g1, uint64_t* tot_g2, const PartLds* part, uint64_t* tot_cand)
 {
     constexpr uint32_t kRound = 4;
     __shared__ uint32_t s_cw[kApplyThreads / 64];
@@ -747,6 +839,7 @@ __device__ uint32_t walk_prefix(const DeviceState& d, uint64_t off, uint64_t bud
         }
     }
     if (threadIdx.x == 0) {
+        if (tot_cand) *tot_cand = off + (uint32_t)tot;  // candidates before and in this shard
         L.cpre[NR] = (uint32_t)(tot >> 32);
         if (part) {
             part->cc[NR] = total_cost;
@@ -778,15 +871,22 @@ __device__ __forceinline__ uint32_t chunk_range(const uint32_t* cpre, uint32_t N
     return lo;
 }
 
-template <class F>
+struct NoWaveHook {
+    __device__ void operator()(bool, const uint4&) const {}
+};
+
+// f(region, entry, candidate, budget position, g2x index) per visited event;
+// h(visited and a candidate, entry) by the whole wave after every round.
+template <class F, class H = NoWaveHook>
 __device__ void budget_walk(const DeviceState& d, uint64_t off, uint64_t budget, uint32_t* s_lds, uint64_t* s_red,
-                            F&& f, uint64_t* tot_g1 = nullptr, uint64_t* tot_g2 = nullptr, uint64_t* tclock = nullptr,
-                            bool partition = false)
+                            F&& f, H h = H{}, uint64_t* tot_g1 = nullptr, uint64_t* tot_g2 = nullptr, uint64_t* tclock = nullptr,
+                            bool partition = false, uint64_t* tot_cand = nullptr)
 {
     const uint32_t NR = d.n_ranges;
     const WalkLds L = walk_lds_view(s_lds, NR);
     const PartLds P{s_lds + 3 * NR + 1, s_lds + 4 * NR + 2};
-    const uint32_t items = NR + walk_prefix(d, off, budget, L, s_red, tot_g1, tot_g2, partition ? &P : nullptr);
+    const uint32_t items =
+        NR + walk_prefix(d, off, budget, L, s_red, tot_g1, tot_g2, partition ? &P : nullptr, tot_cand);
     if (tclock && threadIdx.x == 0) *tclock = __builtin_amdgcn_s_memrealtime();
     const uint32_t lane = threadIdx.x & 63, w = wave_uniform(threadIdx.x >> 6);
     // consecutive items on different workgroups: the ranges that hold the
@@ -834,6 +934,7 @@ __device__ void budget_walk(const DeviceState& d, uint64_t off, uint64_t budget,
             const uint64_t bc = __ballot(cand);
             const uint64_t pre = P + mbcnt64(bc);  // spike candidates before this event
             if (v && pre < budget) f(region, e[j], cand, pre, base + j * 64 + lane);
+            h(cand && pre < budget, e[j]);
             P += (uint64_t)__popcll(bc);
         }
     }
@@ -991,9 +1092,6 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
         s_now = *d.clock;
         s_pass = *d.pass_index;
     }
-    // every gate workgroup has its copy of the filter image: zero it for the next k_bitmap
-    for (uint32_t i = blockIdx.x * kApplyThreads + threadIdx.x; i < 2 * d.filter_words; i += gridDim.x * kApplyThreads)
-        d.filter[i] = 0u;
     __syncthreads();
     if (threadIdx.x == 0) tc[1] = __builtin_amdgcn_s_memrealtime();
     const float R = s_R, rb = s_rb;
@@ -1002,7 +1100,12 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     const bool prune = kp.w_prune > 0.0f, genesis = d.grown != nullptr && kp.p_new > 0.0f;
     uint32_t upd = 0, nf = 0, npr = 0;
     __shared__ uint64_t s_g1, s_g2;  // the pass's gate totals (workgroup 0)
+    __shared__ uint64_t s_cand;      // spike candidates up to and including this shard
     const bool first = blockIdx.x == 0;  // workgroup 0 also counts the pass's gate totals
+    // the next pass's bitmap build (steady state): this thread's first item, loads in flight
+    const uint64_t nitems = d.build_next ? next_items(d, kp) : 0;
+    const uint64_t x0 = (uint64_t)threadIdx.x * gridDim.x + blockIdx.x, xs = (uint64_t)gridDim.x * kApplyThreads;
+    const NextItem it0 = x0 < nitems ? next_item_load(d, kp, pass, x0) : NextItem{0u, 0u, 0u};
     budget_walk(d, rank_offset(kp, gathered, rank), kp.max_spikes, s_lds, s_red,
                 [&](uint64_t region, const uint4& e, bool f, uint64_t pre, uint64_t slot) {
         const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.y & 0x7FFFFFFFu));
@@ -1026,7 +1129,10 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
         }
         ++upd;
         if (f) {
-            if (stamp) d.last_fired[e.w] = now;  // brain.metal:125-126
+            if (stamp) {
+                d.last_fired[e.w] = now;  // brain.metal:125-126
+                d.fired_ring[(pass & (kFiredRing - 1)) * kp.max_spikes + pre] = e.w;
+            }
             ++nf;
             if (genesis) {  // README §5 synaptogenesis: slot `pre` of this pass
                 const uint64_t x = splitmix64_at(d.seed ^ ABNN_GENESIS_KEY, (pass << 32) | pre);
@@ -1038,7 +1144,18 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
                 }
             }
         }
-    }, first ? &s_g1 : nullptr, first ? &s_g2 : nullptr, tc + 2, true);
+    }, [&](bool fired, const uint4& e) {  // this pass's spikes into the next pass's bitmap
+        if (d.build_next && stamp) wave_set_next(d, fired, e.w);
+    }, first ? &s_g1 : nullptr, first ? &s_g2 : nullptr, tc + 2, true, &s_cand);
+    wave_set_next(d, it0.i < it0.lim, it0.n);
+    const uint64_t xw = x0 - (uint64_t)(threadIdx.x & 63) * gridDim.x;  // the wave's lowest item (lane 0)
+    for (uint64_t k = xs; xw + k < nitems; k += xs) {  // wave-uniform
+        const NextItem it = x0 + k < nitems ? next_item_load(d, kp, pass, x0 + k) : NextItem{0u, 0u, 0u};
+        wave_set_next(d, it.i < it.lim, it.n);
+    }
+    // the spike list's length (positions below the budget)
+    if (stamp && first && threadIdx.x == 0)
+        d.n_fired_ring[pass & (kFiredRing - 1)] = (uint32_t)(s_cand < kp.max_spikes ? s_cand : kp.max_spikes);
     // sharded passes: every rank's spikes from the gathered exchange records,
     // budget order across ranks = global event order (brain.metal:125-126);
     // nothing of this kernel reads lastFired

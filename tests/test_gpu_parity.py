@@ -265,3 +265,59 @@ def test_config3_full_size_parity(gpu):
     assert g.scalars()["clock"] == o.clock
     st_g, st_o = g.stats(), o.stats()
     assert st_g == st_o
+
+
+def _bitmap(g):
+    import ctypes as C
+    nw = 2 * ((g.n_neuron() + 63) // 64)
+    out = np.zeros(nw, dtype=np.uint32)
+    inc = C.c_int(0)
+    f = g._lib.abnn_debug_bitmap
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_int)]
+    f.restype = C.c_int
+    assert f(g._h, out.ctypes.data, nw, C.byref(inc)) == 0
+    return out, bool(inc.value)
+
+
+def _expected_bitmap(last_fired_at_start, now, n_words, window=5):
+    bits = ((np.uint64(now) - last_fired_at_start.astype(np.uint64)) <= np.uint64(window)).astype(np.uint8)
+    bits = np.concatenate([bits, np.zeros(n_words * 32 - bits.size, np.uint8)])
+    return np.packbits(bits.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").ravel().astype(np.uint32)
+
+
+def test_recent_bitmap_update_with_host_writes(gpu):
+    """The steady-state bitmap (built by k_apply from the last passes' spike
+    lists) against the bitmap recomputed from lastFired every pass, and the
+    whole state against the oracle, across the host writes that force k_bitmap
+    rebuilds: set_timestamps, set_last_fired (recent and future values), a
+    clock jump."""
+    g, o = _pair(99_488, 1_000_000, 1_000_000)
+    modes = []
+    for k in range(34):
+        now = g.scalars()["clock"]
+        lf0 = g.last_fired()  # lastFired at pass start, host writes included
+        if k == 12:
+            g.set_timestamps([300, 5000, 77_000], now)
+            o.set_timestamps([300, 5000, 77_000], now)
+            lf0[[300, 5000, 77_000]] = now
+        if k == 18:
+            v = np.full(1000, now - 2, np.uint64)
+            v[::7] = now + 3  # not recent until the clock gets there
+            g.set_last_fired(v, 40_000)
+            o.last_fired[40_000:41_000] = v
+            lf0[40_000:41_000] = v
+        if k == 24:
+            sc = g.scalars()
+            g.set_scalars(sc["clock"] + 100, sc["reward"], sc["rbar"], sc["pass_index"])
+            so = o.scalars()
+            o.set_scalars(so["clock"] + 100, so["reward"], so["rbar"], so["pass_index"])
+            now += 100
+        lf0[:256] = now  # the stimulus is stamped at pass start
+        g.encode_traversal(1)
+        o.pass_threaded(nthreads=16)
+        bm, inc_next = _bitmap(g)
+        modes.append(inc_next)
+        assert np.array_equal(bm, _expected_bitmap(lf0, now, bm.size)), f"bitmap, pass {k}"
+        _assert_same(g, o, f"pass {k}")
+    assert all(modes[5:12]) and all(modes[28:]), modes  # built by k_apply before and after the writes
+    assert not any(modes[12:17]) and not any(modes[18:28]), modes
