@@ -67,7 +67,7 @@ class Scalars(C.Structure):
 
 
 MODE_SWEEP, MODE_RANDOM = 0, 1  # abnn_params.mode (include/abnn/abnn.h)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class Stats(C.Structure):
@@ -88,7 +88,8 @@ class Stats(C.Structure):
 
 class State(C.Structure):
     _fields_ = [
-        ("syn_src", C.c_void_p),
+        ("syn_src_lo", C.c_void_p),
+        ("syn_src_hi", C.c_void_p),
         ("syn_dst", C.c_void_p),
         ("syn_w", C.c_void_p),
         ("last_fired", C.c_void_p),

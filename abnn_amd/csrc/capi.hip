@@ -109,8 +109,8 @@ void free_all(abnn_brain* b)
 {
     if (!b) return;
     (void)hipSetDevice(b->device);
-    void* ptrs[] = {b->d.syn.src,   b->d.syn.dst,    b->d.syn.w,
-                    b->syn_alt.src, b->syn_alt.dst,  b->syn_alt.w,
+    void* ptrs[] = {b->d.syn.lo,    b->d.syn.hi,     b->d.syn.dst,    b->d.syn.w,
+                    b->syn_alt.lo,  b->syn_alt.hi,   b->syn_alt.dst,  b->syn_alt.w,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->bitmap_buf[0], b->bitmap_buf[1], b->filter_buf[0], b->filter_buf[1], b->d.range_info,    b->d.range_g1,  b->d.g2x,
                     b->d.chunk_cnt,
@@ -163,14 +163,22 @@ abnn_status ensure_idx_scratch(abnn_brain* b, uint64_t n)
     return ABNN_OK;
 }
 
-// Device records are three arrays (SynArrays); abnn_synapse is the host
-// interchange format.  Capacity `count` per array.
+// Device records are the packed src streams, dst and w (SynArrays, engine.h);
+// abnn_synapse is the host interchange format.  Capacity `count` records.
 abnn_status alloc_syn(SynArrays* a, uint64_t count)
 {
-    ST_TRY(dalloc(&a->src, count));
+    ST_TRY(dalloc(&a->lo, count));
+    ST_TRY(dalloc(&a->hi, hi_bytes(count)));
     ST_TRY(dalloc(&a->dst, count));
     return dalloc(&a->w, count);
 }
+
+// src values of records [first, first + m) <-> host u32 (interchange form),
+// through a device staging buffer and the pack / unpack kernels.
+struct SrcStage {
+    uint32_t* dev = nullptr;
+    ~SrcStage() { if (dev) (void)hipFree(dev); }
+};
 
 // Chunked copies between device arrays [first, first + n) and host records.
 constexpr uint64_t kXferRecs = 1u << 22;
@@ -179,12 +187,15 @@ abnn_status records_d2h(const SynArrays& a, uint64_t first, uint64_t n, abnn_syn
 {
     std::vector<uint32_t> s, t;
     std::vector<float> w;
+    SrcStage st;
+    if (n) ST_TRY(dalloc(&st.dev, std::min<uint64_t>(kXferRecs, n)));
     for (uint64_t i = 0; i < n; i += kXferRecs) {
         const uint64_t m = std::min<uint64_t>(kXferRecs, n - i);
         s.resize(m);
         t.resize(m);
         w.resize(m);
-        HIP_TRY(hipMemcpy(s.data(), a.src + first + i, m * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(launch_unpack_src(a, st.dev, first + i, m, nullptr));
+        HIP_TRY(hipMemcpy(s.data(), st.dev, m * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(t.data(), a.dst + first + i, m * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(w.data(), a.w + first + i, m * 4, hipMemcpyDeviceToHost));
         for (uint64_t k = 0; k < m; ++k) out[i + k] = {s[k], t[k], w[k], 0.0f};
@@ -196,6 +207,8 @@ abnn_status records_h2d(const SynArrays& a, uint64_t first, uint64_t n, const ab
 {
     std::vector<uint32_t> s, t;
     std::vector<float> w;
+    SrcStage st;
+    if (n) ST_TRY(dalloc(&st.dev, std::min<uint64_t>(kXferRecs, n)));
     for (uint64_t i = 0; i < n; i += kXferRecs) {
         const uint64_t m = std::min<uint64_t>(kXferRecs, n - i);
         s.resize(m);
@@ -206,7 +219,9 @@ abnn_status records_h2d(const SynArrays& a, uint64_t first, uint64_t n, const ab
             t[k] = in[i + k].dst;
             w[k] = in[i + k].w;
         }
-        HIP_TRY(hipMemcpy(a.src + first + i, s.data(), m * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(st.dev, s.data(), m * 4, hipMemcpyHostToDevice));
+        HIP_TRY(launch_pack_src(a, st.dev, first + i, m, nullptr));
+        HIP_TRY(hipDeviceSynchronize());  // the staging buffer is reused
         HIP_TRY(hipMemcpy(a.dst + first + i, t.data(), m * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(a.w + first + i, w.data(), m * 4, hipMemcpyHostToDevice));
     }
@@ -499,7 +514,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     *out = nullptr;
     REQUIRE(dims->n_input > 0 || dims->n_output > 0 || dims->n_hidden > 0, "no neurons");
     const uint64_t n_nrn = (uint64_t)dims->n_input + dims->n_output + dims->n_hidden;
-    REQUIRE(n_nrn <= 0xFFFFFFFFull, "N_NRN must fit u32 (SynapsePacked src/dst are u32)");
+    REQUIRE(n_nrn < kMaxNeurons, "N_NRN must be below 2^24 - 1 (src is held in 24 bits on the device, DESIGN.md 4)");
     abnn_params p;
     if (params) p = *params;
     else abnn_default_params(&p);
@@ -512,8 +527,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     REQUIRE(p.mode != ABNN_MODE_RANDOM || E < 0xFFFFFFFFull, "random mode: events per pass must fit u32");
     const bool genesis = p.p_new > 0.0f && p.compact_every > 0;
     // Gate kernel shape: threads per workgroup x events per lane x KiB per LDS
-    // filter image (ABNN_GATE="1024x8f32"; tuning knob, the default is the measured best).
-    uint32_t gate_block = 1024, gate_k = 8, filter_kib = 32;
+    // filter image (ABNN_GATE="1024x16f32"; tuning knob, the default is the measured best:
+    // profiles/r01s_shape_sweep.txt).
+    uint32_t gate_block = 1024, gate_k = 16, filter_kib = 32;
     if (const char* env = std::getenv("ABNN_GATE")) {
         unsigned gb = 0, gk = 0, fk = 0;
         const int got = std::sscanf(env, "%ux%uf%u", &gb, &gk, &fk);
@@ -578,6 +594,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (const char* env = std::getenv("ABNN_RANGE_MAP")) d.range_map = std::atoi(env) ? 1u : 0u;
     d.adapt_gain = 2;
     if (const char* env = std::getenv("ABNN_ADAPT_GAIN")) d.adapt_gain = (uint32_t)std::min(4, std::max(1, std::atoi(env)));
+    d.chunk_penalty = 25;  // 1 us per full chunk (~15 % of its refractory stage)
+    if (const char* env = std::getenv("ABNN_CHUNK_PENALTY")) d.chunk_penalty = (uint32_t)std::max(0, std::atoi(env));
     configure(b);  // sweep partition for the creation size
     const uint64_t max_ranges = (uint64_t)std::min<int>(kMaxGateBlocks, cus * per_cu) * (gate_block / 64);
     d.n_bitmap_words = (uint32_t)(2 * ((n_nrn + 63) / 64));
@@ -668,7 +686,8 @@ abnn_status abnn_state_ptrs(abnn_brain* b, abnn_state* out)
     // the caller may write lastFired or the clock behind the handle's back:
     // rebuild the recent-spike bitmap from lastFired every pass from now on
     b->ext_ptrs = true;
-    out->syn_src = b->d.syn.src;
+    out->syn_src_lo = b->d.syn.lo;
+    out->syn_src_hi = b->d.syn.hi;
     out->syn_dst = b->d.syn.dst;
     out->syn_w = b->d.syn.w;
     out->last_fired = b->d.last_fired;

@@ -35,16 +35,33 @@ struct alignas(16) PassWork {
     abnn_stats stats;      // host-kept counters (grown); the device ones live in DeviceState::wg_stats
 };
 
-// Synapse records on the device, structure of arrays: record i is
-// {src[i], dst[i], w[i]} (SynapsePacked without its never-read pad).  The
-// sweep's gate streams only src: 4 B per visited event instead of 16.  Each
-// array holds capacity + kDummyRecords entries (zero padding: the gate's last
-// iteration reads past the sweep).
+// Synapse records on the device, structure of arrays: record
+// i is {src[i], dst[i], w[i]} (SynapsePacked without its never-read pad).
+// src is held in 24 bits (N_NRN < 2^24 - 1, checked at create; the tombstone
+// src is kSrcNone) as two streams, so the sweep's gate reads 3 B per visited
+// event: lo[i] = bits 0..15 (u16, natural order) and hi = bits 16..23 (u8)
+// permuted within every 256-record group so that the one 4-B hi word a gate
+// lane loads per group holds the four records of its two lo words:
+//   group G = i / 256, r = i % 256, kh = r / 128, lane = (r % 128) / 2, s = r % 2
+//   hi byte at 256 G + 4 lane + 2 kh + s                           (hi_pos)
+// Each array holds capacity + kDummyRecords entries (zero padding: the gate's
+// last iteration reads past the sweep; hi rounded up to whole groups).
+constexpr uint32_t kSrcNone = 0xFFFFFFu;   // 24-bit tombstone src (downloads as 0xFFFFFFFF)
+constexpr uint64_t kMaxNeurons = kSrcNone; // N_NRN < 2^24 - 1
+
 struct SynArrays {
-    uint32_t* src;
+    uint16_t* lo;
+    uint8_t* hi;
     uint32_t* dst;
     float* w;
 };
+
+__host__ __device__ inline uint64_t hi_pos(uint64_t i)
+{
+    return (i & ~255ull) | ((i >> 1) & 63ull) << 2 | ((i >> 7) & 1ull) << 1 | (i & 1ull);
+}
+
+__host__ __device__ inline uint64_t hi_bytes(uint64_t count) { return (count + 255) & ~255ull; }
 
 // Kernel-facing view of a handle's device state.
 struct DeviceState {
@@ -74,7 +91,7 @@ struct DeviceState {
     uint32_t* dead;           // pruning on: tombstones per kCompactChunk records (structural update)
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     PassWork* work;
-    uint64_t* wave_clock;     // [4 * n_ranges] per-wave gate times {start, stream done, end (100 MHz), quarter costs (4 x u16, 40 ns)}
+    uint64_t* wave_clock;     // [4 * n_ranges] per-wave gate times {start, stream done, end, entry} (100 MHz, diagnostics)
     uint32_t* fired_ring;     // [kFiredRing * max_spikes] spike list of pass q at (q % kFiredRing), budget order
     uint32_t* n_fired_ring;   // [kFiredRing] their lengths (k_apply workgroup 0)
     uint64_t* apply_clock;    // [8 * kWalkBlocks] per-workgroup k_apply timeline (diagnostics, 100 MHz)
@@ -82,6 +99,7 @@ struct DeviceState {
     uint32_t* range_bounds_next;  // [n_ranges + 1] the next pass's (partition_bounds in k_apply; the host swaps)
     uint32_t adapt_ranges;    // rebalance the partition after every pass (default on; ABNN_STATIC_RANGES=1: off)
     uint32_t adapt_gain;      // a boundary moves adapt_gain / 4 of the way to its target (1..4, ABNN_ADAPT_GAIN; default 2)
+    uint32_t chunk_penalty;   // partition cost added per full chunk, 40-ns units (ABNN_CHUNK_PENALTY)
     uint32_t range_map;       // gate wave -> range: 0 blocked (workgroup b: ranges b*NW..), 1 interleaved (ABNN_RANGE_MAP=1)
     uint64_t n_syn;           // local records
     uint64_t n_nrn;
@@ -141,6 +159,8 @@ hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int3
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);
 // Structural update: stable compaction into `dst`, block b of kCompactChunk
 // records starting at offsets[b] (live counts from the k_apply tombstone tally).
+hipError_t launch_pack_src(const SynArrays& a, const uint32_t* in_dev, uint64_t first, uint64_t n, hipStream_t s);
+hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t first, uint64_t n, hipStream_t s);
 hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offsets, const SynArrays& dst,
                           hipStream_t s);
 hipError_t launch_generate(const DeviceState& d, uint32_t n_in, uint32_t n_out, uint64_t seed,

@@ -146,6 +146,21 @@ __device__ __forceinline__ uint64_t pick_record(uint64_t seed, uint64_t stream, 
     return __umul64hi(((uint64_t)x1 << 32) | x0, n_syn);
 }
 
+// The packed src of record i (engine.h, SynArrays): 24 bits, kSrcNone for a
+// tombstone; src32 widens it to the interchange value (0xFFFFFFFF).
+__device__ __forceinline__ uint32_t src_of(const SynArrays& a, uint64_t i)
+{
+    return (uint32_t)a.lo[i] | (uint32_t)a.hi[hi_pos(i)] << 16;
+}
+
+__device__ __forceinline__ uint32_t src32(uint32_t v) { return v == kSrcNone ? 0xFFFFFFFFu : v; }
+
+__device__ __forceinline__ void set_src(const SynArrays& a, uint64_t i, uint32_t v)
+{
+    a.lo[i] = (uint16_t)v;
+    a.hi[hi_pos(i)] = (uint8_t)(v >> 16);
+}
+
 // Record visited by local event t: itself (sweep, brain.metal:70) or its pick.
 __device__ __forceinline__ uint64_t rec_index(const DeviceState& d, uint64_t t, uint64_t pass)
 {
@@ -502,8 +517,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     constexpr int NW = BLOCK / 64;
     constexpr uint32_t IE = 64 * K;
     constexpr int KD = kTrack ? K : 1;                 // dst words in flight (track_visits)
+    constexpr int NG = K / 4;                          // sweep: 256-event groups per iteration
+    constexpr int KH = kRandom ? K : 1;                // random: hi bytes in flight
     constexpr uint32_t LG = __builtin_ctz(FW);
-    constexpr uint32_t SE = kChunk + 64;               // a chunk + one k-step
+    constexpr uint32_t SE = kChunk + 128;              // a chunk + one staging step (<= 128 events)
+    static_assert(K % 4 == 0, "the packed src stream is read in 256-event groups");
     static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
     __shared__ uint32_t s_f1[FW], s_f2[FW];
     __shared__ uint32_t s_off[NW][SE], s_src[NW][SE];
@@ -520,7 +538,13 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     uint32_t* st_off = s_off[wid];
     uint32_t* st_src = s_src[wid];
 
-    uint32_t nxs[K], nxd[KD];
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();  // diagnostics: the prologue
+    // Records in flight.  Sweep: the packed src stream (engine.h, SynArrays):
+    // per 256-event group g a lane holds two lo words (events 128 kh + 2 lane
+    // + {0, 1}, kh = 0, 1) and one hi word (the same four events' bits
+    // 16..23), 3 B per event.  Random mode: per event k (t = 64 k + lane) the
+    // lo half-word and the hi byte of its picked record.
+    uint32_t nxs[kRandom ? K : 2 * NG], nxh[kRandom ? KH : NG], nxd[KD];
     const uint64_t pass = kRandom ? *d.pass_index : 0;
     auto issue = [&](uint64_t it, bool live) {
         if constexpr (kRandom) {  // random-edge mode: a per-lane random record per event
@@ -529,18 +553,29 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 const uint64_t t = it * IE + k * 64 + lane;
                 const bool real = live && t < d.events;
                 const uint64_t e = real ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : 0;
-                nxs[k] = __builtin_nontemporal_load(real ? d.syn.src + e : d.dummy + (k * 64 + lane));
+                nxs[k] = __builtin_nontemporal_load(d.syn.lo + e);
+                nxh[k] = __builtin_nontemporal_load(d.syn.hi + hi_pos(e));
                 if constexpr (kTrack)
                     nxd[k] = __builtin_nontemporal_load(real ? d.syn.dst + e : d.dummy + (k * 64 + lane));
             }
         } else {
-            const uint32_t* bs = live ? d.syn.src + it * IE : d.dummy;  // wave-uniform
+            // wave-uniform bases; past the range the zero dummy block
+            const uint32_t* bl = live ? reinterpret_cast<const uint32_t*>(d.syn.lo) + it * (IE / 2) : d.dummy;
+            const uint32_t* bh = live ? reinterpret_cast<const uint32_t*>(d.syn.hi) + it * (IE / 4) : d.dummy;
 #pragma unroll
-            for (int k = 0; k < K; ++k) nxs[k] = __builtin_nontemporal_load(bs + k * 64 + lane);
-            if constexpr (kTrack) {
+            for (int g = 0; g < NG; ++g) {
+                nxs[2 * g] = __builtin_nontemporal_load(bl + g * 128 + lane);
+                nxs[2 * g + 1] = __builtin_nontemporal_load(bl + g * 128 + 64 + lane);
+                nxh[g] = __builtin_nontemporal_load(bh + g * 64 + lane);
+            }
+            if constexpr (kTrack) {  // dst of the same events: one 8-B word per (g, kh)
                 const uint32_t* bd = live ? d.syn.dst + it * IE : d.dummy;
 #pragma unroll
-                for (int k = 0; k < K; ++k) nxd[k] = __builtin_nontemporal_load(bd + k * 64 + lane);
+                for (int j = 0; j < 2 * NG; ++j) {
+                    const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(bd + j * 128) + lane);
+                    nxd[2 * j] = (uint32_t)v;
+                    nxd[2 * j + 1] = (uint32_t)(v >> 32);
+                }
             }
         }
     };
@@ -566,17 +601,13 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     }
     __syncthreads();
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    // clock checkpoints at the range's quarter iterations (diagnostics:
-    // where inside a range the time went, tools/wave_clock.py)
     const uint64_t len = it_end - it_begin;
-    const uint64_t cp1 = it_begin + (len >> 2), cp2 = it_begin + (len >> 1), cp3 = it_begin + ((len * 3) >> 2);
-    uint64_t t1 = t_start, t2 = t_start, t3 = t_start;
 
     const uint32_t nn = (uint32_t)d.n_nrn;  // N_NRN < 2^32 (checked at create)
     uint32_t pend = 0, nch = 0;
     uint4 tot = make_uint4(0u, 0u, 0u, 0u);
     auto stage_at = [&](uint32_t q) { return make_uint2(st_off[q], st_src[q]); };
-    // wave-uniform: a full chunk through the refractory stage now; the (< 64)
+    // wave-uniform: a full chunk through the refractory stage now; the (< 128)
     // entries past it move to the front of the stage
     auto chunk_out = [&]() {
         const uint4 c = refrac_chunk<kChunk / 64, kRandom>(d, kp, region, region + (uint64_t)nch * kChunk, kChunk,
@@ -586,22 +617,37 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         tot.y += c.y;
         tot.z += c.z;
         const uint32_t rest = pend - kChunk;
-        const uint32_t xo = lane < rest ? st_off[kChunk + lane] : 0u, xs = lane < rest ? st_src[kChunk + lane] : 0u;
-        if (lane < rest) {
-            st_off[lane] = xo;
-            st_src[lane] = xs;
+#pragma unroll
+        for (uint32_t h = 0; h < 128; h += 64) {
+            const uint32_t q = h + lane;
+            const uint32_t xo = q < rest ? st_off[kChunk + q] : 0u, xs = q < rest ? st_src[kChunk + q] : 0u;
+            if (q < rest) {
+                st_off[q] = xo;
+                st_src[q] = xs;
+            }
         }
         ++nch;
         pend = rest;
     };
     for (uint64_t it = it_begin; it < it_end; ++it) {
+        // src[k] of event idx(k) of this iteration: sweep k = 4 g + 2 kh + s,
+        // idx = 256 g + 128 kh + 2 lane + s (v_perm: lo half s, hi byte 2 kh + s);
+        // random k: idx = 64 k + lane
+        auto idx_of = [&](int k) -> uint32_t {
+            return kRandom ? (uint32_t)(k * 64) + lane : (uint32_t)((k >> 2) * 256 + ((k >> 1) & 1) * 128 + (k & 1)) + 2 * lane;
+        };
         uint32_t src[K];
         uint32_t dst[KD];
-        if (it == cp1) t1 = __builtin_amdgcn_s_memrealtime();
-        if (it == cp2) t2 = __builtin_amdgcn_s_memrealtime();
-        if (it == cp3) t3 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
-        for (int k = 0; k < K; ++k) src[k] = nxs[k];
+        for (int k = 0; k < K; ++k) {
+            if constexpr (kRandom) {
+                src[k] = (nxs[k] & 0xFFFFu) | (nxh[k] & 0xFFu) << 16;
+            } else {
+                const int g = k >> 2, kh = (k >> 1) & 1, sh = k & 1;
+                const uint32_t sel = 0x0C000000u | (uint32_t)(4 + 2 * kh + sh) << 16 | (uint32_t)(2 * sh + 1) << 8 | (uint32_t)(2 * sh);
+                src[k] = __builtin_amdgcn_perm(nxh[g], nxs[2 * g + kh], sel);
+            }
+        }
         // The SIMD arbiter issues strictly by priority, then age: with a fixed
         // order the last of a SIMD's four waves streams ~15 % slower than the
         // first.  Rotating every wave through the four ranks every four
@@ -616,7 +662,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             vmask = 0;
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (base + k * 64 + lane < d.events) vmask |= 1u << k;
+                if (base + idx_of(k) < d.events) vmask |= 1u << k;
         }
 
         // Pre-spike filter (brain.metal:73-77 pre-selection): both LDS words of
@@ -641,17 +687,37 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         }
         if (__ballot(fm != 0) == 0) continue;
         const uint32_t rel = (uint32_t)(base - region);
+        if constexpr (kRandom) {  // event order = (k, lane)
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const bool h = (fm >> k) & 1u;
-            const uint64_t b1 = __ballot(h);
-            if (h) {
-                const uint32_t q = pend + mbcnt64(b1);
-                st_off[q] = rel + k * 64 + lane;
-                st_src[q] = src[k];
+            for (int k = 0; k < K; ++k) {
+                const bool h = (fm >> k) & 1u;
+                const uint64_t b1 = __ballot(h);
+                if (h) {
+                    const uint32_t q = pend + mbcnt64(b1);
+                    st_off[q] = rel + idx_of(k);
+                    st_src[q] = src[k];
+                }
+                pend += (uint32_t)__popcll(b1);
+                if (pend >= kChunk) chunk_out();  // a k-step stages at most 64
             }
-            pend += (uint32_t)__popcll(b1);
-            if (pend >= kChunk) chunk_out();  // a k-step stages at most 64
+        } else {  // event order = (lane, s) within each (g, kh) step of 128 events
+#pragma unroll
+            for (int j = 0; j < 2 * NG; ++j) {
+                const bool h0 = (fm >> (2 * j)) & 1u, h1 = (fm >> (2 * j + 1)) & 1u;
+                const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
+                if ((b0 | b1) == 0) continue;  // wave-uniform
+                const uint32_t q = pend + mbcnt64(b0) + mbcnt64(b1);
+                if (h0) {
+                    st_off[q] = rel + idx_of(2 * j);
+                    st_src[q] = src[2 * j];
+                }
+                if (h1) {
+                    st_off[q + h0] = rel + idx_of(2 * j + 1);
+                    st_src[q + h0] = src[2 * j + 1];
+                }
+                pend += (uint32_t)(__popcll(b0) + __popcll(b1));
+                if (pend >= kChunk) chunk_out();  // a step stages at most 128
+            }
         }
     }
     const uint64_t t_stream = __builtin_amdgcn_s_memrealtime();
@@ -663,8 +729,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // the last chunk's refractory stage after the stream costs every wave
         // about the same and would bias short ranges) drives the next pass's
         // partition (partition_bounds): 40-ns units, clamped to [1, 0xFFFF],
-        // 0 for an empty range
-        const uint64_t gt = (t_stream - t_start) >> 2;
+        // 0 for an empty range.  Every full chunk adds chunk_penalty: the
+        // dense stretch's time varies from pass to pass by more than the
+        // stream's (the partition follows one pass late), so its ranges are
+        // made shorter than the average, leaving room for that variation.
+        const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
         const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
         d.range_info[r] = make_uint4(cost, tot.y + c.y, tot.z + c.z, nch);
         d.range_g1[r] = tot.x + c.x;
@@ -672,12 +741,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         d.wave_clock[4 * r] = t_start;
         d.wave_clock[4 * r + 1] = t_stream;
         d.wave_clock[4 * r + 2] = __builtin_amdgcn_s_memrealtime();
-        // the four quarters' stream times, 16 bits each in 40-ns units
-        auto q16 = [](uint64_t a, uint64_t b) -> uint64_t {
-            const uint64_t t = (b - a) >> 2;
-            return t > 0xFFFFu ? 0xFFFFu : t;
-        };
-        d.wave_clock[4 * r + 3] = q16(t_start, t1) | q16(t1, t2) << 16 | q16(t2, t3) << 32 | q16(t3, t_stream) << 48;
+        d.wave_clock[4 * r + 3] = t_entry;
     }
 }
 
@@ -1119,7 +1183,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
         // middle of the next pass's record stream (+30 us of gate time,
         // tools/exp_variants.py).
         if (store && prune && w < kp.w_prune) {  // README §5: the synapse is removed
-            __builtin_nontemporal_store(0xFFFFFFFFu, d.syn.src + ri);
+            set_src(d.syn, ri, kSrcNone);
             __builtin_nontemporal_store(0xFFFFFFFFu, d.syn.dst + ri);
             __builtin_nontemporal_store(w, d.syn.w + ri);
             if (d.dead) atomicAdd(d.dead + ri / kCompactChunk, 1u);  // tally for the structural update
@@ -1229,18 +1293,18 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint
     for (int j = 0; j < 4; ++j) {  // all loads in flight first
         const uint64_t i = base + (uint64_t)j * kCompactThreads + threadIdx.x;
         const bool in = i < n;
-        rs[j] = in ? __builtin_nontemporal_load(syn.src + i) : 0xFFFFFFFFu;
+        rs[j] = in ? src_of(syn, i) : kSrcNone;
         rd[j] = in ? __builtin_nontemporal_load(syn.dst + i) : 0u;
         rw[j] = in ? __builtin_nontemporal_load(syn.w + i) : 0.0f;
     }
     uint64_t o = offsets[blockIdx.x];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const bool live = rs[j] != 0xFFFFFFFFu;
+        const bool live = rs[j] != kSrcNone;
         uint64_t tot;
         const uint64_t pre = block_exclusive_scan(live ? 1u : 0u, &tot, s_wave);
         if (live) {
-            __builtin_nontemporal_store(rs[j], dst.src + o + pre);
+            set_src(dst, o + pre, rs[j]);
             __builtin_nontemporal_store(rd[j], dst.dst + o + pre);
             __builtin_nontemporal_store(rw[j], dst.w + o + pre);
         }
@@ -1273,7 +1337,7 @@ __global__ __launch_bounds__(256) void k_generate(DeviceState d, uint32_t n_in, 
             dst = (uint32_t)(lo + (((x1 >> 32) * range) >> 32));
             w = 0.1f + unit24(x2) * (0.2f - 0.1f);
         }
-        d.syn.src[k] = src;
+        set_src(d.syn, k, src);
         d.syn.dst[k] = dst;
         d.syn.w[k] = w;
     }
@@ -1286,7 +1350,7 @@ __global__ __launch_bounds__(256) void k_checksum(DeviceState d, uint64_t* out)
     uint64_t acc = 0;
     for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < d.n_syn; k += stride) {
         const uint64_t i = d.syn_offset + k;
-        const uint64_t a = ((uint64_t)d.syn.src[k] << 32) | d.syn.dst[k];
+        const uint64_t a = ((uint64_t)src32(src_of(d.syn, k)) << 32) | d.syn.dst[k];
         const uint64_t b = (uint64_t)__float_as_uint(d.syn.w[k]) << 32;  // pad = 0
         acc += mix64(a ^ mix64(b + i * 0x9E3779B97F4A7C15ull));
     }
@@ -1427,6 +1491,38 @@ hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s)
 {
     hipLaunchKernelGGL(k_renorm, dim3(blocks_for(d.n_nrn > 0 ? d.n_nrn : 1)), dim3(256), 0, s, d,
                        base);
+    return hipGetLastError();
+}
+
+// Interchange src values (u32, 0xFFFFFFFF = tombstone) <-> the packed
+// streams, records [first, first + n).
+__global__ __launch_bounds__(256) void k_pack_src(SynArrays a, const uint32_t* in, uint64_t first, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t v = in[i];
+        set_src(a, first + i, v >= kSrcNone ? kSrcNone : v);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_unpack_src(SynArrays a, uint32_t* out, uint64_t first, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        out[i] = src32(src_of(a, first + i));
+}
+
+hipError_t launch_pack_src(const SynArrays& a, const uint32_t* in_dev, uint64_t first, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack_src, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, a,
+                       in_dev, first, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t first, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unpack_src, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, a,
+                       out_dev, first, n);
     return hipGetLastError();
 }
 

@@ -61,13 +61,14 @@ PLASTICITY = dict(w_prune=0.105, p_new=0.25, w_init=0.5, compact_every=50)
 
 def algorithmic_bytes(stats: dict, track_visits: bool) -> int:
     """Bytes the streaming gate kernel must move from HBM: the
-    4-B src word of every visited event -- the records are held as arrays and
-    the pre-spike gate reads nothing else (+4 B dst read and 8 B lastVisited
-    write per event with track_visits).  The pre-spike lookup of lastFired[src]
-    is served by the per-pass LDS filter / L2 bitmap built by k_bitmap, which
-    reads lastFired once per pass (8 B per neuron, k_bitmap's own bytes)."""
+    3-B (24-bit) src of every visited event -- the records are held as arrays
+    and the pre-spike gate reads nothing else (+4 B dst read and 8 B
+    lastVisited write per event with track_visits).  The pre-spike lookup of
+    lastFired[src] is served by the per-pass LDS filter / L2 bitmap, built by
+    k_apply from the last passes' spike lists (k_bitmap, after host writes,
+    reads lastFired once: 8 B per neuron)."""
     e = stats["events"]
-    return 4 * e + (12 * e if track_visits else 0)
+    return 3 * e + (12 * e if track_visits else 0)
 
 
 def survey_bytes(stats: dict, track_visits: bool) -> int:
@@ -215,8 +216,9 @@ def main():
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
             "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": launches,
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "bytes_formula": ("4*E (src-array stream; E visited events) -- DESIGN.md §5" if mode == 0 else
-                              "4*E (one random src word per pick; HBM moves >= 64 B per "
+            "bytes_formula": ("3*E (24-bit src stream: 2-B lo + 1-B hi per event; E visited events) -- "
+                              "DESIGN.md §5" if mode == 0 else
+                              "3*E (one random 24-bit src per pick; HBM moves >= 64 B per "
                               "random access) -- DESIGN.md §5"),
             "survey_formula_bytes_per_launch": int(survey_per_launch),
             "survey_formula_achieved": round(survey_per_launch / (avg_gate_ms * 1e-3) / 1e9, 1),

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ABNN_ABI_VERSION 4
+#define ABNN_ABI_VERSION 5
 
 typedef enum abnn_status {
     ABNN_OK = 0,
@@ -53,10 +53,13 @@ typedef enum abnn_status {
 
 /* SynapsePacked -- brain.metal:11, brain.h:21, README §2.2.  16 bytes, AoS.
  * This is the INTERCHANGE format (upload/download, .bnn, the C++ wrapper).
- * On the device the records are held as three arrays (abnn_state, DESIGN.md
- * §4): the sweep's gate needs only `src`, so it streams 4 B per event instead
- * of 16.  `pad` is not stored; downloads return 0 (the reference never writes
- * or reads it: brain.metal:11, brain-engine.cpp:31-53). */
+ * On the device the records are held as arrays (abnn_state):
+ * the sweep's gate needs only `src`, held in 24 bits, so it streams 3 B per
+ * event instead of 16.  `pad` is not stored; downloads return 0 (the
+ * reference never writes or reads it: brain.metal:11, brain-engine.cpp:31-53).
+ * N_NRN = n_input + n_output + n_hidden must be below 2^24 - 1 (16,777,215;
+ * the reference's configurations reach 5,000,512): abnn_brain_create returns
+ * ABNN_ERR_INVALID above. */
 typedef struct abnn_synapse {
     uint32_t src;
     uint32_t dst;
@@ -179,9 +182,16 @@ typedef struct abnn_stats {
 } abnn_stats;
 
 /* Borrowed device pointers (brain.h:54-58 buffer getters).  bufSyn_ is held
- * as a structure of arrays: record i is {syn_src[i], syn_dst[i], syn_w[i], 0}. */
+ * as a structure of arrays: record i is {src(i), syn_dst[i], syn_w[i], 0}
+ * with the 24-bit src split in two streams (N_NRN < 2^24 - 1):
+ *   src(i) = syn_src_lo[i] | syn_src_hi[hp(i)] << 16,
+ *   hp(i)  = 256 (i / 256) + 4 ((i % 128) / 2) + 2 ((i % 256) / 128) + i % 2,
+ * 0xFFFFFF for a removed synapse (downloads report 0xFFFFFFFF).  Taking the
+ * pointers makes every later pass rebuild the recent-spike bitmap from
+ * lastFired (the caller may write it behind the handle's back). */
 typedef struct abnn_state {
-    uint32_t* syn_src;       /* n_syn (bufSyn_ .src)                     */
+    uint16_t* syn_src_lo;    /* n_syn: src bits 0..15                    */
+    uint8_t* syn_src_hi;     /* n_syn rounded up to 256: src bits 16..23 */
     uint32_t* syn_dst;       /* n_syn (bufSyn_ .dst)                     */
     float* syn_w;            /* n_syn (bufSyn_ .w)                       */
     uint64_t* last_fired;    /* N_NRN (bufLastFire_)                     */

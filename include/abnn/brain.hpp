@@ -129,17 +129,18 @@ public:
 
     // Borrowed device pointers (brain.h:54-58).  The reference's budget buffer
     // has no equivalent: the budget is the max_spikes parameter.
-    // bufSyn_ as three device arrays (abnn.h abnn_state); SynapsePacked is
-    // the upload/download/.bnn format.
+    // bufSyn_ as device arrays (abnn.h abnn_state: src in two streams);
+    // SynapsePacked is the upload/download/.bnn format.
     struct SynapseArrays {
-        uint32_t* src;
+        uint16_t* src_lo;
+        uint8_t* src_hi;
         uint32_t* dst;
         float* w;
     };
     SynapseArrays synapse_buffer() const
     {
         const abnn_state s = state();
-        return {s.syn_src, s.syn_dst, s.syn_w};
+        return {s.syn_src_lo, s.syn_src_hi, s.syn_dst, s.syn_w};
     }
     uint64_t* last_fired_buffer() const { return state().last_fired; }
     uint64_t* clock_buffer() const { return state().clock; }

@@ -26,14 +26,16 @@ def find(d, pat):
 def steady(trace_csv, n_last=30):
     rows = list(csv.DictReader(open(trace_csv)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_bitmap")]
+    # a pass runs from one k_gate to the next (k_bitmap, when launched,
+    # precedes the gate and is counted with the previous pass)
+    idx = [i for i, r in enumerate(rows) if "k_gate" in r["Kernel_Name"].split("(")[0]]
     per = {}
     starts = idx[-n_last:]
     for a in starts:
         j = a
-        while j < len(rows) and (j == a or not rows[j]["Kernel_Name"].startswith("k_bitmap")):
+        while j < len(rows) and (j == a or "k_gate" not in rows[j]["Kernel_Name"].split("(")[0]):
             r = rows[j]
-            per.setdefault(r["Kernel_Name"], []).append(
+            per.setdefault(r["Kernel_Name"].split("(")[0].split("<")[0].split(" ")[-1], []).append(
                 (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
             j += 1
     spans = [(int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
@@ -47,7 +49,7 @@ def pmc_values(d, counter):
         return []
     vals = []
     for r in csv.DictReader(open(f)):
-        if r.get("Kernel_Name", "").startswith("k_gate") and r.get("Counter_Name") == counter:
+        if "k_gate" in r.get("Kernel_Name", "").split("(")[0] and r.get("Counter_Name") == counter:
             vals.append(float(r["Counter_Value"]))
     return vals
 

@@ -36,6 +36,9 @@ for p in range(passes):
     w = buf[:4 * nr].reshape(-1, 4)
     w = w[w[:, 0] > 0]
     t0 = w[:, 0].min()
+    print(f"  entry (before the filter load) to start: " + " ".join(
+        f"{v:5.2f}" for v in np.percentile((w[:, 0] - w[:, 3]) * 10e-3, [0, 50, 100])) +
+        f" us; first entry {(w[:, 3].min() - t0) * 10e-3:.2f} us; last end - first entry {(w[:, 2].max() - w[:, 3].min()) * 10e-3:.2f} us")
     st, se, en = (w[:, 0] - t0) * 10e-3, (w[:, 1] - t0) * 10e-3, (w[:, 2] - t0) * 10e-3  # us
     q = lambda x: " ".join(f"{v:7.1f}" for v in np.percentile(x, [0, 10, 50, 90, 99, 100]))
     print(f"pass {p}: waves {len(w)}   percentiles 0/10/50/90/99/100 (us)")
