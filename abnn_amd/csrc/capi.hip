@@ -109,8 +109,8 @@ void free_all(abnn_brain* b)
 {
     if (!b) return;
     (void)hipSetDevice(b->device);
-    void* ptrs[] = {b->d.syn.lo,    b->d.syn.hi,     b->d.syn.dst,    b->d.syn.w,
-                    b->syn_alt.lo,  b->syn_alt.hi,   b->syn_alt.dst,  b->syn_alt.w,
+    void* ptrs[] = {b->d.syn.lo,    b->d.syn.hi,     b->d.syn.dst,    b->d.syn.w,   b->d.syn.src32,
+                    b->syn_alt.lo,  b->syn_alt.hi,   b->syn_alt.dst,  b->syn_alt.w, b->syn_alt.src32,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->bitmap_buf[0], b->bitmap_buf[1], b->filter_buf[0], b->filter_buf[1], b->d.range_info,    b->d.range_g1,  b->d.g2x,
                     b->d.chunk_cnt,
@@ -165,11 +165,12 @@ abnn_status ensure_idx_scratch(abnn_brain* b, uint64_t n)
 
 // Device records are the packed src streams, dst and w (SynArrays, engine.h);
 // abnn_synapse is the host interchange format.  Capacity `count` records.
-abnn_status alloc_syn(SynArrays* a, uint64_t count)
+abnn_status alloc_syn(SynArrays* a, uint64_t count, bool random_mode)
 {
     ST_TRY(dalloc(&a->lo, count));
     ST_TRY(dalloc(&a->hi, hi_bytes(count)));
     ST_TRY(dalloc(&a->dst, count));
+    if (random_mode) ST_TRY(dalloc(&a->src32, count));
     return dalloc(&a->w, count);
 }
 
@@ -604,7 +605,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     abnn_status s;
     // build_buffers, brain.cpp:52-69: allocate and zero every buffer.
     // padded: the gate's last iteration reads up to one iteration past the sweep
-    if ((s = alloc_syn(&d.syn, cap + kDummyRecords)) != ABNN_OK) return fail(s);
+    if ((s = alloc_syn(&d.syn, cap + kDummyRecords, p.mode == ABNN_MODE_RANDOM)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_fired, n_nrn)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_visited, n_nrn)) != ABNN_OK) return fail(s);
     uint64_t* sb = nullptr;
@@ -633,7 +634,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, cap)) != ABNN_OK) return fail(s);
     if (p.compact_every > 0) {  // structural updates: the compaction's second buffer + scratch
         const uint64_t nb = (cap + kCompactChunk - 1) / kCompactChunk;
-        if ((s = alloc_syn(&b->syn_alt, cap + kDummyRecords)) != ABNN_OK) return fail(s);
+        if ((s = alloc_syn(&b->syn_alt, cap + kDummyRecords, p.mode == ABNN_MODE_RANDOM)) != ABNN_OK) return fail(s);
         if ((s = dalloc(&b->compact_offsets, nb)) != ABNN_OK) return fail(s);
         if (p.w_prune > 0.0f && (s = dalloc(&d.dead, nb)) != ABNN_OK) return fail(s);
     }

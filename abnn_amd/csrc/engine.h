@@ -54,6 +54,8 @@ struct SynArrays {
     uint8_t* hi;
     uint32_t* dst;
     float* w;
+    uint32_t* src32;  // random mode only: the same src as one u32 per record, so a pick is
+                      // one random DRAM access, not two (kept in step by set_src)
 };
 
 __host__ __device__ inline uint64_t hi_pos(uint64_t i)

@@ -159,6 +159,7 @@ __device__ __forceinline__ void set_src(const SynArrays& a, uint64_t i, uint32_t
 {
     a.lo[i] = (uint16_t)v;
     a.hi[hi_pos(i)] = (uint8_t)(v >> 16);
+    if (a.src32) a.src32[i] = v;
 }
 
 // Record visited by local event t: itself (sweep, brain.metal:70) or its pick.
@@ -518,7 +519,6 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     constexpr uint32_t IE = 64 * K;
     constexpr int KD = kTrack ? K : 1;                 // dst words in flight (track_visits)
     constexpr int NG = K / 4;                          // sweep: 256-event groups per iteration
-    constexpr int KH = kRandom ? K : 1;                // random: hi bytes in flight
     constexpr uint32_t LG = __builtin_ctz(FW);
     constexpr uint32_t SE = kChunk + 128;              // a chunk + one staging step (<= 128 events)
     static_assert(K % 4 == 0, "the packed src stream is read in 256-event groups");
@@ -543,8 +543,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // per 256-event group g a lane holds two lo words (events 128 kh + 2 lane
     // + {0, 1}, kh = 0, 1) and one hi word (the same four events' bits
     // 16..23), 3 B per event.  Random mode: per event k (t = 64 k + lane) the
-    // lo half-word and the hi byte of its picked record.
-    uint32_t nxs[kRandom ? K : 2 * NG], nxh[kRandom ? KH : NG], nxd[KD];
+    // u32 src of its picked record (the src32 mirror).
+    uint32_t nxs[kRandom ? K : 2 * NG], nxh[NG], nxd[KD];
     const uint64_t pass = kRandom ? *d.pass_index : 0;
     auto issue = [&](uint64_t it, bool live) {
         if constexpr (kRandom) {  // random-edge mode: a per-lane random record per event
@@ -553,8 +553,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 const uint64_t t = it * IE + k * 64 + lane;
                 const bool real = live && t < d.events;
                 const uint64_t e = real ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : 0;
-                nxs[k] = __builtin_nontemporal_load(d.syn.lo + e);
-                nxh[k] = __builtin_nontemporal_load(d.syn.hi + hi_pos(e));
+                nxs[k] = __builtin_nontemporal_load(d.syn.src32 + e);  // one access per pick
                 if constexpr (kTrack)
                     nxd[k] = __builtin_nontemporal_load(real ? d.syn.dst + e : d.dummy + (k * 64 + lane));
             }
@@ -641,7 +640,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if constexpr (kRandom) {
-                src[k] = (nxs[k] & 0xFFFFu) | (nxh[k] & 0xFFu) << 16;
+                src[k] = nxs[k];
             } else {
                 const int g = k >> 2, kh = (k >> 1) & 1, sh = k & 1;
                 const uint32_t sel = 0x0C000000u | (uint32_t)(4 + 2 * kh + sh) << 16 | (uint32_t)(2 * sh + 1) << 8 | (uint32_t)(2 * sh);

@@ -59,16 +59,17 @@ def parse():
 PLASTICITY = dict(w_prune=0.105, p_new=0.25, w_init=0.5, compact_every=50)
 
 
-def algorithmic_bytes(stats: dict, track_visits: bool) -> int:
+def algorithmic_bytes(stats: dict, track_visits: bool, random_mode: bool = False) -> int:
     """Bytes the streaming gate kernel must move from HBM: the
     3-B (24-bit) src of every visited event -- the records are held as arrays
     and the pre-spike gate reads nothing else (+4 B dst read and 8 B
     lastVisited write per event with track_visits).  The pre-spike lookup of
     lastFired[src] is served by the per-pass LDS filter / L2 bitmap, built by
     k_apply from the last passes' spike lists (k_bitmap, after host writes,
-    reads lastFired once: 8 B per neuron)."""
+    reads lastFired once: 8 B per neuron).  Random mode: one u32 src per pick
+    (the src32 mirror)."""
     e = stats["events"]
-    return 3 * e + (12 * e if track_visits else 0)
+    return (4 if random_mode else 3) * e + (12 * e if track_visits else 0)
 
 
 def survey_bytes(stats: dict, track_visits: bool) -> int:
@@ -205,7 +206,7 @@ def main():
         # one gate launch per pass; HIP events time a sample of them (every
         # TIMING_EVERY-th), so bytes per launch come from the pass count
         passes = max(1, stats["passes"])
-        bytes_per_launch = algorithmic_bytes(stats, track) / passes
+        bytes_per_launch = algorithmic_bytes(stats, track, mode == 1) / passes
         achieved = bytes_per_launch / (avg_gate_ms * 1e-3) / 1e9
         survey_per_launch = survey_bytes(stats, track) / passes
         default_run = mode == 0 and events == wl.events
@@ -218,8 +219,8 @@ def main():
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "bytes_formula": ("3*E (24-bit src stream: 2-B lo + 1-B hi per event; E visited events) -- "
                               "DESIGN.md §5" if mode == 0 else
-                              "3*E (one random 24-bit src per pick; HBM moves >= 64 B per "
-                              "random access) -- DESIGN.md §5"),
+                              "4*E (one random u32 src per pick, the src32 mirror; HBM moves >= 64 B "
+                              "per random access) -- DESIGN.md §5"),
             "survey_formula_bytes_per_launch": int(survey_per_launch),
             "survey_formula_achieved": round(survey_per_launch / (avg_gate_ms * 1e-3) / 1e9, 1),
             "survey_formula": "24*E + 8*G1 (SURVEY §8d; G1 pre-gated) -- counts an 8-B lastFired[src] "

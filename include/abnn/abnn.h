@@ -186,7 +186,9 @@ typedef struct abnn_stats {
  * with the 24-bit src split in two streams (N_NRN < 2^24 - 1):
  *   src(i) = syn_src_lo[i] | syn_src_hi[hp(i)] << 16,
  *   hp(i)  = 256 (i / 256) + 4 ((i % 128) / 2) + 2 ((i % 256) / 128) + i % 2,
- * 0xFFFFFF for a removed synapse (downloads report 0xFFFFFFFF).  Taking the
+ * 0xFFFFFF for a removed synapse (downloads report 0xFFFFFFFF).  Random mode
+ * keeps an internal u32 copy of src for its picks: write records through
+ * abnn_upload_synapses there, not through these pointers.  Taking the
  * pointers makes every later pass rebuild the recent-spike bitmap from
  * lastFired (the caller may write it behind the handle's back). */
 typedef struct abnn_state {
