@@ -207,6 +207,16 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t x)
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(x), 63);
 }
 
+// Workgroup barrier for LDS communication only: unlike __syncthreads() it does
+// not wait for the wave's outstanding global stores and atomics (a
+// workgroup-scope release fence on global memory waits for vmcnt(0)).
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Sum of one u64 per thread over an NT-thread workgroup (every thread gets it).
 template <int NT>
 __device__ uint64_t block_sum(uint64_t v, uint64_t* s_wave)
@@ -1038,13 +1048,12 @@ __device__ void stamp_gathered(const DeviceState& d, const KernelParams& kp, con
     }
 }
 
-// The end of a pass, by the last k_apply workgroup (every other one has read
-// the pass-start scalars): rBar (brain.metal:110-113), clock tick
+// The end of a pass, by one thread of the last k_apply workgroup (every other
+// one has read the pass-start scalars): rBar (brain.metal:110-113), clock tick
 // (brain.metal:129).
 __device__ void finalize_pass(const DeviceState& d, const KernelParams& kp, const int32_t* gathered, uint32_t world,
                               uint64_t now, float R, float rbar, uint64_t pass)
 {
-    if (threadIdx.x != 0) return;
     uint64_t events = d.events;
     int64_t t0 = d.work->t0_g2;
     if (gathered) {
@@ -1142,7 +1151,6 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     __shared__ uint32_t s_u[kWalkWaves], s_f[kWalkWaves], s_p[kWalkWaves];
     __shared__ uint64_t s_now, s_pass;
     __shared__ float s_R, s_rb;
-    __shared__ uint32_t s_last;
     // per-workgroup timeline (diagnostics, abnn_debug_apply_clock): entry,
     // scalars, walk prefix, walk done, partition, ticket, pass end
     uint64_t* tc = d.apply_clock + 8 * blockIdx.x;
@@ -1167,7 +1175,12 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     const bool first = blockIdx.x == 0;  // workgroup 0 also counts the pass's gate totals
     // the next pass's bitmap build (steady state): this thread's first item, loads in flight
     const uint64_t nitems = d.build_next ? next_items(d, kp) : 0;
-    const uint64_t x0 = (uint64_t)threadIdx.x * gridDim.x + blockIdx.x, xs = (uint64_t)gridDim.x * kApplyThreads;
+    // counted from the workgroup's last thread down: the items land in the last
+    // wave, away from wave 0 (the walk's heavy items) and the ticket wave --
+    // gfx9's vmcnt covers stores and atomics, so a later load in the same wave
+    // would wait for these atomics
+    const uint32_t tr = kApplyThreads - 1 - threadIdx.x;
+    const uint64_t x0 = (uint64_t)tr * gridDim.x + blockIdx.x, xs = (uint64_t)gridDim.x * kApplyThreads;
     const NextItem it0 = x0 < nitems ? next_item_load(d, kp, pass, x0) : NextItem{0u, 0u, 0u};
     budget_walk(d, rank_offset(kp, gathered, rank), kp.max_spikes, s_lds, s_red,
                 [&](uint64_t region, const uint4& e, bool f, uint64_t pre, uint64_t slot) {
@@ -1211,7 +1224,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
         if (d.build_next && stamp) wave_set_next(d, fired, e.w);
     }, first ? &s_g1 : nullptr, first ? &s_g2 : nullptr, tc + 2, true, &s_cand);
     wave_set_next(d, it0.i < it0.lim, it0.n);
-    const uint64_t xw = x0 - (uint64_t)(threadIdx.x & 63) * gridDim.x;  // the wave's lowest item (lane 0)
+    const uint64_t xw = x0 - (uint64_t)(63 - (threadIdx.x & 63)) * gridDim.x;  // the wave's lowest item (lane 63)
     for (uint64_t k = xs; xw + k < nitems; k += xs) {  // wave-uniform
         const NextItem it = x0 + k < nitems ? next_item_load(d, kp, pass, x0 + k) : NextItem{0u, 0u, 0u};
         wave_set_next(d, it.i < it.lim, it.n);
@@ -1232,8 +1245,15 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
         s_f[threadIdx.x >> 6] = wf;
         s_p[threadIdx.x >> 6] = wp;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
+    lds_barrier();  // the weight stores and bitmap atomics stay in flight
+    // one lane of the second-to-last wave (no build items, rarely a walk
+    // store) takes the ticket, adds the statistics (no-return atomics into this
+    // workgroup's own slot: no load waits behind the pass's stores) and, in the
+    // last workgroup to arrive, ends the pass
+    constexpr uint32_t kLeader = kApplyThreads - 128;
+    if (threadIdx.x == kLeader) {
+        const uint32_t ticket = __hip_atomic_fetch_add((gu32*)(&d.work->ticket), 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
         uint32_t tu = 0, tf = 0, tp = 0;
         for (uint32_t v = 0; v < kWalkWaves; ++v) {
             tu += s_u[v];
@@ -1241,28 +1261,21 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
             tp += s_p[v];
         }
         abnn_stats* st = d.wg_stats + blockIdx.x;
-        abnn_stats x = *st;
-        x.updated += tu;
-        x.fired += tf;
-        x.pruned += tp;
+        typedef unsigned long long ull;
+        if (tu) atomicAdd((ull*)&st->updated, (ull)tu);
+        if (tf) atomicAdd((ull*)&st->fired, (ull)tf);
+        if (tp) atomicAdd((ull*)&st->pruned, (ull)tp);
         if (first) {
-            x.passes += 1;
-            x.events += d.events;
-            x.pre_gated += s_g1;
-            x.post_gated += s_g2;
+            atomicAdd((ull*)&st->passes, 1ull);
+            atomicAdd((ull*)&st->events, (ull)d.events);
+            atomicAdd((ull*)&st->pre_gated, (ull)s_g1);
+            atomicAdd((ull*)&st->post_gated, (ull)s_g2);
         }
-        *st = x;
-        // the last workgroup to arrive ends the pass; every workgroup's
-        // pass-start scalar loads are complete (used above through LDS)
-        const uint32_t ticket = __hip_atomic_fetch_add((gu32*)(&d.work->ticket), 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        s_last = ticket == gridDim.x - 1;
         tc[5] = __builtin_amdgcn_s_memrealtime();
-    }
-    __syncthreads();
-    if (s_last) {
-        finalize_pass(d, kp, gathered, world, now, R, rb, pass);
-        if (threadIdx.x == 0) tc[6] = __builtin_amdgcn_s_memrealtime();
+        if (ticket == gridDim.x - 1) {
+            finalize_pass(d, kp, gathered, world, now, R, rb, pass);
+            tc[6] = __builtin_amdgcn_s_memrealtime();
+        }
     }
 }
 
