@@ -596,6 +596,10 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.adapt_gain = 2;
     if (const char* env = std::getenv("ABNN_ADAPT_GAIN")) d.adapt_gain = (uint32_t)std::min(4, std::max(1, std::atoi(env)));
     d.chunk_penalty = 25;  // 1 us per full chunk (~15 % of its refractory stage)
+    d.tail_prio = 4;
+    d.prio_clock = 0;
+    if (const char* env = std::getenv("ABNN_PRIO_CLOCK")) d.prio_clock = std::atoi(env) ? 1u : 0u;
+    if (const char* env = std::getenv("ABNN_TAIL_PRIO")) d.tail_prio = (uint32_t)std::min(4, std::max(0, std::atoi(env)));
     if (const char* env = std::getenv("ABNN_CHUNK_PENALTY")) d.chunk_penalty = (uint32_t)std::max(0, std::atoi(env));
     configure(b);  // sweep partition for the creation size
     const uint64_t max_ranges = (uint64_t)std::min<int>(kMaxGateBlocks, cus * per_cu) * (gate_block / 64);

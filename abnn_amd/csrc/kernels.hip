@@ -661,7 +661,13 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // order the last of a SIMD's four waves streams ~15 % slower than the
         // first.  Rotating every wave through the four ranks every four
         // iterations equalises them (tools/ubench_soa.hip, profiles/r01p_*).
-        if (((it - it_begin) & 3u) == 0) set_priority((uint32_t)((it - it_begin) >> 2) + wid / 4u);
+        // prio_clock: the rank follows the wall clock (~10 us per step) instead
+        // of the wave's own iteration count, so the four waves of a SIMD never
+        // share a rank (iteration counts drift apart, and on a tie the arbiter
+        // favours the oldest wave)
+        if (((it - it_begin) & 3u) == 0)
+            set_priority((d.prio_clock ? (uint32_t)(__builtin_amdgcn_s_memrealtime() >> 10)
+                                       : (uint32_t)((it - it_begin) >> 2)) + wid / 4u);
 #pragma unroll
         for (int k = 0; k < KD; ++k) dst[k] = kTrack ? nxd[k] : 0u;
         issue(it + 1, it + 1 < it_end);  // next iteration's records in flight first
@@ -730,6 +736,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         }
     }
     const uint64_t t_stream = __builtin_amdgcn_s_memrealtime();
+    // the tail (latency-bound) runs at the issue priority tail_prio, not at
+    // whatever rank the rotation left the wave in (4: keep)
+    if (d.tail_prio < 4) set_priority(d.tail_prio);
     // the range's last chunk: refractory stage by this wave
     const uint64_t tb = region + (uint64_t)nch * kChunk;
     const uint4 c = refrac_chunk<kChunk / 64, kRandom>(d, kp, region, tb, pend, now, pass, stage_at);
