@@ -389,7 +389,7 @@ abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
     d.filter_next = b->filter_buf[(p + 1) & 1];
     d.stim_first = b->stim_first;
     d.stim_count = b->stim_count;
-    const bool prebuilt = !xchg_out && b->next_built && b->built_stim[0] == b->stim_first &&
+    const bool prebuilt = b->next_built && b->built_stim[0] == b->stim_first &&
                           b->built_stim[1] == b->stim_count;
     b->next_built = false;
     if (!prebuilt) HIP_TRY(launch_bitmap(d, b->kp, b->stim_first, b->stim_count, s));
@@ -409,7 +409,7 @@ abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
 abnn_status run_apply(abnn_brain* b, const int32_t* gathered, uint32_t world, uint32_t rank, hipStream_t s)
 {
     DeviceState& d = b->d;
-    d.build_next = !gathered && build_next_ok(b) ? 1u : 0u;
+    d.build_next = build_next_ok(b) ? 1u : 0u;
     d.n_next_stim = 0;
     if (d.build_next) {  // distinct stimulus ranges of passes p+1-W .. p+1 (p+1: the current one)
         const uint64_t W = b->params.window_pre, p = b->pass_host;
@@ -435,8 +435,8 @@ abnn_status run_commit(abnn_brain* b, const int32_t* gathered, uint32_t world, b
                        hipStream_t s)
 {
     host_tick(b);
-    // sharded passes stamp from the gathered lists, not fired_ring
-    b->clean_passes = gathered ? 0 : b->clean_passes + 1;
+    // sharded passes write the merged spike list into fired_ring too
+    b->clean_passes += 1;
     if (renorm) {  // renormalise_if_needed, brain.cpp:125-141; kernel brain.metal:135-145
         HIP_TRY(launch_renorm(b->d, b->clock_host, s));
         const uint64_t base = b->clock_host;

@@ -1039,22 +1039,35 @@ typedef __attribute__((address_space(1))) uint64_t gu64;
 
 // Sharded passes: stamp rank r's first min(count_r, budget - offset_r) spikes
 // (the gathered exchange records, rank order); workgroups take slices.
-__device__ void stamp_gathered(const DeviceState& d, const KernelParams& kp, const int32_t* gathered, uint32_t world,
-                               uint64_t now)
+// The merged list is also this pass's spike list (fired_ring, global budget
+// order) and, in steady state, goes into the next pass's bitmap like a
+// single-GPU pass's spikes.  Returns the list's length (every thread).
+__device__ uint64_t stamp_gathered(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
+                                   uint32_t world, uint64_t now, uint64_t pass)
 {
     const uint32_t words = xchg_words(kp.max_spikes);
     const uint64_t budget = kp.max_spikes;
+    uint32_t* ring = d.fired_ring + (pass & (kFiredRing - 1)) * (uint64_t)kp.max_spikes;
+    const uint32_t lane = threadIdx.x & 63;
     uint64_t off = 0;
     for (uint32_t r = 0; r < world && off < budget; ++r) {
         const int64_t cnt = *reinterpret_cast<const int64_t*>(gathered + r * words);
         const int32_t* sp = gathered + r * words + 2 * ABNN_SUMMARY_WORDS;
         const uint64_t room = budget - off, n = (uint64_t)cnt < room ? (uint64_t)cnt : room;
-        for (uint64_t i = (uint64_t)blockIdx.x * kApplyThreads + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kApplyThreads) {
-            const uint32_t nrn = (uint32_t)sp[i];
-            if (nrn < d.n_nrn) d.last_fired[nrn] = now;
+        // wave-uniform trip count (wave_set_next is wave-converged)
+        for (uint64_t i0 = (uint64_t)blockIdx.x * kApplyThreads + (threadIdx.x - lane); i0 < n;
+             i0 += (uint64_t)gridDim.x * kApplyThreads) {
+            const uint64_t i = i0 + lane;
+            const uint32_t nrn = i < n ? (uint32_t)sp[i] : 0xFFFFFFFFu;
+            if (nrn < d.n_nrn) {
+                d.last_fired[nrn] = now;
+                ring[off + i] = nrn;
+            }
+            if (d.build_next) wave_set_next(d, nrn < d.n_nrn, nrn);
         }
         off += n;
     }
+    return off;
 }
 
 // The end of a pass, by one thread of the last k_apply workgroup (every other
@@ -1244,7 +1257,10 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     // sharded passes: every rank's spikes from the gathered exchange records,
     // budget order across ranks = global event order (brain.metal:125-126);
     // nothing of this kernel reads lastFired
-    if (gathered) stamp_gathered(d, kp, gathered, world, now);
+    if (gathered) {
+        const uint64_t nsp = stamp_gathered(d, kp, gathered, world, now, pass);
+        if (first && threadIdx.x == 0) d.n_fired_ring[pass & (kFiredRing - 1)] = (uint32_t)nsp;
+    }
     if (threadIdx.x == 0) tc[3] = __builtin_amdgcn_s_memrealtime();
     // statistics: every workgroup adds into its own slot (no cross-workgroup
     // sum; abnn_get_stats adds the slots)
