@@ -597,6 +597,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (const char* env = std::getenv("ABNN_ADAPT_GAIN")) d.adapt_gain = (uint32_t)std::min(4, std::max(1, std::atoi(env)));
     d.chunk_penalty = 25;  // 1 us per full chunk (~15 % of its refractory stage)
     d.tail_prio = 4;
+    d.apply_blocks = kWalkBlocks;
+    if (const char* env = std::getenv("ABNN_APPLY_BLOCKS"))
+        d.apply_blocks = (uint32_t)std::min<int>(kWalkBlocks, std::max(1, std::atoi(env)));
     d.prio_clock = 0;
     if (const char* env = std::getenv("ABNN_PRIO_CLOCK")) d.prio_clock = std::atoi(env) ? 1u : 0u;
     if (const char* env = std::getenv("ABNN_TAIL_PRIO")) d.tail_prio = (uint32_t)std::min(4, std::max(0, std::atoi(env)));

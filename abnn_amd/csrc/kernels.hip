@@ -1514,7 +1514,7 @@ hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xc
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
                         uint32_t world, uint32_t rank, hipStream_t s)
 {
-    const dim3 g(kWalkBlocks), b(kApplyThreads);
+    const dim3 g(d.apply_blocks ? d.apply_blocks : kWalkBlocks), b(kApplyThreads);
     if (d.mode == ABNN_MODE_RANDOM) {
         hipLaunchKernelGGL(k_claim, g, b, walk_lds(d), s, d, kp, gathered, rank);
         hipError_t e = hipGetLastError();
