@@ -38,7 +38,8 @@ TIMING_EVERY = 8       # gate launches sampled by HIP events (the roofline's ave
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200,
+                    help="timed passes (the reference engine runs passes forever; 200 x ~0.13 ms)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
