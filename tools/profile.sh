@@ -12,7 +12,7 @@ mkdir -p "$out" profiles
 export TMPDIR=/tmp
 run() { timeout -k 10 420 "$@"; rc=$?; if [ $rc -ne 0 ]; then echo "FATAL rc=$rc: $*"; exit 100; fi; }
 run rocprofv3 --kernel-trace --stats -T --output-format csv -d "$out/trace" -o run -- \
-    python3 bench.py --config "$cfg" --steps 30 --warmup 10 --no-cpu-baseline > "$out/bench_trace.json"
+    python3 bench.py --config "$cfg" --steps 200 --warmup 10 --no-cpu-baseline > "$out/bench_trace.json"
 if [ "${PMC:-1}" = 1 ]; then
 run rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$out/fetch" -o run -- \
     python3 bench.py --config "$cfg" --steps 10 --warmup 10 --no-cpu-baseline > "$out/bench_fetch.json"
