@@ -139,6 +139,7 @@ SIGNATURES = [
     ("abnn_traverse", C.c_int, [_VP, _U32, _VP]),
     ("abnn_synchronize", C.c_int, [_VP, _VP]),
     ("abnn_exchange_bytes", C.c_uint64, [_VP]),
+    ("abnn_set_global_events", C.c_int, [_VP, _U64]),
     ("abnn_shard_gate", C.c_int, [_VP, _VP, _VP]),
     ("abnn_shard_apply", C.c_int, [_VP, _VP, _U32, _U32, _VP]),
     ("abnn_shard_commit", C.c_int, [_VP, _VP, _U32, _VP]),
@@ -146,6 +147,7 @@ SIGNATURES = [
     ("abnn_reset_stats", C.c_int, [_VP]),
     ("abnn_enable_timing", C.c_int, [_VP, C.c_int]),
     ("abnn_get_kernel_time", C.c_int, [_VP, C.POINTER(C.c_double), _PU64]),
+    ("abnn_get_kernel_times", C.c_int, [_VP, _VP, _U64, _PU64]),
     ("abnn_save_bnn", C.c_int, [_VP, C.c_char_p]),
     ("abnn_load_bnn", C.c_int, [_VP, C.c_char_p]),
     ("abnn_save_flat", C.c_int, [_VP, C.c_char_p]),

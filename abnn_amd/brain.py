@@ -204,6 +204,10 @@ class Brain:
         """Bytes of this shard's exchange record (summary + local spike list, abnn.h)."""
         return int(self._lib.abnn_exchange_bytes(self._h))
 
+    def set_global_events(self, n: int) -> None:
+        """Visited events of all shards per pass (after structural updates)."""
+        call("abnn_set_global_events", self._h, int(n))
+
     def shard_gate(self, xchg_ptr: int, stream=None) -> None:
         call("abnn_shard_gate", self._h, xchg_ptr, _stream_ptr(stream))
 
@@ -231,6 +235,13 @@ class Brain:
         n = C.c_uint64()
         call("abnn_get_kernel_time", self._h, C.byref(ms), C.byref(n))
         return float(ms.value), int(n.value)
+
+    def kernel_times(self, cap: int = 1 << 16) -> np.ndarray:
+        """The timed gate launches since the last call, one by one (ms)."""
+        out = np.zeros(cap, dtype=np.float32)
+        n = C.c_uint64()
+        call("abnn_get_kernel_times", self._h, _ptr(out), cap, C.byref(n))
+        return out[:min(int(n.value), cap)].astype(np.float64)
 
     # ---- persistence (brain.cpp:161-178, README §2) --------------------------------------------
     def save(self, path: str | os.PathLike) -> None:

@@ -229,14 +229,28 @@ abnn_status records_h2d(const SynArrays& a, uint64_t first, uint64_t n, const ab
     return ABNN_OK;
 }
 
+// Every record names two neurons, or is the pruning tombstone {src = dst =
+// 0xFFFFFFFF} that downloads, .bnn and flat saves of a pruned brain hold
+// between structural updates (abnn.h; k_pack_src maps it to kSrcNone).
 abnn_status validate_records(const abnn_brain* b, const abnn_synapse* s, uint64_t n)
 {
     for (uint64_t i = 0; i < n; ++i)
-        if (s[i].src >= b->n_nrn || s[i].dst >= b->n_nrn) {
+        if ((s[i].src >= b->n_nrn || s[i].dst >= b->n_nrn) &&
+            !(s[i].src == 0xFFFFFFFFu && s[i].dst == 0xFFFFFFFFu)) {
             set_err("synapse " + std::to_string(i) + " has src/dst >= N_NRN (" +
                     std::to_string(b->n_nrn) + ")");
             return ABNN_ERR_INVALID;
         }
+    return ABNN_OK;
+}
+
+// Host-written records may hold tombstones (a saved pruned brain): recount the
+// structural update's per-block tally over them (pruning on only).
+abnn_status retally(abnn_brain* b, uint64_t first, uint64_t n)
+{
+    if (!b->d.dead || n == 0) return ABNN_OK;
+    HIP_TRY(launch_tally_dead(b->d.syn, b->dims.n_syn, b->d.dead, first, n, nullptr));
+    HIP_TRY(hipDeviceSynchronize());
     return ABNN_OK;
 }
 
@@ -253,7 +267,11 @@ void host_tick(abnn_brain* b)
 abnn_status time_begin(abnn_brain* b, hipStream_t s, EventPair** out)
 {
     *out = nullptr;
-    if (b->timing <= 0 || (b->timing_count++ % (uint64_t)b->timing) != 0) return ABNN_OK;
+    if (b->timing <= 0) return ABNN_OK;
+    // sampling every n-th launch starts at the second one: the first launch
+    // after enable_timing is the one most likely to carry a transient
+    const uint64_t n = (uint64_t)b->timing, c = b->timing_count++;
+    if (c % n != (n > 1 ? 1u : 0u)) return ABNN_OK;
     if (b->events_used == b->events.size()) {
         EventPair p;
         HIP_TRY(hipEventCreate(&p.a));
@@ -714,7 +732,8 @@ abnn_status abnn_upload_synapses(abnn_brain* b, uint64_t first, const abnn_synap
     REQUIRE(first <= b->dims.n_syn && n <= b->dims.n_syn - first, "range out of bounds");
     ST_TRY(validate_records(b, src, n));
     ST_TRY(sync_all(b));
-    return records_h2d(b->d.syn, first, n, src);
+    ST_TRY(records_h2d(b->d.syn, first, n, src));
+    return retally(b, first, n);
 }
 
 abnn_status abnn_download_synapses(abnn_brain* b, uint64_t first, abnn_synapse* dst, uint64_t n)
@@ -918,6 +937,13 @@ uint64_t abnn_exchange_bytes(const abnn_brain* b)
     return b ? 4ull * xchg_words(b->params.max_spikes) : 0;
 }
 
+abnn_status abnn_set_global_events(abnn_brain* b, uint64_t global_events)
+{
+    REQUIRE(b, "null argument");
+    b->dims.global_events = global_events;
+    return ABNN_OK;
+}
+
 abnn_status abnn_shard_gate(abnn_brain* b, void* xchg_dev, void* stream)
 {
     REQUIRE(b && xchg_dev, "null argument");
@@ -1046,6 +1072,17 @@ abnn_status abnn_get_kernel_time(abnn_brain* b, double* ms_total, uint64_t* laun
     return ABNN_OK;
 }
 
+abnn_status abnn_get_kernel_times(abnn_brain* b, float* out_ms, uint64_t cap, uint64_t* launches)
+{
+    REQUIRE(b && launches && (out_ms || cap == 0), "null argument");
+    ST_TRY(sync_all(b));
+    for (size_t i = 0; i < b->events_used && i < cap; ++i)
+        HIP_TRY(hipEventElapsedTime(&out_ms[i], b->events[i].a, b->events[i].b));
+    *launches = b->events_used;
+    b->events_used = 0;
+    return ABNN_OK;
+}
+
 // ---- persistence -----------------------------------------------------------
 
 abnn_status abnn_save_bnn(abnn_brain* b, const char* path)
@@ -1120,7 +1157,7 @@ abnn_status abnn_load_bnn(abnn_brain* b, const char* path)
         }
     }
     std::fclose(f);
-    return ABNN_OK;
+    return retally(b, 0, b->dims.n_syn);
 }
 
 abnn_status abnn_save_flat(abnn_brain* b, const char* path)
@@ -1241,7 +1278,7 @@ abnn_status abnn_load_flat(abnn_brain* b, const char* path)
         set_err(std::string("flat load failed: ") + path);
         return ABNN_ERR_IO;
     }
-    return ABNN_OK;
+    return retally(b, 0, N);
 }
 
 }  // extern "C"

@@ -168,6 +168,9 @@ hipError_t launch_pack_src(const SynArrays& a, const uint32_t* in_dev, uint64_t 
 hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t first, uint64_t n, hipStream_t s);
 hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offsets, const SynArrays& dst,
                           hipStream_t s);
+// dead[] (pruning tally) recounted for the blocks that hold records [first, first + count) of n
+hipError_t launch_tally_dead(const SynArrays& a, uint64_t n, uint32_t* dead, uint64_t first, uint64_t count,
+                             hipStream_t s);
 hipError_t launch_generate(const DeviceState& d, uint32_t n_in, uint32_t n_out, uint64_t seed,
                            hipStream_t s);
 hipError_t launch_checksum(const DeviceState& d, uint64_t* out_dev, hipStream_t s);

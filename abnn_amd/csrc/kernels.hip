@@ -1349,6 +1349,23 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint
     }
 }
 
+// The structural update's tombstone tally recounted from the records (after a
+// host upload, which may hold tombstones: a saved pruned brain): dead[b] =
+// tombstones among records [b kCompactChunk, (b + 1) kCompactChunk) of the
+// first n, for blocks b0 + blockIdx.x.
+__global__ __launch_bounds__(256) void k_tally_dead(SynArrays a, uint64_t n, uint32_t* dead, uint64_t b0)
+{
+    __shared__ uint64_t s_wave[4];
+    const uint64_t b = b0 + blockIdx.x, base = b * kCompactChunk;
+    uint64_t c = 0;
+    for (uint32_t k = threadIdx.x; k < (uint32_t)kCompactChunk; k += 256) {
+        const uint64_t i = base + k;
+        c += i < n && src_of(a, i) == kSrcNone;
+    }
+    c = block_sum<256>(c, s_wave);
+    if (threadIdx.x == 0) dead[b] = (uint32_t)c;
+}
+
 // ---------------------------------------------------------------------------
 // k_generate: synthetic graph (recipe of brain-engine.cpp:31-53, portable RNG).
 __global__ __launch_bounds__(256) void k_generate(DeviceState d, uint32_t n_in, uint32_t n_out,
@@ -1569,6 +1586,15 @@ hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offs
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_compact, dim3((uint32_t)((n + kCompactChunk - 1) / kCompactChunk)),
                        dim3(kCompactThreads), 0, s, syn, n, offsets, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_tally_dead(const SynArrays& a, uint64_t n, uint32_t* dead, uint64_t first, uint64_t count,
+                             hipStream_t s)
+{
+    if (count == 0 || first >= n) return hipSuccess;
+    const uint64_t b0 = first / kCompactChunk, b1 = (std::min(first + count, n) + kCompactChunk - 1) / kCompactChunk;
+    hipLaunchKernelGGL(k_tally_dead, dim3((uint32_t)(b1 - b0)), dim3(256), 0, s, a, n, dead, b0);
     return hipGetLastError();
 }
 

@@ -84,6 +84,9 @@ class TorchComm:
     def all_reduce_max(self, t) -> None:
         self._run(lambda x: self._dist.all_reduce(x, op=self._dist.ReduceOp.MAX, group=self.group), t)
 
+    def all_reduce_sum(self, t) -> None:
+        self._run(lambda x: self._dist.all_reduce(x, op=self._dist.ReduceOp.SUM, group=self.group), t)
+
 
 def sharded_pass(engine: Engine, comm, xchg, gathered) -> None:
     """One C1 pass over all shards: gate -> all-gather of the records -> apply -> commit."""
@@ -133,10 +136,24 @@ class ShardedBrain:
         self.xchg = torch.zeros(words, dtype=torch.int32, device=dev)
         self.gathered = torch.zeros(words * self.world, dtype=torch.int32, device=dev)
         self.engine = _GpuEngine(self.brain, lambda: torch.cuda.current_stream(dev))
+        self.compact_every = int(self.brain.params.compact_every)
+        self._passes = 0
 
     def step(self, passes: int = 1) -> None:
         for _ in range(passes):
             sharded_pass(self.engine, self.comm, self.xchg, self.gathered)
+            self._passes += 1
+            if self.compact_every and self._passes % self.compact_every == 0:
+                self.refresh_global_events()
+
+    def refresh_global_events(self) -> None:
+        """A structural update changed every shard's record count, and with it
+        the shard's visited events: re-sum them for the clock-tick rule
+        (abnn_set_global_events)."""
+        t = self._torch.tensor([self.brain.visited_events()], dtype=self._torch.int64, device=self.xchg.device)
+        self.comm.all_reduce_sum(t)
+        self.global_events = int(t.item())
+        self.brain.set_global_events(self.global_events)
 
     def local_events(self) -> int:
         return self.brain.visited_events()

@@ -11,6 +11,9 @@ generated on the GPU; every pass stamps all 256 inputs.
 One "step" = one whole pass: stimulus + bitmap + streaming gate + budget scan +
 apply + finalize (+ the two exchanges at N>1).  `value` = visited events of all
 ranks per second over the K timed steps (max over ranks of the wall time).
+Before the W warm-up passes, --settle untimed passes (default 64) take the
+freshly built graph through its start-up transient (lastFired = 0 gates every
+event in passes 0-5); the JSON reports them (config.settle_passes/settle_s).
 
 N > 1 (torchrun, one process per GPU, RCCL): the 1B-synapse graph is split in
 N contiguous shards; every GPU sweeps 150M events of its shard per pass
@@ -28,11 +31,24 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-TIMING_EVERY = 8       # gate launches sampled by HIP events (the roofline's average duration)
+# Start-up transient of a freshly built brain: lastFired = 0
+# makes passes 0-5 gate every event (passes 3-5 run the refractory stage on all
+# 150M), passes 6-9 drain it, and the recent set grows from ~8k to ~13k
+# neurons over passes ~42-55 as the spikes leave the 256 outputs.  These
+# passes run before warm-up, untimed, like loading a running brain.
+SETTLE_PASSES = 64
+
+
+def timing_every(steps: int) -> int:
+    """Gate launches sampled by HIP events (the roofline's average duration):
+    every 4th in short runs, every 8th from 100 timed passes on."""
+    return 4 if steps < 100 else 8
 
 
 def parse():
@@ -41,6 +57,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=200,
                     help="timed passes (the reference engine runs passes forever; 200 x ~0.13 ms)")
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--settle", type=int, default=SETTLE_PASSES,
+                    help="untimed passes from the freshly built graph to the steady state, before "
+                         "the warm-up (the start-up transient, DESIGN.md §6)")
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -91,17 +110,22 @@ def load_traffic(config: str):
         return None
 
 
-def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, extra: dict) -> dict:
+def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, extra: dict,
+                 settle: int) -> dict:
     """The threaded C oracle ("port") on the host cores.  Sweep: the pass only
     ever touches the first E synapses, so the sample holds exactly those and
-    produces the identical pass results.  Random mode: picks span the whole
-    graph, so the sample is a graph of at most 150M synapses (bounded host
-    memory and generation time) with the same neurons and events.  6 untimed
-    passes reach the steady state."""
+    produces the identical pass results (same settle passes as the GPU run, so
+    the same steady state).  Random mode: picks span the whole graph, so the
+    sample is a graph of at most 150M synapses (bounded host memory and
+    generation time) with the same neurons and events -- a REDUCED graph: the
+    picks hit a smaller working set than the GPU's, which likely overstates
+    the CPU rate."""
     from oracle import oracle as O
 
+    reduced = False
     if mode == 1:
         n_syn = min(wl.n_syn, 150_000_000)
+        reduced = n_syn < wl.n_syn
         E = O.visited_events(events, n_syn, 1)
         what = f"{n_syn:,}-synapse random graph ({wl.name} recipe), {E:,} random picks per pass"
     else:
@@ -114,12 +138,15 @@ def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, ex
     if extra:
         ob.set_reward(0.25)
         what += " with the same plasticity settings"
-    ob.pass_threaded(6, nthreads=threads)
+    ob.pass_threaded(settle, nthreads=threads)
     t0 = time.perf_counter()
     ob.pass_threaded(timed_passes, nthreads=threads)
     dt = time.perf_counter() - t0
     return {"value": timed_passes * E / dt, "unit": "events/s", "cores": threads, "kind": "port",
-            "sample": f"{what}, {wl.n_neuron:,} neurons, 6 untimed + {timed_passes} timed passes, "
+            "n_syn": n_syn, "graph": ("reduced: %d of %d synapses, picks hit a smaller working set than "
+                                      "the GPU's (likely overstates the CPU rate)" % (n_syn, wl.n_syn))
+            if reduced else "same records as the GPU run",
+            "sample": f"{what}, {wl.n_neuron:,} neurons, {settle} untimed + {timed_passes} timed passes, "
                       f"oracle_pass_threaded with {threads} threads"}
 
 
@@ -176,18 +203,26 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    # start-up transient (untimed): the freshly built graph to its steady state
+    ts = time.perf_counter()
+    step(args.settle)
+    sync()
+    settle_s = time.perf_counter() - ts
     step(args.warmup)
     sync()
     brain.reset_stats()
-    # HIP events around every 8th gate launch: an event pair costs ~11 us of
-    # stream time, so timing every pass would tax the measured rate
-    brain.enable_timing(TIMING_EVERY)
+    # HIP events around a sample of the gate launches (an event pair costs
+    # stream time, so timing every pass would tax the measured rate); the
+    # sample starts at the second timed launch
+    every = timing_every(args.steps)
+    brain.enable_timing(every)
     sync()
     t0 = time.perf_counter()
     step(args.steps)
     sync()
     dt = time.perf_counter() - t0
-    gate_ms, launches = brain.kernel_time()
+    launch_ms = brain.kernel_times()
+    gate_ms, launches = float(launch_ms.sum()), int(launch_ms.size)
     stats = brain.stats()
     if dist is not None:
         tdev = f"cuda:{device}" if backend == "nccl" else "cpu"
@@ -217,6 +252,12 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
             "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": launches,
+            "min_launch_ms": round(float(launch_ms.min()), 4) if launches else None,
+            "median_launch_ms": round(float(np.median(launch_ms)), 4) if launches else None,
+            "timing_every": every,
+            # a launch cannot take longer than the pass it is part of: if the
+            # sample says so, the timed window still held the transient
+            "steady": bool(launches and avg_gate_ms <= dt / args.steps * 1e3),
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "bytes_formula": ("3*E (24-bit src stream: 2-B lo + 1-B hi per event; E visited events) -- "
                               "DESIGN.md §5" if mode == 0 else
@@ -233,7 +274,9 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-            cpu = cpu_baseline(wl, events, mode, threads, args.cpu_passes, extra)
+            # random mode on the CPU is ~100x slower per pass: 6 settle passes
+            cpu = cpu_baseline(wl, events, mode, threads, args.cpu_passes, extra,
+                               args.settle if mode == 0 else min(args.settle, 6))
         out = {
             "metric": "traversal events/sec at 1B synapses, 5M neurons; achieved HBM GB/s",
             "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
@@ -249,6 +292,7 @@ def main():
                                     grown=stats.get("grown", 0)) if args.plasticity else None),
                 "parallelism": (f"synapse-shard dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)"))
                                if world > 1 else "single GPU",
+                "settle_passes": args.settle, "settle_s": round(settle_s, 4),
                 "pre_gated_frac": stats["pre_gated"] / max(1, stats["events"]),
                 "spikes_per_pass": stats["fired"] / max(1, stats["passes"]),
             },

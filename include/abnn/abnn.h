@@ -300,6 +300,11 @@ abnn_status abnn_synchronize(abnn_brain* b, void* stream);
  * exactly abnn_traverse.                                                     */
 #define ABNN_SUMMARY_WORDS 4
 uint64_t abnn_exchange_bytes(const abnn_brain* b);
+/* abnn_dims.global_events after the shards' record counts changed (structural
+ * updates): the visited events of all shards per pass (the clock-tick rule,
+ * brain.metal:61,129).  The caller sums the shards' visited events (an
+ * all-reduce) and sets it on every rank.                                    */
+abnn_status abnn_set_global_events(abnn_brain* b, uint64_t global_events);
 abnn_status abnn_shard_gate(abnn_brain* b, void* xchg_dev, void* stream);
 abnn_status abnn_shard_apply(abnn_brain* b, const void* gathered_dev, uint32_t world,
                              uint32_t rank, void* stream);
@@ -309,13 +314,18 @@ abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t 
 /* ---- statistics / timing ---------------------------------------------------- */
 abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out);   /* synchronises */
 abnn_status abnn_reset_stats(abnn_brain* b);
-/* every > 0: every `every`-th pass records HIP events around the gate
- * (streaming) kernel on the stream it is launched on (an event pair costs
- * ~11 us of stream time per pass, so sampling keeps it out of the rate);
- * 0: off.  abnn_get_kernel_time returns the summed milliseconds and the count
- * of timed launches since the last call.                                    */
+/* every > 0: HIP events around the gate (streaming) kernel, on the stream it
+ * is launched on, for every launch (every = 1) or every `every`-th launch
+ * starting with the second after this call (an event pair costs stream time,
+ * so sampling keeps it out of the rate; the first launch is skipped because
+ * it is the one most likely to carry a transient); 0: off.
+ * abnn_get_kernel_time returns the summed milliseconds and the count of timed
+ * launches since the last call; abnn_get_kernel_times the same launches one by
+ * one (up to `cap` of them into out_ms; *launches = how many were timed).
+ * Either call resets the record.                                            */
 abnn_status abnn_enable_timing(abnn_brain* b, int every);
 abnn_status abnn_get_kernel_time(abnn_brain* b, double* ms_total, uint64_t* launches);
+abnn_status abnn_get_kernel_times(abnn_brain* b, float* out_ms, uint64_t cap, uint64_t* launches);
 
 /* ---- persistence ------------------------------------------------------------
  * .bnn = u32 N_SYN, u32 N_NRN, N_SYN x 16-B SynapsePacked (Brain::save/load,

@@ -81,6 +81,45 @@ def test_plasticity_large_with_visits(gpu):
     assert g.stats() == o.stats()
 
 
+@pytest.mark.parametrize("fmt", ["bnn", "flat", "upload"])
+def test_pruned_brain_round_trips_before_its_structural_update(gpu, tmp_path, fmt):
+    """A pruned brain holds tombstones {src = dst = 0xFFFFFFFF} until its next
+    structural update; saving it there and loading the file into a fresh
+    handle must work and the structural update of the loaded
+    brain must compact exactly like the original's (its tombstone tally is
+    recounted from the loaded records)."""
+    import abnn_amd
+
+    kw = dict(p_new=0.0, compact_every=8)
+    g, o = _pair(0, **kw)
+    for _ in range(6):  # passes 3-5 prune; no structural update yet (pass_index 6 % 8)
+        g.encode_traversal(1)
+        o.pass_serial()
+    syn = g.download_synapses()
+    tomb = (syn["src"] == 0xFFFFFFFF) & (syn["dst"] == 0xFFFFFFFF)
+    assert tomb.any() and g.n_syn() == 120_000
+    h = abnn_amd.Brain(256, 256, 3000, 120_000, 120_000, syn_capacity=140_000, **dict(SP, seed=13, **kw))
+    if fmt == "bnn":
+        g.save(tmp_path / "m.bnn")
+        h.load(tmp_path / "m.bnn")
+    elif fmt == "flat":
+        g.save_flat(tmp_path / "m.flat")
+        h.load_flat(tmp_path / "m.flat")
+    else:
+        h.upload_synapses(syn)
+    if fmt != "flat":
+        h.set_last_fired(g.last_fired())
+    s = g.scalars()
+    h.set_scalars(s["clock"], s["reward"], s["rbar"], s["pass_index"])
+    h.set_auto_stimulus(0, 256)
+    assert np.array_equal(h.download_synapses().view(np.uint32), syn.view(np.uint32))
+    for k in range(4):  # through the structural update after pass_index 8
+        h.encode_traversal(1)
+        o.pass_serial()
+        _same(h, o, f"{fmt} pass {k}")
+    assert h.n_syn() < 120_000
+
+
 def test_plasticity_virtual_shards_vs_oracle_shards(gpu):
     import torch
 
