@@ -66,15 +66,21 @@ struct abnn_brain {
     // discontinuity, the highest lastFired value the host wrote (creation's
     // zeros included), the stimulus of the last kFiredRing passes, whether
     // the next pass's bitmap was built (and for which stimulus), borrowed
-    // state pointers handed out.  Bitmap and images are double-buffered by
-    // pass parity.
+    // state pointers handed out.  Bitmap and images are triple-buffered by
+    // pass % 3: read by pass p, built by pass p - 1, zeroed by pass p - 2.
     uint64_t clean_passes = 0, max_host_stamp = 0;
     uint64_t stim_ring[kFiredRing][2] = {};
     bool next_built = false;
     uint64_t built_stim[2] = {};
     bool ext_ptrs = false, force_full_bitmap = false;
-    uint32_t* bitmap_buf[2] = {};
-    uint32_t* filter_buf[2] = {};
+    uint32_t* bitmap_buf[3] = {};
+    uint32_t* filter_buf[3] = {};
+    // fused single-GPU sweep passes (ABNN_FUSED=0: gate + apply launches):
+    // whether the previous pass was fused (its gate costs are in cost_buf[cost
+    // parity ^ 1] and its prologue adapts the partition), the look-back words
+    bool use_fused = true, last_pass_fused = false;
+    uint32_t* cost_buf[2] = {};
+    uint32_t cost_parity = 0;
     bool pending_renorm = false;   // shard protocol: decided at gate time
     int timing = 0;                // time every timing-th gate launch (0: off)
     uint64_t timing_count = 0;
@@ -85,6 +91,7 @@ struct abnn_brain {
     uint64_t* u64_scratch = nullptr;
     int cus = 256, per_cu = 1;     // gate partition inputs (configure)
     uint64_t pass_host = 0;        // mirror of pass_index (structural-update schedule)
+    uint64_t rot = 0;              // passes run by this handle: the bitmap buffers' rotation (never reset)
     // structural updates (compact_every > 0): the second record buffer the
     // compaction writes into (swapped with d.syn), and its scan scratch
     SynArrays syn_alt{};
@@ -102,6 +109,14 @@ abnn_status sync_all(abnn_brain* b)
 {
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipDeviceSynchronize());
+    // a fused pass whose look-back gave up waiting (never expected: every
+    // gate workgroup is resident) reports it here instead of hanging the GPU
+    uint32_t err = 0;
+    if (b->d.work) HIP_TRY(hipMemcpy(&err, &b->d.work->error, 4, hipMemcpyDeviceToHost));
+    if (err) {
+        set_err("fused pass: a look-back wait timed out (results of that pass are invalid)");
+        return ABNN_ERR_HIP;
+    }
     return ABNN_OK;
 }
 
@@ -112,12 +127,14 @@ void free_all(abnn_brain* b)
     void* ptrs[] = {b->d.syn.lo,    b->d.syn.hi,     b->d.syn.dst,    b->d.syn.w,   b->d.syn.src32,
                     b->syn_alt.lo,  b->syn_alt.hi,   b->syn_alt.dst,  b->syn_alt.w, b->syn_alt.src32,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
-                    b->bitmap_buf[0], b->bitmap_buf[1], b->filter_buf[0], b->filter_buf[1], b->d.range_info,    b->d.range_g1,  b->d.g2x,
+                    b->bitmap_buf[0], b->bitmap_buf[1], b->bitmap_buf[2], b->filter_buf[0], b->filter_buf[1],
+                    b->filter_buf[2], b->cost_buf[0], b->cost_buf[1], b->d.lb_status,
+                    b->d.range_info,    b->d.range_g1,  b->d.g2x,
                     b->d.chunk_cnt,
                     b->d.wg_stats, b->d.claim,  b->d.g2src,      b->d.grown,
                     b->d.dead,      b->compact_offsets,
                     b->d.work,      b->idx_scratch,
-                    b->u64_scratch,  b->d.wave_clock,  b->d.apply_clock, b->d.fired_ring, b->d.n_fired_ring, b->d.range_bounds,  b->d.range_bounds_next,
+                    b->u64_scratch,  b->d.wave_clock,  b->d.apply_clock, b->d.fired_ring, b->d.n_fired_ring, b->d.range_bounds,  b->d.range_bounds_next, b->d.range_bounds_prev,
                     const_cast<uint32_t*>(b->d.dummy)};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -370,6 +387,7 @@ abnn_status structural_update(abnn_brain* b)
     grown += added;
     HIP_TRY(hipMemcpy(&d.work->stats.grown, &grown, 8, hipMemcpyHostToDevice));
     configure(b);
+    b->last_pass_fused = false;  // new ranges: the measured costs do not apply
     return reset_ranges(b);
 }
 
@@ -395,16 +413,18 @@ bool build_next_ok(const abnn_brain* b)
            b->clean_passes + 1 >= W && b->clock_host >= b->max_host_stamp + W;
 }
 
-// bitmap + streaming gate (with the refractory stage) [+ the exchange record
-// of a sharded pass]: the first half of every pass.
-abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
+// This pass's recent-spike buffers (triple-buffered by pass % 3) and, unless
+// the previous pass built them, the bitmap from lastFired (k_bitmap).
+abnn_status pass_buffers(abnn_brain* b, hipStream_t s)
 {
     DeviceState& d = b->d;
-    const uint64_t p = b->pass_host;
-    d.bitmap = b->bitmap_buf[p & 1];
-    d.filter = b->filter_buf[p & 1];
-    d.bitmap_next = b->bitmap_buf[(p + 1) & 1];
-    d.filter_next = b->filter_buf[(p + 1) & 1];
+    const uint64_t p = b->rot;  // not pass_host: set_scalars may move that
+    d.bitmap = b->bitmap_buf[p % 3];
+    d.filter = b->filter_buf[p % 3];
+    d.bitmap_next = b->bitmap_buf[(p + 1) % 3];
+    d.filter_next = b->filter_buf[(p + 1) % 3];
+    d.bitmap_clear = b->bitmap_buf[(p + 2) % 3];
+    d.filter_clear = b->filter_buf[(p + 2) % 3];
     d.stim_first = b->stim_first;
     d.stim_count = b->stim_count;
     const bool prebuilt = b->next_built && b->built_stim[0] == b->stim_first &&
@@ -413,18 +433,11 @@ abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
     if (!prebuilt) HIP_TRY(launch_bitmap(d, b->kp, b->stim_first, b->stim_count, s));
     b->stim_ring[b->pass_host % kFiredRing][0] = b->stim_first;
     b->stim_ring[b->pass_host % kFiredRing][1] = b->stim_count;
-    EventPair* ev = nullptr;
-    ST_TRY(time_begin(b, s, &ev));
-    HIP_TRY(launch_gate(b->d, b->kp, s));
-    if (ev) HIP_TRY(hipEventRecord(ev->b, s));
-    if (xchg_out) HIP_TRY(launch_scan(b->d, b->kp, xchg_out, s));
     return ABNN_OK;
 }
 
-// budget walk, weight update, stamps, pass end; k_apply writes the next
-// pass's partition into range_bounds_next, which becomes current here
-// (kernel arguments are captured at launch)
-abnn_status run_apply(abnn_brain* b, const int32_t* gathered, uint32_t world, uint32_t rank, hipStream_t s)
+// Whether this pass builds the next one's bitmap, and from which stimulus ranges.
+void plan_build(abnn_brain* b)
 {
     DeviceState& d = b->d;
     d.build_next = build_next_ok(b) ? 1u : 0u;
@@ -441,11 +454,69 @@ abnn_status run_apply(abnn_brain* b, const int32_t* gathered, uint32_t world, ui
         for (uint64_t q = p + 1 - W; q <= p; ++q) add(b->stim_ring[q % kFiredRing][0], b->stim_ring[q % kFiredRing][1]);
         add(b->stim_first, b->stim_count);
     }
+}
+
+// bitmap + streaming gate (with the refractory stage) [+ the exchange record
+// of a sharded pass]: the first half of every pass.
+abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
+{
+    ST_TRY(pass_buffers(b, s));
+    b->last_pass_fused = false;
+    EventPair* ev = nullptr;
+    ST_TRY(time_begin(b, s, &ev));
+    HIP_TRY(launch_gate(b->d, b->kp, s));
+    if (ev) HIP_TRY(hipEventRecord(ev->b, s));
+    if (xchg_out) HIP_TRY(launch_scan(b->d, b->kp, xchg_out, s));
+    return ABNN_OK;
+}
+
+// After a pass: the partition it computed for the next one becomes current
+// (kernel arguments are captured at launch), its own becomes the previous one.
+void rotate_bounds(abnn_brain* b)
+{
+    DeviceState& d = b->d;
+    uint32_t* prev = d.range_bounds_prev;
+    d.range_bounds_prev = d.range_bounds;
+    d.range_bounds = d.range_bounds_next;
+    d.range_bounds_next = prev;
+}
+
+// budget walk, weight update, stamps, pass end; k_apply writes the next
+// pass's partition into range_bounds_next (rotate_bounds)
+abnn_status run_apply(abnn_brain* b, const int32_t* gathered, uint32_t world, uint32_t rank, hipStream_t s)
+{
+    DeviceState& d = b->d;
+    plan_build(b);
     HIP_TRY(launch_apply(d, b->kp, gathered, world, rank, s));
     b->next_built = d.build_next != 0;
     b->built_stim[0] = b->stim_first;
     b->built_stim[1] = b->stim_count;
-    std::swap(b->d.range_bounds, b->d.range_bounds_next);
+    rotate_bounds(b);
+    return ABNN_OK;
+}
+
+// The whole single-GPU sweep pass in one launch (kernels.hip, k_gate<...,
+// kFused>): gate, look-back budget walk, weight update, stamps, pass end.  Its
+// prologue computes the next pass's partition (range_bounds_next) from the
+// previous fused pass's gate costs.
+abnn_status run_fused(abnn_brain* b, hipStream_t s)
+{
+    DeviceState& d = b->d;
+    ST_TRY(pass_buffers(b, s));
+    plan_build(b);
+    d.prologue_adapt = b->last_pass_fused && d.adapt_ranges ? 1u : 0u;
+    d.cost_in = b->cost_buf[b->cost_parity ^ 1u];
+    d.cost_out = b->cost_buf[b->cost_parity];
+    EventPair* ev = nullptr;
+    ST_TRY(time_begin(b, s, &ev));
+    HIP_TRY(launch_fused_pass(d, b->kp, s));
+    if (ev) HIP_TRY(hipEventRecord(ev->b, s));
+    b->next_built = d.build_next != 0;
+    b->built_stim[0] = b->stim_first;
+    b->built_stim[1] = b->stim_count;
+    rotate_bounds(b);
+    b->cost_parity ^= 1u;
+    b->last_pass_fused = true;
     return ABNN_OK;
 }
 
@@ -464,6 +535,7 @@ abnn_status run_commit(abnn_brain* b, const int32_t* gathered, uint32_t world, b
         b->clock_host = 0;
     }
     b->pass_host += 1;
+    b->rot += 1;
     const uint32_t ce = b->params.compact_every;
     if (ce != 0 && b->pass_host % ce == 0) ST_TRY(structural_update(b));  // README §5
     return ABNN_OK;
@@ -640,10 +712,14 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.reward = reinterpret_cast<float*>(sb + 1);
     d.rbar = d.reward + 1;
     d.pass_index = sb + 2;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
         if ((s = dalloc(&b->bitmap_buf[i], (uint64_t)d.n_bitmap_words + 2)) != ABNN_OK) return fail(s);
         if ((s = dalloc(&b->filter_buf[i], 2 * kMaxFilterWords)) != ABNN_OK) return fail(s);
     }
+    for (int i = 0; i < 2; ++i)
+        if ((s = dalloc(&b->cost_buf[i], max_ranges)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.lb_status, kMaxGateBlocks)) != ABNN_OK) return fail(s);
+    if (const char* env = std::getenv("ABNN_FUSED")) b->use_fused = std::atoi(env) != 0;
     d.bitmap = b->bitmap_buf[0];
     d.filter = b->filter_buf[0];
     if ((s = dalloc(&d.range_info, max_ranges)) != ABNN_OK) return fail(s);
@@ -669,13 +745,14 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     }
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.wave_clock, 4 * (uint64_t)kMaxRanges + 16)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.wave_clock, (uint64_t)kWaveClock * kMaxRanges + 32)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.apply_clock, 8 * (uint64_t)kWalkBlocks)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.fired_ring, (uint64_t)kFiredRing * std::max(1u, p.max_spikes))) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.n_fired_ring, kFiredRing)) != ABNN_OK) return fail(s);
     b->force_full_bitmap = std::getenv("ABNN_FULL_BITMAP") != nullptr;
     if ((s = dalloc(&d.range_bounds, max_ranges + 1)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.range_bounds_next, max_ranges + 1)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.range_bounds_prev, max_ranges + 1)) != ABNN_OK) return fail(s);
     d.adapt_ranges = std::getenv("ABNN_STATIC_RANGES") ? 0u : 1u;
     if ((s = reset_ranges(b)) != ABNN_OK) return fail(s);
     *out = b;
@@ -917,8 +994,12 @@ abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream)
     for (uint32_t i = 0; i < passes; ++i) {
         // the host reads the clock at encode time, before the pass (brain.cpp:127-128)
         const bool renorm = b->clock_host > b->params.renorm_thresh;
-        ST_TRY(run_gate(b, nullptr, s));
-        ST_TRY(run_apply(b, nullptr, 1, 0, s));
+        if (b->use_fused && fused_pass_supported(b->d)) {
+            ST_TRY(run_fused(b, s));
+        } else {
+            ST_TRY(run_gate(b, nullptr, s));
+            ST_TRY(run_apply(b, nullptr, 1, 0, s));
+        }
         ST_TRY(run_commit(b, nullptr, 1, renorm, s));
     }
     return ABNN_OK;
@@ -975,13 +1056,14 @@ abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t 
     return run_commit(b, static_cast<const int32_t*>(gathered_dev), world, renorm, s);
 }
 
-// Diagnostics (not part of abnn.h): the last pass's per-wave gate times
-// {start, stream done, end, hw id} in 100 MHz ticks, then the range bounds.
+// Diagnostics (not part of abnn.h): the last pass's per-wave gate times,
+// kWaveClock u64 per range (engine.h, DeviceState::wave_clock), 100 MHz ticks.
 abnn_status abnn_debug_wave_clock(abnn_brain* b, uint64_t* out, uint64_t n)
 {
     REQUIRE(b && out, "null argument");
     ST_TRY(sync_all(b));
-    HIP_TRY(hipMemcpy(out, b->d.wave_clock, std::min<uint64_t>(n, 4ull * kMaxRanges + 16) * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out, b->d.wave_clock, std::min<uint64_t>(n, (uint64_t)kWaveClock * kMaxRanges + 32) * 8,
+                      hipMemcpyDeviceToHost));
     return ABNN_OK;
 }
 

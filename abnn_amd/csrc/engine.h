@@ -25,15 +25,26 @@ static_assert(kMaxRanges % kApplyThreads == 0, "range prefix: whole ranges per t
 constexpr int kDummyRecords = 64 * 32;  // >= 64 lanes x max events per lane; also the record-buffer padding
 constexpr uint32_t kFiredRing = 8;     // spike lists kept (the bitmap build needs window_pre < kFiredRing)
 constexpr uint32_t kChunk = 384;        // pre-gated events per chunk (staged in LDS by a gate wave)
+constexpr uint32_t kWaveClock = 12;     // diagnostics: u64 words per gate wave (wave_clock)
 constexpr uint32_t kChunkSlotDiv = 128; // chunk_cnt index = (region + c * kChunk) / 128 (unique per chunk)
 
 // Per-pass bookkeeping in device memory (one per handle).
 struct alignas(16) PassWork {
     uint32_t t0_g2;        // global event 0 passed both gates this pass (re-armed by finalize_pass)
-    uint32_t ticket;       // k_apply workgroups done this pass (the last one finalizes, re-arms it)
-    uint32_t pad[2];
+    uint32_t ticket;       // k_apply (fused pass: gate) workgroups done this pass (the last one finalizes, re-arms it)
+    uint32_t epoch;        // fused passes run so far: tags this pass's look-back words (never set by the host)
+    uint32_t error;        // fused pass: a look-back wait gave up (abnn_synchronize reports it)
+    uint32_t spec_wgs;     // fused pass: gate workgroups predicted below the budget cut (the last pass's, less one)
+    uint32_t pad[3];
     abnn_stats stats;      // host-kept counters (grown); the device ones live in DeviceState::wg_stats
 };
+
+// Fused single-GPU sweep pass (k_gate<..., kFused>): per gate
+// workgroup one look-back word {tag = epoch + 1 : 32 | kind : 2 | value : 30},
+// kind 1 = the spike candidates of the workgroup's ranges (capped at the
+// budget).  max_spikes < 2^30.
+constexpr uint32_t kLbAggregate = 1u;
+constexpr uint32_t kLbSpinLimit = 1u << 22;  // ~1 s of polls: then error, never a hang
 
 // Synapse records on the device, structure of arrays: record
 // i is {src[i], dst[i], w[i]} (SynapsePacked without its never-read pad).
@@ -76,8 +87,10 @@ struct DeviceState {
     float* rbar;              // [1]
     uint32_t* bitmap;         // [n_bitmap_words] exact recent-spike bitmap of this pass
     uint32_t* filter;         // [2 * filter_words] the two folded bitmap images of this pass
-    uint32_t* bitmap_next;    // the next pass's (double-buffered by pass parity; zeroed by the gate)
+    uint32_t* bitmap_next;    // the next pass's (triple-buffered by pass % 3; zeroed by the pass before)
     uint32_t* filter_next;
+    uint32_t* bitmap_clear;   // the one after it (pass + 2): zeroed by this pass's gate
+    uint32_t* filter_clear;
     uint64_t stim_first, stim_count;  // this pass's stimulus range (stamped `now` at pass start)
     uint32_t build_next;      // k_apply builds bitmap_next / filter_next (steady state)
     uint32_t n_next_stim;     // stimulus ranges of passes p+1-W..p+1 (distinct), for the build
@@ -93,12 +106,15 @@ struct DeviceState {
     uint32_t* dead;           // pruning on: tombstones per kCompactChunk records (structural update)
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     PassWork* work;
-    uint64_t* wave_clock;     // [4 * n_ranges] per-wave gate times {start, stream done, end, entry} (100 MHz, diagnostics)
+    uint64_t* wave_clock;     // [kWaveClock * n_ranges] per-wave gate times {start, stream done, refractory
+                              // tail done, entry, (fused) look-back done, walk done} (100 MHz, diagnostics)
     uint32_t* fired_ring;     // [kFiredRing * max_spikes] spike list of pass q at (q % kFiredRing), budget order
     uint32_t* n_fired_ring;   // [kFiredRing] their lengths (k_apply workgroup 0)
     uint64_t* apply_clock;    // [8 * kWalkBlocks] per-workgroup k_apply timeline (diagnostics, 100 MHz)
     uint32_t* range_bounds;   // [n_ranges + 1] first iteration of each range (this pass)
-    uint32_t* range_bounds_next;  // [n_ranges + 1] the next pass's (partition_bounds in k_apply; the host swaps)
+    uint32_t* range_bounds_next;  // [n_ranges + 1] the next pass's (k_apply's partition_bounds, or the fused
+                                  // pass's prologue; the host rotates the three)
+    uint32_t* range_bounds_prev;  // [n_ranges + 1] the previous pass's (the fused prologue's cost curve)
     uint32_t adapt_ranges;    // rebalance the partition after every pass (default on; ABNN_STATIC_RANGES=1: off)
     uint32_t adapt_gain;      // a boundary moves adapt_gain / 4 of the way to its target (1..4, ABNN_ADAPT_GAIN; default 2)
     uint32_t chunk_penalty;   // partition cost added per full chunk, 40-ns units (ABNN_CHUNK_PENALTY)
@@ -106,6 +122,13 @@ struct DeviceState {
     uint32_t tail_prio;       // gate issue priority for a wave's tail, 0..3 (4: keep; ABNN_TAIL_PRIO)
     uint32_t prio_clock;      // gate priority rotation by wall clock (1) or by iteration (0; ABNN_PRIO_CLOCK)
     uint32_t range_map;       // gate wave -> range: 0 blocked (workgroup b: ranges b*NW..), 1 interleaved (ABNN_RANGE_MAP=1)
+    // fused pass: look-back words [gate_blocks]; gate costs of the previous
+    // pass (read by the prologue when prologue_adapt) and of this one
+    uint64_t* lb_status;
+    const uint32_t* cost_in;
+    uint32_t* cost_out;
+    uint32_t prologue_adapt;  // the previous pass was fused over the same ranges: its costs move the next
+                              // pass's partition (computed in this one's prologue)
     uint64_t n_syn;           // local records
     uint64_t n_nrn;
     uint32_t n_input;
@@ -154,6 +177,11 @@ int gate_blocks_per_cu(uint32_t block, uint32_t k, uint32_t filter_words, bool t
 hipError_t launch_bitmap(const DeviceState& d, const KernelParams& kp, uint64_t stim_first,
                          uint64_t stim_count, hipStream_t s);
 hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t s);
+// The whole single-GPU sweep pass in one launch (gate + look-back budget walk +
+// weight update + stamps + pass end).  fused_pass_supported: the shape and
+// range count it is compiled for.
+bool fused_pass_supported(const DeviceState& d);
+hipError_t launch_fused_pass(const DeviceState& d, const KernelParams& kp, hipStream_t s);
 // Sharded passes: this shard's exchange record (summary + local spike list).
 hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out, hipStream_t s);
 // The rest of the pass: budget walk, weight update, stamps and, in its last

@@ -115,6 +115,10 @@ __device__ __forceinline__ uint32_t wave_uniform(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
+// Global-memory views for agent-scope atomics (sc1 loads and stores).
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k)
 {
     uint64_t z = seed + (k + 1u) * 0x9E3779B97F4A7C15ull;
@@ -231,8 +235,10 @@ __device__ uint64_t block_sum(uint64_t v, uint64_t* s_wave)
     return t;
 }
 
-// Exclusive scan of one u64 per thread over an NT-thread workgroup.
-template <int NT = kScanThreads>
+// Exclusive scan of one u64 per thread over an NT-thread workgroup.  kLds:
+// LDS-only barriers (the waves' outstanding global loads and stores stay in
+// flight).
+template <int NT = kScanThreads, bool kLds = false>
 __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total, uint64_t* s_wave)
 {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -244,14 +250,16 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total, uint64_t* 
         if (lane >= (uint32_t)o) inc += y;
     }
     if (lane == 63) s_wave[wid] = inc;
-    __syncthreads();
+    if (kLds) lds_barrier();
+    else __syncthreads();
     uint64_t before = 0, tot = 0;
     for (uint32_t w = 0; w < nw; ++w) {
         uint64_t x = s_wave[w];
         if (w < wid) before += x;
         tot += x;
     }
-    __syncthreads();
+    if (kLds) lds_barrier();
+    else __syncthreads();
     *total = tot;
     return before + inc - v;
 }
@@ -365,6 +373,31 @@ __device__ __forceinline__ void wave_set_next(const DeviceState& d, bool act, ui
     if (act) recent_set_next_word(d, j, 1u << (n & 31u));
 }
 
+// Fused pass: wave_set_next behind a per-workgroup LDS cache of the bitmap
+// words this workgroup has already set this pass (a direct-mapped {word, bits}
+// per slot, written whole as one 8-B LDS word, so an entry never claims a bit
+// it has not set; a lost update only costs a repeated atomic).  The dense
+// input->output ranges fire the 256 outputs over and over: without it their
+// same-word atomics serialise the walk.
+constexpr uint32_t kSetCache = 256;
+
+__device__ __forceinline__ void wave_set_next_dedup(const DeviceState& d, bool act, uint32_t n, uint64_t* cache)
+{
+    const uint32_t j = n >> 5, bit = 1u << (n & 31u);
+    uint64_t* c = cache + (j & (kSetCache - 1));
+    if (act) {
+        const uint64_t e = *c;
+        if ((uint32_t)(e >> 32) == j && ((uint32_t)e & bit)) act = false;
+    }
+    if (__ballot(act) == 0) return;
+    wave_set_next(d, act, n);
+    if (act) {
+        const uint64_t e = *c;
+        const uint32_t b = (uint32_t)(e >> 32) == j ? (uint32_t)e | bit : bit;
+        *c = (uint64_t)j << 32 | b;
+    }
+}
+
 // The items of the build that do not depend on this pass: the spike lists of
 // passes p+1-W..p-1 and the stimulus ranges.  Item x of k_apply thread t of
 // workgroup g is x = t * gridDim + g (every workgroup gets a few), its loads
@@ -440,9 +473,17 @@ __device__ __forceinline__ uint4 range_totals(const DeviceState& d, uint32_t r) 
 // compacted from g2x[base] on.  `at(q)` yields the q-th staged {offset, src}.
 // Batches of R rounds of 64 keep every load of a lane in flight at once.
 // Returns {pre-gated, survivors, candidates, 0}.
-template <int R, bool kRandom, class At>
+// kFused: the entry is {offset | candidate << 31, w, updated w, dst} -- every
+// input of the update (brain.metal:101-121) is known here (w, the candidate
+// bit, isi, the pass-start reward and rBar); the budget walk only decides
+// whether the event is below the budget (then fired = candidate).  With spec
+// (the workgroup is predicted to lie below the pass's budget cut) the updated
+// weight is stored here already; the walk restores w where the prediction was
+// wrong.
+template <int R, bool kRandom, bool kFused, class At>
 __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const KernelParams& kp, uint64_t region,
-                                              uint64_t base, uint32_t n, uint64_t now, uint64_t pass, At&& at)
+                                              uint64_t base, uint32_t n, uint64_t now, uint64_t pass, float Rw,
+                                              float rbw, bool spec, At&& at)
 {
     const uint32_t lane = threadIdx.x & 63, nn = (uint32_t)d.n_nrn;
     uint32_t n_g1 = 0, n_g2 = 0, n_cand = 0;
@@ -485,16 +526,418 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
             const uint64_t bg = __ballot(g2);
             if (g2) {
                 const uint64_t o = base + n_g2 + mbcnt64(bg);
-                const uint32_t isi = __float_as_uint((float)(now - ld[j])) | (cand ? 0x80000000u : 0u);
-                d.g2x[o] = make_uint4(rel[j], isi, __float_as_uint(w[j]), dst[j]);
+                if constexpr (kFused) {
+                    const float wn = updated_weight(kp, w[j], cand, Rw, rbw, (float)(now - ld[j]));
+                    d.g2x[o] = make_uint4(rel[j] | (cand ? 0x80000000u : 0u), __float_as_uint(w[j]),
+                                          __float_as_uint(wn), dst[j]);
+                    if (spec) __builtin_nontemporal_store(wn, d.syn.w + region + rel[j]);  // brain.metal:122
+                } else {
+                    const uint32_t isi = __float_as_uint((float)(now - ld[j])) | (cand ? 0x80000000u : 0u);
+                    d.g2x[o] = make_uint4(rel[j], isi, __float_as_uint(w[j]), dst[j]);
+                }
                 if (d.g2src) d.g2src[o] = src[j];  // synaptogenesis keeps src
-                if (tg == 0) d.work->t0_g2 = 1u;
+                if (tg == 0)  // read by the pass's last workgroup (fused pass): write-through
+                    __hip_atomic_store((gu32*)&d.work->t0_g2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             n_g2 += (uint32_t)__popcll(bg);
             n_cand += (uint32_t)__popcll(__ballot(cand));
         }
     }
     return make_uint4(n_g1, n_g2, n_cand, 0u);
+}
+
+// ---------------------------------------------------------------------------
+// The weight update of one event that reached it (brain.metal:101-126), shared
+// by k_apply and the fused pass.  Per-pass inputs are the pass-start scalars
+// (C1); the counters are the caller's.
+struct ApplyCtx {
+    float R, rb;
+    uint64_t now, pass;
+    bool random;     // random-edge mode: only the claim's winner stores
+    bool stamp;      // stamp lastFired[dst] = now here (k_apply, single GPU)
+    bool ring;       // write the spike list (fired_ring, budget position)
+    bool ring_sc1;   // ... write-through: the fused pass's last workgroup reads it in-launch
+    bool prune, genesis;
+    bool precomputed;  // the entry holds the updated weight (fused pass: refrac_chunk<..., kFused>)
+    uint32_t upd, nf, npr;
+};
+
+// A spike of the pass (brain.metal:125-126): stamp (k_apply), the spike list
+// (budget position pre), synaptogenesis.
+__device__ __forceinline__ void record_spike(const DeviceState& d, const KernelParams& kp, ApplyCtx& c,
+                                             const uint4& e, uint64_t pre, uint64_t slot)
+{
+    if (c.stamp) d.last_fired[e.w] = c.now;  // brain.metal:125-126
+    if (c.ring) {
+        uint32_t* q = d.fired_ring + (c.pass & (kFiredRing - 1)) * kp.max_spikes + pre;
+        if (c.ring_sc1) __hip_atomic_store((gu32*)q, e.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *q = e.w;
+    }
+    ++c.nf;
+    if (c.genesis) {  // README §5 synaptogenesis: slot `pre` of this pass
+        const uint64_t x = splitmix64_at(d.seed ^ ABNN_GENESIS_KEY, (c.pass << 32) | pre);
+        if (unit24(x) < kp.p_new) {
+            const uint64_t span = d.n_nrn - d.n_input;
+            d.grown[(c.pass % kp.compact_every) * kp.max_spikes + pre] =
+                make_uint4(d.g2src[slot], d.n_input + (uint32_t)(((x & 0xFFFFFFFFull) * span) >> 32),
+                           __float_as_uint(kp.w_init), 1u);
+        }
+    }
+}
+
+__device__ __forceinline__ void apply_event(const DeviceState& d, const KernelParams& kp, ApplyCtx& c,
+                                            uint64_t region, const uint4& e, bool f, uint64_t pre, uint64_t slot)
+{
+    const float w = c.precomputed ? __uint_as_float(e.z)
+                                  : updated_weight(kp, __uint_as_float(e.z), f, c.R, c.rb, __uint_as_float(e.y & 0x7FFFFFFFu));
+    const uint64_t t = region + e.x, ri = rec_index(d, t, c.pass);
+    // random mode: of the events that updated one synapse this pass, the
+    // highest (k_claim) stores its weight; every one of them still counts
+    const bool store = !c.random || d.claim[ri] == (uint32_t)(t + 1);
+    if (c.random && store) d.claim[ri] = 0u;  // re-armed for the next pass
+    // brain.metal:122.  Non-temporal: a plain 4-B store leaves ~160k
+    // scattered dirty partial lines per pass whose write-back lands in the
+    // middle of the next pass's record stream (+30 us of gate time,
+    // tools/exp_variants.py).
+    if (store && c.prune && w < kp.w_prune) {  // README §5: the synapse is removed
+        set_src(d.syn, ri, kSrcNone);
+        __builtin_nontemporal_store(0xFFFFFFFFu, d.syn.dst + ri);
+        __builtin_nontemporal_store(w, d.syn.w + ri);
+        if (d.dead) atomicAdd(d.dead + ri / kCompactChunk, 1u);  // tally for the structural update
+        ++c.npr;
+    } else if (store) {
+        __builtin_nontemporal_store(w, d.syn.w + ri);
+    }
+    ++c.upd;
+    if (f) record_spike(d, kp, c, e, pre, slot);
+}
+
+// One boundary of the adaptive sweep partition (partition_bounds below, and
+// the fused pass's prologue): boundary k moves adapt_gain / 4 of the way from
+// `from` (its place this pass) towards the iteration where a measured
+// cumulative gate cost cc (exclusive prefix over the ranges of bounds rb,
+// cc[NR] = total) reaches k / NR of the total, rounded to the nearest
+// iteration.
+__device__ __forceinline__ uint32_t adapted_bound(const DeviceState& d, const uint32_t* cc, const uint32_t* rb,
+                                                  uint32_t NR, uint32_t k, uint32_t total_cost, uint32_t from)
+{
+    uint32_t nb = from;
+    if (d.adapt_ranges && k > 0 && k < NR && total_cost > 0) {
+        const uint32_t T = (uint32_t)((uint64_t)k * total_cost / NR);
+        uint32_t lo = 0, hi = NR;  // last range with cc <= T (its cost is > 0)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (cc[mid] <= T) lo = mid;
+            else hi = mid;
+        }
+        // target in 1/256 iterations; both terms of the move are monotonic
+        // in k, so ranges never overlap
+        const uint32_t cr = cc[lo + 1] - cc[lo];
+        const uint64_t tfp = (uint64_t)rb[lo] * 256u +
+                             (cr ? (uint64_t)(T - cc[lo]) * (rb[lo + 1] - rb[lo]) * 256u / cr : 0u);
+        const uint32_t g = d.adapt_gain;
+        nb = (uint32_t)(((uint64_t)from * 256u * (4u - g) + tfp * g + 512u) >> 10);
+    }
+    return nb;
+}
+
+// ---------------------------------------------------------------------------
+// Fused single-GPU sweep pass (k_gate<..., kFused>): the budget
+// walk of k_apply moves into the gate waves, with a decoupled look-back at
+// workgroup level.  When every wave of workgroup b is through its refractory
+// stage, b publishes the spike candidates of its ranges (capped at the
+// budget) in its look-back word; wave 0 then sweeps the words of ALL lower
+// workgroups in one poll (up to 8 per lane, write-through loads) until they are
+// all published -- their sum (capped) is the candidates before b -- and every
+// wave walks its own survivors from there.  The words are tagged with the
+// pass's epoch, so none is reset between passes.  Every published value is a
+// lower bound of the candidates before b, so a workgroup stops waiting as soon
+// as the published ones reach the budget: workgroups past the budget's end
+// never wait for stragglers.  Once EVERY word is published, every refractory
+// stage of the pass (the lastFired reads) is done: the workgroups that own
+// spikes stamp them (brain.metal:125-126) and workgroup 0 ends the pass --
+// no ticket, no last workgroup.
+constexpr uint32_t kLbMaxWords = 8;  // look-back words per lane: gate_blocks <= 512
+constexpr uint32_t kFusedMaxRanges = 4096;  // the partition's LDS cost prefix (FusedLds::cc)
+
+// One wave sweeps the words of workgroups [0, n): their values (capped sum)
+// once all carry `tag`, or as soon as the published ones reach the budget
+// (stop_at_budget).  vals: this lane's words (q = 64 i + lane), for the caller.
+__device__ uint32_t wg_poll(const DeviceState& d, uint32_t n, uint32_t tag, uint32_t budget, bool stop_at_budget,
+                            uint32_t (&vals)[kLbMaxWords])
+{
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t spins = 0;; ++spins) {  // wave-uniform
+        uint64_t sum = 0;
+        bool ok = true;
+#pragma unroll
+        for (uint32_t i = 0; i < kLbMaxWords; ++i) {
+            const uint32_t q = i * 64 + lane;
+            vals[i] = 0u;
+            if (i * 64 < n && q < n) {
+                const uint64_t s = __hip_atomic_load((gu64*)(d.lb_status + q), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                const bool mine = (uint32_t)(s >> 32) == tag;
+                vals[i] = mine ? (uint32_t)s & 0x3FFFFFFFu : 0u;
+                sum += vals[i];
+                ok = ok && mine;
+            }
+        }
+        const uint64_t tot = wave_sum<uint64_t>(sum);
+        if (__ballot(!ok) == 0 || (stop_at_budget && tot >= budget)) return (uint32_t)(tot < budget ? tot : budget);
+        if (spins >= kLbSpinLimit) {  // never hang the GPU: report and go on
+            if (lane == 0) __hip_atomic_store((gu32*)&d.work->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return budget;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// The NEXT pass's boundaries of this workgroup's ranges, range_bounds_next[k]
+// for k in [b NW, (b + 1) NW) (and NR by the last workgroup), by ONE wave --
+// the first of the workgroup through its refractory stage, so off the
+// critical path.  With prologue_adapt they move from this pass's bounds
+// towards the cost curve the previous pass measured over its bounds (cost_in
+// over range_bounds_prev: one pass more lag than k_apply's partition_bounds,
+// which moves from the bounds its costs were measured over); cc: the LDS
+// exclusive cost prefix (NR + 1 u32).  Otherwise they stay.
+template <int NW>
+__device__ void fused_next_bounds(const DeviceState& d, uint32_t* cc)
+{
+    const uint32_t lane = threadIdx.x & 63, NR = d.n_ranges, k = blockIdx.x * NW + lane;
+    const bool mine = (lane < (uint32_t)NW || k == NR) && k <= NR;  // this workgroup's boundaries
+    if (!d.prologue_adapt || !d.adapt_ranges || NR < 2) {  // wave-uniform
+        if (mine) d.range_bounds_next[k] = d.range_bounds[k];
+        return;
+    }
+    // rows of 64 costs, coalesced, 8 rows of loads in flight per lane; each
+    // row scanned across the wave (DPP) on top of the rows before it
+    const uint32_t rows = (NR + 63) / 64;  // NR <= kFusedMaxRanges
+    uint32_t run = 0;
+    for (uint32_t j0 = 0; j0 < rows; j0 += 8) {  // wave-uniform
+        uint32_t v[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+            const uint32_t q = (j0 + u) * 64 + lane;
+            v[u] = q < NR ? d.cost_in[q] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+            const uint32_t q = (j0 + u) * 64 + lane;
+            const uint32_t inc = wave_incl_scan(v[u]);
+            if (q < NR) cc[q] = run + inc - v[u];
+            run += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        }
+    }
+    const uint32_t total = run;
+    if (lane == 0) cc[NR] = total;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    if (mine) d.range_bounds_next[k] = adapted_bound(d, cc, d.range_bounds_prev, NR, k, total, d.range_bounds[k]);
+}
+
+// LDS of the fused pass's end (per workgroup).
+template <int NW>
+struct FusedLds {
+    uint64_t setc[kSetCache];          // wave_set_next_dedup's cache
+    uint32_t cc[kFusedMaxRanges + 1];  // fused_next_bounds
+    uint32_t cand[NW];                 // spike candidates of each wave's range (capped at the budget)
+    uint32_t stat[5];                  // pre-gated, survivors, updated, fired, pruned
+    uint32_t excl;                     // candidates of all lower workgroups (capped)
+    uint32_t done;                     // waves through their refractory stage
+    uint32_t total;                    // candidates of the pass (capped; workgroup 0)
+};
+
+// Fused pass: range r's wave after its refractory stage (g1 pre-gated, S
+// survivors -- contiguous from g2x[region] -- and C spike candidates; its
+// stream took `stream_cost` 40-ns units, the next pass's partition cost): the
+// next partition (first wave of the workgroup), its share of the next bitmap
+// build, the workgroup look-back, the walk of its own survivors, statistics,
+// the stamps of the workgroup's spikes once every refractory stage of the
+// pass is done, and (workgroup 0) the pass's end.  Pass-start scalars (C1) as
+// read at kernel entry.
+template <int BLOCK, int NW>
+__device__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region, uint32_t g1,
+                          uint32_t S, uint32_t C, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
+                          float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L, uint64_t t_entry,
+                          uint64_t t_start, uint64_t t_stream)
+{
+    constexpr uint32_t RW = kChunk / 64;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
+    const uint32_t tag = epoch + 1u;
+    const uint64_t t_tail = __builtin_amdgcn_s_memrealtime();
+    uint32_t order = 0;
+    if (lane == 0) {
+        L.cand[wid] = C < budget ? C : budget;
+        const uint32_t cost = stream_cost;
+        d.cost_out[r] = empty ? 0u : (cost < 1 ? 1u : (cost > 0xFFFFu ? 0xFFFFu : cost));
+        order = atomicAdd(&L.done, 1u);
+    }
+    if (wave_uniform(order) == 0) fused_next_bounds<NW>(d, L.cc);
+    // this wave's share of the next pass's bitmap build that does not depend
+    // on this pass (the spike lists of passes p+1-W..p-1, the stimulus): it
+    // fills the wait for the workgroup's other ranges
+    if (d.build_next) {
+        const uint64_t nitems = next_items(d, kp), step = (uint64_t)d.n_ranges * 64;
+        for (uint64_t x0 = (uint64_t)r * 64; x0 < nitems; x0 += step) {  // wave-uniform
+            const uint64_t x = x0 + lane;
+            const NextItem it = x < nitems ? next_item_load(d, kp, pass, x) : NextItem{0u, 0u, 0u};
+            wave_set_next_dedup(d, it.i < it.lim, it.n, L.setc);
+        }
+    }
+    lds_barrier();  // every range of the workgroup through its refractory stage
+    uint32_t vals[kLbMaxWords];
+    if (wid == 0) {
+        uint32_t c = lane < (uint32_t)NW ? L.cand[lane] : 0u;
+        c = wave_sum(c);
+        if (lane == 0)
+            __hip_atomic_store((gu64*)(d.lb_status + blockIdx.x),
+                               (uint64_t)tag << 32 | (uint64_t)kLbAggregate << 30 | (c < budget ? c : budget),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t e = wg_poll(d, blockIdx.x, tag, budget, true, vals);
+        if (lane == 0) L.excl = e;
+    }
+    lds_barrier();
+    const uint32_t excl_wg = L.excl;
+    uint64_t P = excl_wg;
+    uint64_t c_wg = 0;  // the workgroup's candidates
+    for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
+        if (w < wid) P += L.cand[w];
+        c_wg += L.cand[w];
+    }
+    const uint64_t t_lb = __builtin_amdgcn_s_memrealtime();
+    // the budget walk of k_apply over this range alone, in event order
+    ApplyCtx ac{R, rb, now, pass, false, false, true, false, kp.w_prune > 0.0f, d.grown != nullptr && kp.p_new > 0.0f,
+                true, 0u, 0u, 0u};
+    // batches of RW x 64 survivors; the next batch's loads are issued before
+    // this one's stores (gfx9's vmcnt also counts stores: a load issued after
+    // them would wait for them)
+    uint4 e[RW];
+    auto load_batch = [&](uint32_t b0, uint4 (&x)[RW]) {
+#pragma unroll
+        for (uint32_t j = 0; j < RW; ++j) {
+            const uint32_t q = b0 + j * 64 + lane;
+            x[j] = q < S ? d.g2x[region + q] : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    // spec (refrac_chunk stored every updated weight already): only the
+    // spikes, and a restore of w from the budget's end on; once every
+    // candidate of the range is below the budget the rest needs nothing.
+    // Otherwise the walk of k_apply, which ends at the budget.
+    uint32_t upd_rest = 0;  // spec: survivors below the budget not visited (wave-uniform)
+    uint32_t seen = 0;      // candidates visited
+    const bool walk = spec ? !(C == 0 && P < budget) : P < budget;
+    if (walk) load_batch(0, e);
+    else if (spec) upd_rest = S;
+    for (uint32_t b0 = 0; walk && b0 < S; b0 += RW * 64) {  // wave-uniform
+        if (!spec && P >= budget) break;
+        if (spec && P < budget && seen == C) {
+            upd_rest = S - b0;
+            break;
+        }
+        uint4 en[RW];
+        if (b0 + RW * 64 < S) load_batch(b0 + RW * 64, en);
+#pragma unroll
+        for (uint32_t j = 0; j < RW; ++j) {
+            if (b0 + j * 64 >= S || (!spec && P >= budget)) break;  // wave-uniform
+            const uint32_t q = b0 + j * 64 + lane;
+            const bool v = q < S, cand = v && (e[j].x >> 31);
+            const uint4 x = make_uint4(e[j].x & 0x7FFFFFFFu, e[j].y, e[j].z, e[j].w);
+            const uint64_t bc = __ballot(cand);
+            const uint64_t pre = P + mbcnt64(bc);  // spike candidates before this event
+            const bool below = v && pre < budget;
+            if (!spec) {
+                if (below) apply_event(d, kp, ac, region, x, cand, pre, region + q);
+            } else if (below) {
+                ++ac.upd;
+                if (cand) record_spike(d, kp, ac, x, pre, region + q);
+            } else if (v) {  // mispredicted: past the budget, w stays (brain.metal:85-88)
+                __builtin_nontemporal_store(__uint_as_float(x.y), d.syn.w + region + x.x);
+            }
+            if (d.build_next) wave_set_next_dedup(d, cand && pre < budget, x.w, L.setc);  // this pass's spikes
+            P += (uint64_t)__popcll(bc);
+            seen += (uint32_t)__popcll(bc);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < RW; ++j) e[j] = en[j];
+    }
+    const uint64_t t_walk = __builtin_amdgcn_s_memrealtime();
+    const uint32_t wu = wave_sum(ac.upd) + upd_rest, wf = wave_sum(ac.nf), wp = wave_sum(ac.npr);
+    if (lane == 0) {
+        atomicAdd(&L.stat[0], g1);
+        atomicAdd(&L.stat[1], S);
+        atomicAdd(&L.stat[2], wu);
+        atomicAdd(&L.stat[3], wf);
+        atomicAdd(&L.stat[4], wp);
+        uint64_t* wc = d.wave_clock + (uint64_t)kWaveClock * r;  // diagnostics (tools/wave_clock.py)
+        wc[0] = t_start;
+        wc[1] = t_stream;
+        wc[2] = t_tail;
+        wc[3] = t_entry;
+        wc[4] = t_lb;
+        wc[5] = t_walk;
+        wc[8] = S;
+        wc[9] = C;
+        wc[10] = excl_wg;
+        wc[11] = wu;
+    }
+    // the workgroup's spikes: budget positions [s0, s1) of the spike list,
+    // written by its waves (plain stores: this workgroup reads them, behind
+    // the barrier's workgroup-scope fence)
+    const uint32_t s0 = excl_wg, s1 = (uint32_t)(excl_wg + c_wg < budget ? excl_wg + c_wg : budget);
+    const bool first = blockIdx.x == 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        typedef unsigned long long ull;
+        abnn_stats* st = d.wg_stats + blockIdx.x % kWalkBlocks;
+        atomicAdd((ull*)&st->pre_gated, (ull)L.stat[0]);
+        atomicAdd((ull*)&st->post_gated, (ull)L.stat[1]);
+        if (L.stat[2]) atomicAdd((ull*)&st->updated, (ull)L.stat[2]);
+        if (L.stat[3]) atomicAdd((ull*)&st->fired, (ull)L.stat[3]);
+        if (L.stat[4]) atomicAdd((ull*)&st->pruned, (ull)L.stat[4]);
+        if (first) {
+            atomicAdd((ull*)&st->passes, 1ull);
+            atomicAdd((ull*)&st->events, (ull)d.events);
+        }
+    }
+    if (s1 <= s0 && !first) return;  // workgroup-uniform: nothing to stamp
+    // every workgroup's word published = every refractory stage of the pass
+    // done: no lastFired read is left, the stamps may land
+    if (wid == 0) {
+        const uint32_t tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
+        if (first) {
+            // the next pass's prediction (refrac_chunk's spec): the workgroups
+            // below the one where the budget ran out, less one
+            uint32_t run = 0, cut = gridDim.x;
+#pragma unroll
+            for (uint32_t i = 0; i < kLbMaxWords; ++i) {
+                const uint32_t inc = wave_incl_scan(vals[i]) + run;  // prefix through word 64 i + lane
+                const uint64_t hit = __ballot(inc >= budget && inc - vals[i] < budget);
+                if (hit && cut == gridDim.x) cut = i * 64 + (uint32_t)__builtin_ctzll(hit);
+                run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            }
+            if (lane == 0) {
+                L.total = tot;
+                d.work->spec_wgs = cut >= gridDim.x ? gridDim.x : (cut > 0 ? cut - 1 : 0u);
+            }
+        }
+    }
+    lds_barrier();
+    const uint32_t* ring = d.fired_ring + (pass & (kFiredRing - 1)) * (uint64_t)budget;
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
+        const uint32_t nrn = ring[i];
+        if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
+    }
+    if (first && threadIdx.x == 0) {  // the pass's end: every workgroup has read the pass-start scalars
+        d.n_fired_ring[pass & (kFiredRing - 1)] = L.total;
+        const uint32_t t0 = __hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t0 != 0u && budget > 0) *d.rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
+        *d.clock = now + kp.clock_inc;                                        // brain.metal:129
+        *d.pass_index = pass + 1;
+        __hip_atomic_store((gu32*)&d.work->t0_g2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        d.work->epoch = epoch + 1u;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -522,7 +965,13 @@ __device__ __forceinline__ void set_priority(uint32_t p)
     }
 }
 
-template <int BLOCK, int K, int FW, bool kTrack, bool kRandom>
+// kFused (sweep mode, blocked range map): the whole single-GPU pass in this
+// launch -- after its refractory stage every wave joins its workgroup's
+// look-back (wg_lookback above), walks its own survivors up to the budget (the
+// weight update of k_apply: apply_event), and the last workgroup ends the pass
+// (fused_finalize).  Its survivors are written contiguously from the range's
+// region start (no per-chunk slots: the wave walks them itself).
+template <int BLOCK, int K, int FW, bool kTrack, bool kRandom, bool kFused>
 __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
     constexpr int NW = BLOCK / 64;
@@ -533,22 +982,34 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     constexpr uint32_t SE = kChunk + 128;              // a chunk + one staging step (<= 128 events)
     static_assert(K % 4 == 0, "the packed src stream is read in 256-event groups");
     static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
+    static_assert(!(kFused && kRandom), "the fused pass is sweep-mode only");
     __shared__ uint32_t s_f1[FW], s_f2[FW];
     __shared__ uint32_t s_off[NW][SE], s_src[NW][SE];
+    __shared__ FusedLds<NW> s_fz;            // fused: the pass end's workgroup state
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wid = wave_uniform(tid >> 6);
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();  // diagnostics: the prologue
     // range of this wave: blocked (a workgroup's waves sweep neighbouring
     // ranges) or interleaved (neighbouring ranges on different CUs / XCDs, so
     // a dense stretch of the graph does not land on one CU)
-    const uint32_t r = d.range_map ? wid * gridDim.x + blockIdx.x : blockIdx.x * NW + wid;
+    const uint32_t r = (!kFused && d.range_map) ? wid * gridDim.x + blockIdx.x : blockIdx.x * NW + wid;
     const uint64_t it_begin = d.range_bounds[r], it_end = d.range_bounds[r + 1];  // adaptive partition
     const uint64_t region = it_begin * IE;
     const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
+    // fused: the pass-start reward and rBar (brain.metal:105-106; C1) for the
+    // updated weights of the refractory stage
+    const float Rw = kFused ? *d.reward : 0.0f, rbw = kFused ? *d.rbar : 0.0f;
+    // fused: the pass index and epoch (workgroup 0 advances both at the end,
+    // once every workgroup has read them), and whether this workgroup is
+    // predicted below the budget cut (the previous pass's cut, less one); never
+    // with pruning (a pruned record's src and dst change, which a restore would
+    // have to undo too)
+    const uint64_t pass_f = kFused ? *d.pass_index : 0;
+    const uint32_t epoch = kFused ? d.work->epoch : 0u;
+    const bool spec = kFused && !(kp.w_prune > 0.0f) && blockIdx.x < d.work->spec_wgs;
     uint32_t* st_off = s_off[wid];
     uint32_t* st_src = s_src[wid];
-
-    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();  // diagnostics: the prologue
     // Records in flight.  Sweep: the packed src stream (engine.h, SynArrays):
     // per 256-event group g a lane holds two lo words (events 128 kh + 2 lane
     // + {0, 1}, kh = 0, 1) and one hi word (the same four events' bits
@@ -597,18 +1058,26 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             l1[i] = f[i];
             l2[i] = f[FW / 4 + i];
         }
-        // the next pass's bitmap and images are zeroed here (k_apply or
-        // k_bitmap builds them), a slice per workgroup; this pass's stimulus
-        // is stamped by workgroup 0 (the refractory stage reads it as now)
+        // the bitmap and images of the pass after next are zeroed here (the
+        // next pass builds them: k_apply, the fused pass, or k_bitmap), a
+        // slice per workgroup; this pass's stimulus is stamped by workgroup 0
+        // (the refractory stage reads it as now)
         const uint32_t nz = d.n_bitmap_words + 2 * FW, per = (nz + gridDim.x - 1) / gridDim.x;
         for (uint32_t i = blockIdx.x * per + tid; i < min(nz, (blockIdx.x + 1) * per); i += BLOCK) {
-            if (i < d.n_bitmap_words) d.bitmap_next[i] = 0u;
-            else d.filter_next[i - d.n_bitmap_words] = 0u;
+            if (i < d.n_bitmap_words) d.bitmap_clear[i] = 0u;
+            else d.filter_clear[i - d.n_bitmap_words] = 0u;
         }
         if (blockIdx.x == 0)
             for (uint64_t i = tid; i < d.stim_count; i += BLOCK) d.last_fired[d.stim_first + i] = now;
+        if constexpr (kFused) {
+            if (tid < 5) s_fz.stat[tid] = 0u;
+            if (tid == 0) s_fz.done = 0u;
+            if (tid < kSetCache) s_fz.setc[tid] = ~0ull;
+        }
     }
-    __syncthreads();
+    // the filter images in LDS for every wave; the prologue's global stores
+    // (zeroing, stimulus) and the first records stay in flight
+    lds_barrier();
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const uint64_t len = it_end - it_begin;
 
@@ -618,10 +1087,13 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     auto stage_at = [&](uint32_t q) { return make_uint2(st_off[q], st_src[q]); };
     // wave-uniform: a full chunk through the refractory stage now; the (< 128)
     // entries past it move to the front of the stage
+    // survivors go to chunk c's slots (the walk of k_apply takes chunks as
+    // work items), or, fused, right after the range's earlier survivors
     auto chunk_out = [&]() {
-        const uint4 c = refrac_chunk<kChunk / 64, kRandom>(d, kp, region, region + (uint64_t)nch * kChunk, kChunk,
-                                                           now, pass, stage_at);
-        if (lane == 0) d.chunk_cnt[chunk_slot(region, nch)] = c;
+        const uint64_t at = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
+        const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused>(d, kp, region, at, kChunk, now, pass, Rw, rbw,
+                                                                   spec, stage_at);
+        if (!kFused && lane == 0) d.chunk_cnt[chunk_slot(region, nch)] = c;
         tot.x += c.x;
         tot.y += c.y;
         tot.z += c.z;
@@ -740,8 +1212,16 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // whatever rank the rotation left the wave in (4: keep)
     if (d.tail_prio < 4) set_priority(d.tail_prio);
     // the range's last chunk: refractory stage by this wave
-    const uint64_t tb = region + (uint64_t)nch * kChunk;
-    const uint4 c = refrac_chunk<kChunk / 64, kRandom>(d, kp, region, tb, pend, now, pass, stage_at);
+    const uint64_t tb = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
+    const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
+                                                               stage_at);
+    const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
+    const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
+    if constexpr (kFused) {
+        fused_end<BLOCK, NW>(d, kp, r, region, tot.x + c.x, tot.y + c.y, tot.z + c.z, (uint32_t)gt, len == 0, spec,
+                             now, Rw, rbw, pass_f, epoch, s_fz, t_entry, t_start, t_stream);
+        return;
+    }
     if (lane == 0) {
         // this wave's gate time (start to stream done, full chunks included;
         // the last chunk's refractory stage after the stream costs every wave
@@ -751,15 +1231,13 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // dense stretch's time varies from pass to pass by more than the
         // stream's (the partition follows one pass late), so its ranges are
         // made shorter than the average, leaving room for that variation.
-        const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
-        const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
         d.range_info[r] = make_uint4(cost, tot.y + c.y, tot.z + c.z, nch);
         d.range_g1[r] = tot.x + c.x;
         // diagnostics (tools/wave_clock.py): 100 MHz wall clock
-        d.wave_clock[4 * r] = t_start;
-        d.wave_clock[4 * r + 1] = t_stream;
-        d.wave_clock[4 * r + 2] = __builtin_amdgcn_s_memrealtime();
-        d.wave_clock[4 * r + 3] = t_entry;
+        d.wave_clock[kWaveClock * r] = t_start;
+        d.wave_clock[kWaveClock * r + 1] = t_stream;
+        d.wave_clock[kWaveClock * r + 2] = __builtin_amdgcn_s_memrealtime();
+        d.wave_clock[kWaveClock * r + 3] = t_entry;
     }
 }
 
@@ -821,23 +1299,7 @@ __device__ void partition_bounds(const DeviceState& d, const PartLds& P, uint32_
     const uint32_t slice = (NR + 1 + gridDim.x - 1) / gridDim.x;
     const uint32_t k0 = min(blockIdx.x * slice, NR + 1), k1 = min(k0 + slice, NR + 1);
     for (uint32_t k = k0 + threadIdx.x; k < k1; k += kApplyThreads) {
-        uint32_t nb = P.rb[k];
-        if (d.adapt_ranges && k > 0 && k < NR && total_cost > 0) {
-            const uint32_t T = (uint32_t)((uint64_t)k * total_cost / NR);
-            uint32_t lo = 0, hi = NR;  // last range with cc <= T (its cost is > 0)
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (P.cc[mid] <= T) lo = mid;
-                else hi = mid;
-            }
-            // target in 1/256 iterations; both terms of the move are monotonic
-            // in k, so ranges never overlap
-            const uint32_t cr = P.cc[lo + 1] - P.cc[lo];
-            const uint64_t tfp = (uint64_t)P.rb[lo] * 256u +
-                                 (cr ? (uint64_t)(T - P.cc[lo]) * (P.rb[lo + 1] - P.rb[lo]) * 256u / cr : 0u);
-            const uint32_t g = d.adapt_gain;
-            nb = (uint32_t)(((uint64_t)P.rb[k] * 256u * (4u - g) + tfp * g + 512u) >> 10);
-        }
+        const uint32_t nb = adapted_bound(d, P.cc, P.rb, NR, k, total_cost, P.rb[k]);
         d.range_bounds_next[k] = nb;
     }
 }
@@ -1033,10 +1495,6 @@ __device__ uint64_t rank_offset(const KernelParams& kp, const int32_t* gathered,
     return off < kp.max_spikes ? off : kp.max_spikes;
 }
 
-// ---------------------------------------------------------------------------
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) uint64_t gu64;
-
 // Sharded passes: stamp rank r's first min(count_r, budget - offset_r) spikes
 // (the gathered exchange records, rank order); workgroups take slices.
 // The merged list is also this pass's spike list (fired_ring, global budget
@@ -1191,7 +1649,6 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     const uint64_t now = s_now, pass = s_pass;
     const bool random = d.mode == ABNN_MODE_RANDOM, stamp = gathered == nullptr;
     const bool prune = kp.w_prune > 0.0f, genesis = d.grown != nullptr && kp.p_new > 0.0f;
-    uint32_t upd = 0, nf = 0, npr = 0;
     __shared__ uint64_t s_g1, s_g2;  // the pass's gate totals (workgroup 0)
     __shared__ uint64_t s_cand;      // spike candidates up to and including this shard
     const bool first = blockIdx.x == 0;  // workgroup 0 also counts the pass's gate totals
@@ -1204,44 +1661,10 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     const uint32_t tr = kApplyThreads - 1 - threadIdx.x;
     const uint64_t x0 = (uint64_t)tr * gridDim.x + blockIdx.x, xs = (uint64_t)gridDim.x * kApplyThreads;
     const NextItem it0 = x0 < nitems ? next_item_load(d, kp, pass, x0) : NextItem{0u, 0u, 0u};
+    ApplyCtx ac{R, rb, now, pass, random, stamp, stamp, false, prune, genesis, false, 0u, 0u, 0u};
     budget_walk(d, rank_offset(kp, gathered, rank), kp.max_spikes, s_lds, s_red,
                 [&](uint64_t region, const uint4& e, bool f, uint64_t pre, uint64_t slot) {
-        const float w = updated_weight(kp, __uint_as_float(e.z), f, R, rb, __uint_as_float(e.y & 0x7FFFFFFFu));
-        const uint64_t t = region + e.x, ri = rec_index(d, t, pass);
-        // random mode: of the events that updated one synapse this pass, the
-        // highest (k_claim) stores its weight; every one of them still counts
-        const bool store = !random || d.claim[ri] == (uint32_t)(t + 1);
-        if (random && store) d.claim[ri] = 0u;  // re-armed for the next pass
-        // brain.metal:122.  Non-temporal: a plain 4-B store leaves ~160k
-        // scattered dirty partial lines per pass whose write-back lands in the
-        // middle of the next pass's record stream (+30 us of gate time,
-        // tools/exp_variants.py).
-        if (store && prune && w < kp.w_prune) {  // README §5: the synapse is removed
-            set_src(d.syn, ri, kSrcNone);
-            __builtin_nontemporal_store(0xFFFFFFFFu, d.syn.dst + ri);
-            __builtin_nontemporal_store(w, d.syn.w + ri);
-            if (d.dead) atomicAdd(d.dead + ri / kCompactChunk, 1u);  // tally for the structural update
-            ++npr;
-        } else if (store) {
-            __builtin_nontemporal_store(w, d.syn.w + ri);
-        }
-        ++upd;
-        if (f) {
-            if (stamp) {
-                d.last_fired[e.w] = now;  // brain.metal:125-126
-                d.fired_ring[(pass & (kFiredRing - 1)) * kp.max_spikes + pre] = e.w;
-            }
-            ++nf;
-            if (genesis) {  // README §5 synaptogenesis: slot `pre` of this pass
-                const uint64_t x = splitmix64_at(d.seed ^ ABNN_GENESIS_KEY, (pass << 32) | pre);
-                if (unit24(x) < kp.p_new) {
-                    const uint64_t span = d.n_nrn - d.n_input;
-                    d.grown[(pass % kp.compact_every) * kp.max_spikes + pre] =
-                        make_uint4(d.g2src[slot], d.n_input + (uint32_t)(((x & 0xFFFFFFFFull) * span) >> 32),
-                                   __float_as_uint(kp.w_init), 1u);
-                }
-            }
-        }
+        apply_event(d, kp, ac, region, e, f, pre, slot);
     }, [&](bool fired, const uint4& e) {  // this pass's spikes into the next pass's bitmap
         if (d.build_next && stamp) wave_set_next(d, fired, e.w);
     }, first ? &s_g1 : nullptr, first ? &s_g2 : nullptr, tc + 2, true, &s_cand);
@@ -1264,7 +1687,7 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
     if (threadIdx.x == 0) tc[3] = __builtin_amdgcn_s_memrealtime();
     // statistics: every workgroup adds into its own slot (no cross-workgroup
     // sum; abnn_get_stats adds the slots)
-    const uint32_t wu = wave_sum(upd), wf = wave_sum(nf), wp = wave_sum(npr);
+    const uint32_t wu = wave_sum(ac.upd), wf = wave_sum(ac.nf), wp = wave_sum(ac.npr);
     if ((threadIdx.x & 63) == 0) {
         s_u[threadIdx.x >> 6] = wu;
         s_f[threadIdx.x >> 6] = wf;
@@ -1441,12 +1864,21 @@ hipError_t launch_gate_shape(const DeviceState& d, const KernelParams& kp, hipSt
     const dim3 g(d.gate_blocks), b(BLOCK);
     const bool random = d.mode == ABNN_MODE_RANDOM;
     if (kp.track_visits) {
-        if (random) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true, true>), g, b, 0, s, d, kp);
-        else hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true, false>), g, b, 0, s, d, kp);
+        if (random) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true, true, false>), g, b, 0, s, d, kp);
+        else hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true, false, false>), g, b, 0, s, d, kp);
     } else {
-        if (random) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, true>), g, b, 0, s, d, kp);
-        else hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false>), g, b, 0, s, d, kp);
+        if (random) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, true, false>), g, b, 0, s, d, kp);
+        else hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false, false>), g, b, 0, s, d, kp);
     }
+    return hipGetLastError();
+}
+
+template <int BLOCK, int K, int FW>
+hipError_t launch_fused_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
+{
+    const dim3 g(d.gate_blocks), b(BLOCK);
+    if (kp.track_visits) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true, false, true>), g, b, 0, s, d, kp);
+    else hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false, true>), g, b, 0, s, d, kp);
     return hipGetLastError();
 }
 
@@ -1456,11 +1888,11 @@ int occupancy_shape(bool track, bool random)
     int n = 0;
     hipError_t e;
     if (track)
-        e = random ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, true>, BLOCK, 0)
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, false>, BLOCK, 0);
+        e = random ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, true, false>, BLOCK, 0)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, false, false>, BLOCK, 0);
     else
-        e = random ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, true>, BLOCK, 0)
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, false>, BLOCK, 0);
+        e = random ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, true, false>, BLOCK, 0)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, false, false>, BLOCK, 0);
     return e == hipSuccess ? n : 0;
 }
 
@@ -1512,6 +1944,36 @@ hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t
     switch (shape_key(d.gate_block, d.gate_k, d.filter_words)) {
 #define X(B, K, F) case shape_key(B, K, F): return launch_gate_shape<B, K, F>(d, kp, s);
         ABNN_GATE_SHAPES(X)
+#undef X
+    }
+    return hipErrorInvalidValue;
+}
+
+// Fused pass shapes: 1024-thread workgroups, at most 512 of them (one
+// look-back poll) and 4096 ranges (the partition's LDS prefix), all resident
+// (one per CU: the look-back waits only on other workgroups of the launch,
+// which are resident or done; the wait is bounded anyway).
+#define ABNN_FUSED_SHAPES(X) \
+    X(1024, 8, 8192)         \
+    X(1024, 16, 8192)
+
+bool fused_pass_supported(const DeviceState& d)
+{
+    bool shape = false;
+    switch (shape_key(d.gate_block, d.gate_k, d.filter_words)) {
+#define X(B, K, F) case shape_key(B, K, F): shape = true; break;
+        ABNN_FUSED_SHAPES(X)
+#undef X
+    }
+    return shape && d.mode == ABNN_MODE_SWEEP && d.range_map == 0 && d.gate_blocks > 0 &&
+           d.gate_blocks <= kLbMaxWords * 64 && d.n_ranges <= kFusedMaxRanges;
+}
+
+hipError_t launch_fused_pass(const DeviceState& d, const KernelParams& kp, hipStream_t s)
+{
+    switch (shape_key(d.gate_block, d.gate_k, d.filter_words)) {
+#define X(B, K, F) case shape_key(B, K, F): return launch_fused_shape<B, K, F>(d, kp, s);
+        ABNN_FUSED_SHAPES(X)
 #undef X
     }
     return hipErrorInvalidValue;

@@ -22,18 +22,21 @@ b.build_random_graph(1)
 b.set_auto_stimulus(0, wl.n_input)
 passes = int(sys.argv[1]) if len(sys.argv) > 1 else 12
 first = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # print passes >= first
-for p in range(passes):
+b2b = os.environ.get("B2B", "0") == "1"  # passes back to back (as the bench runs them): only the last is printed
+if b2b:
+    b.encode_traversal(passes - 1)
+for p in range(passes - 1 if b2b else 0, passes):
     b.encode_traversal(1)
     b.synchronize()
     if p < first:
         continue
-    nr = 16384
-    buf = np.zeros(4 * nr + 16, dtype=np.uint64)
+    nr, KW = 16384, 12  # kWaveClock u64 per range (engine.h)
+    buf = np.zeros(KW * nr + 32, dtype=np.uint64)
     f = b._lib.abnn_debug_wave_clock
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     f.restype = ctypes.c_int
     assert f(b._h, buf.ctypes.data, buf.size) == 0
-    w = buf[:4 * nr].reshape(-1, 4)
+    w = buf[:KW * nr].reshape(-1, KW).astype(np.int64)
     w = w[w[:, 0] > 0]
     t0 = w[:, 0].min()
     print(f"  entry (before the filter load) to start: " + " ".join(
@@ -47,7 +50,13 @@ for p in range(passes):
     print(f"  end         {q(en)}")
     print(f"  stream dur  {q(se - st)}")
     print(f"  tail dur    {q(en - se)}")
-    np.save(os.path.join(os.environ.get("OUT", "gpurun_out"), f"wave_clock_p{p}.npy"), buf.reshape(-1, 4)[:len(w)])
+    if (w[:, 5] > 0).all():  # fused pass: look-back done, walk done
+        lb, wk = (w[:, 4] - t0) * 10e-3, (w[:, 5] - t0) * 10e-3
+        print(f"  lookback at {q(lb)}")
+        print(f"  walk done   {q(wk)}")
+        print(f"  lb wait     {q(lb - en)}")
+        print(f"  walk dur    {q(wk - lb)}")
+    np.save(os.path.join(os.environ.get("OUT", "gpurun_out"), f"wave_clock_p{p}.npy"), w)
     rb = np.zeros(len(w) + 1, dtype=np.uint32)
     g = b._lib.abnn_debug_range_bounds
     g.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
