@@ -720,6 +720,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
         if ((s = dalloc(&b->cost_buf[i], max_ranges)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.lb_status, kMaxGateBlocks)) != ABNN_OK) return fail(s);
     if (const char* env = std::getenv("ABNN_FUSED")) b->use_fused = std::atoi(env) != 0;
+    d.spec_mode = 1;
+    if (const char* env = std::getenv("ABNN_SPEC")) d.spec_mode = (uint32_t)std::min(2, std::max(0, std::atoi(env)));
     d.bitmap = b->bitmap_buf[0];
     d.filter = b->filter_buf[0];
     if ((s = dalloc(&d.range_info, max_ranges)) != ABNN_OK) return fail(s);

@@ -127,6 +127,8 @@ struct DeviceState {
     uint64_t* lb_status;
     const uint32_t* cost_in;
     uint32_t* cost_out;
+    uint32_t spec_mode;       // fused: speculative weight stores 0 off, 1 below the predicted cut (default),
+                              // 2 everywhere (ABNN_SPEC; 2 exercises the restore path)
     uint32_t prologue_adapt;  // the previous pass was fused over the same ranges: its costs move the next
                               // pass's partition (computed in this one's prologue)
     uint64_t n_syn;           // local records

@@ -1007,7 +1007,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // have to undo too)
     const uint64_t pass_f = kFused ? *d.pass_index : 0;
     const uint32_t epoch = kFused ? d.work->epoch : 0u;
-    const bool spec = kFused && !(kp.w_prune > 0.0f) && blockIdx.x < d.work->spec_wgs;
+    const bool spec = kFused && !(kp.w_prune > 0.0f) &&
+                      (d.spec_mode == 2 || (d.spec_mode == 1 && blockIdx.x < d.work->spec_wgs));
     uint32_t* st_off = s_off[wid];
     uint32_t* st_src = s_src[wid];
     // Records in flight.  Sweep: the packed src stream (engine.h, SynArrays):

@@ -106,6 +106,49 @@ def test_edge_cases(gpu, over):
     assert g.stats() == o.stats()
 
 
+@pytest.mark.parametrize("env", [{"ABNN_FUSED": "0"}, {"ABNN_SPEC": "2"}, {"ABNN_SPEC": "0"}],
+                         ids=["two-kernel", "spec-everywhere", "spec-off"])
+@pytest.mark.parametrize("over", [{}, dict(max_spikes=1), dict(max_spikes=200_000), dict(events=777_777)],
+                         ids=["default", "budget1", "budget-huge", "partial"])
+def test_pass_variants(gpu, monkeypatch, env, over):
+    """The single-GPU pass's variants against the oracle every pass: the
+    two-kernel pass (k_gate + k_apply, also the sharded and random-mode path),
+    and the fused pass with its speculative weight stores everywhere (every
+    workgroup past the budget's end restores its weights) or nowhere."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    over = dict(over)
+    events = over.pop("events", 1_000_000)
+    g, o = _pair(99_488, 1_000_000, events, seed=3, **over)
+    for k in range(12):
+        if k == 8:
+            g.set_reward(0.5)
+            o.set_reward(0.5)
+        g.encode_traversal(1)
+        o.pass_threaded(nthreads=16)
+        _assert_same(g, o, f"{env} {over} pass {k}")
+    assert g.stats() == o.stats()
+
+
+def test_fused_and_shard_passes_interleaved(gpu):
+    """One handle driven by fused passes (abnn_traverse) and world-1 shard
+    passes (k_gate + k_apply) in turn: the bitmap buffers, the partition and
+    the spike lists hand over between the two paths."""
+    import torch
+
+    g, o = _pair(99_488, 1_000_000, 1_000_000, seed=6)
+    gs = GpuShards([g])
+    for k in range(16):
+        if k % 3 == 2 or k in (7, 8):
+            gs.pass_()
+        else:
+            g.encode_traversal(1)
+        torch.cuda.synchronize()
+        o.pass_threaded(nthreads=16)
+        _assert_same(g, o, f"pass {k}")
+    assert g.stats() == o.stats()
+
+
 def test_empty_and_tiny(gpu):
     import abnn_amd
 
