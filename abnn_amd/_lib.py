@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libabnn_hip.so")
+# ABNN_LIB: another build of the same ABI (A/B timing of kernel variants,
+# tools/ab_variants.sh); the default is the in-tree product library
+LIB_PATH = os.environ.get("ABNN_LIB") or os.path.join(_HERE, "libabnn_hip.so")
 
 SUMMARY_WORDS = 4
 

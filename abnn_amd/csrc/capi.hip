@@ -128,7 +128,7 @@ void free_all(abnn_brain* b)
                     b->syn_alt.lo,  b->syn_alt.hi,   b->syn_alt.dst,  b->syn_alt.w, b->syn_alt.src32,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->bitmap_buf[0], b->bitmap_buf[1], b->bitmap_buf[2], b->filter_buf[0], b->filter_buf[1],
-                    b->filter_buf[2], b->cost_buf[0], b->cost_buf[1], b->d.lb_status,
+                    b->filter_buf[2], b->cost_buf[0], b->cost_buf[1], b->d.lb_status, b->d.cand_list,
                     b->d.range_info,    b->d.range_g1,  b->d.g2x,
                     b->d.chunk_cnt,
                     b->d.wg_stats, b->d.claim,  b->d.g2src,      b->d.grown,
@@ -719,6 +719,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     for (int i = 0; i < 2; ++i)
         if ((s = dalloc(&b->cost_buf[i], max_ranges)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.lb_status, kMaxGateBlocks)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.cand_list, (uint64_t)kFusedMaxRanges * kCandCap)) != ABNN_OK) return fail(s);
     if (const char* env = std::getenv("ABNN_FUSED")) b->use_fused = std::atoi(env) != 0;
     d.spec_mode = 1;
     if (const char* env = std::getenv("ABNN_SPEC")) d.spec_mode = (uint32_t)std::min(2, std::max(0, std::atoi(env)));

@@ -18,6 +18,8 @@ constexpr int kScanThreads = 1024; // k_scan is one workgroup
 constexpr int kMaxGateBlocks = 1024;
 constexpr int kMaxRanges = 16384;  // kMaxGateBlocks x up to 16 waves (one range per gate wave)
 constexpr int kApplyThreads = 1024;  // budget-walk workgroups (k_spikes, k_claim, k_apply)
+constexpr uint32_t kCandCap = 256;      // fused pass: spike candidates listed per range (more: the full walk)
+constexpr uint32_t kFusedMaxRanges = 4096;  // fused pass: ranges (the partition's LDS cost prefix)
 constexpr uint32_t kWalkBlocks = 256; // their grid: 4096 waves, one work item (chunk) per wave at a time
 constexpr int kMaxApplyBlocks = kWalkBlocks;
 static_assert(kMaxApplyBlocks <= kApplyThreads, "the finalizing workgroup reads one apply partial per thread");
@@ -127,6 +129,8 @@ struct DeviceState {
     uint64_t* lb_status;
     const uint32_t* cost_in;
     uint32_t* cost_out;
+    uint2* cand_list;         // fused: per range its first kCandCap spike candidates {survivor index, dst}
+                              // ([kFusedMaxRanges * kCandCap]; the walk reads these, not every survivor)
     uint32_t spec_mode;       // fused: speculative weight stores 0 off, 1 below the predicted cut (default),
                               // 2 everywhere (ABNN_SPEC; 2 exercises the restore path)
     uint32_t prologue_adapt;  // the previous pass was fused over the same ranges: its costs move the next

@@ -483,7 +483,7 @@ __device__ __forceinline__ uint4 range_totals(const DeviceState& d, uint32_t r) 
 template <int R, bool kRandom, bool kFused, class At>
 __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const KernelParams& kp, uint64_t region,
                                               uint64_t base, uint32_t n, uint64_t now, uint64_t pass, float Rw,
-                                              float rbw, bool spec, At&& at)
+                                              float rbw, bool spec, uint32_t crange, uint32_t c0, At&& at)
 {
     const uint32_t lane = threadIdx.x & 63, nn = (uint32_t)d.n_nrn;
     uint32_t n_g1 = 0, n_g2 = 0, n_cand = 0;
@@ -523,7 +523,7 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
             const bool g2 = dst[j] < nn && (now - ld[j]) > (uint64_t)kp.refractory;  // brain.metal:79-83
             const uint64_t tg = d.syn_offset + region + rel[j];
             const bool cand = g2 && spike_candidate(kp, w[j], tg, now);
-            const uint64_t bg = __ballot(g2);
+            const uint64_t bg = __ballot(g2), bcd = __ballot(cand);
             if (g2) {
                 const uint64_t o = base + n_g2 + mbcnt64(bg);
                 if constexpr (kFused) {
@@ -531,6 +531,9 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
                     d.g2x[o] = make_uint4(rel[j] | (cand ? 0x80000000u : 0u), __float_as_uint(w[j]),
                                           __float_as_uint(wn), dst[j]);
                     if (spec) __builtin_nontemporal_store(wn, d.syn.w + region + rel[j]);  // brain.metal:122
+                    const uint32_t ci = c0 + n_cand + mbcnt64(bcd);  // the range's candidate index
+                    if (cand && ci < kCandCap)
+                        d.cand_list[crange * kCandCap + ci] = make_uint2((uint32_t)(base - region) + n_g2 + mbcnt64(bg), dst[j]);
                 } else {
                     const uint32_t isi = __float_as_uint((float)(now - ld[j])) | (cand ? 0x80000000u : 0u);
                     d.g2x[o] = make_uint4(rel[j], isi, __float_as_uint(w[j]), dst[j]);
@@ -540,7 +543,7 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
                     __hip_atomic_store((gu32*)&d.work->t0_g2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             n_g2 += (uint32_t)__popcll(bg);
-            n_cand += (uint32_t)__popcll(__ballot(cand));
+            n_cand += (uint32_t)__popcll(bcd);
         }
     }
     return make_uint4(n_g1, n_g2, n_cand, 0u);
@@ -658,7 +661,6 @@ __device__ __forceinline__ uint32_t adapted_bound(const DeviceState& d, const ui
 // spikes stamp them (brain.metal:125-126) and workgroup 0 ends the pass --
 // no ticket, no last workgroup.
 constexpr uint32_t kLbMaxWords = 8;  // look-back words per lane: gate_blocks <= 512
-constexpr uint32_t kFusedMaxRanges = 4096;  // the partition's LDS cost prefix (FusedLds::cc)
 
 // One wave sweeps the words of workgroups [0, n): their values (capped sum)
 // once all carry `tag`, or as soon as the published ones reach the budget
@@ -760,10 +762,9 @@ struct FusedLds {
 template <int BLOCK, int NW>
 __device__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region, uint32_t g1,
                           uint32_t S, uint32_t C, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
-                          float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L, uint64_t t_entry,
-                          uint64_t t_start, uint64_t t_stream)
+                          float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L, uint64_t t_stream)
 {
-    constexpr uint32_t RW = kChunk / 64;
+    constexpr uint32_t RW = 4;  // rounds of survivors per walk batch (two batches in flight)
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
     const uint32_t tag = epoch + 1u;
     const uint64_t t_tail = __builtin_amdgcn_s_memrealtime();
@@ -827,9 +828,32 @@ __device__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t
     // Otherwise the walk of k_apply, which ends at the budget.
     uint32_t upd_rest = 0;  // spec: survivors below the budget not visited (wave-uniform)
     uint32_t seen = 0;      // candidates visited
-    const bool walk = spec ? !(C == 0 && P < budget) : P < budget;
+    // spec, below the budget, every candidate of the range listed (cand_list):
+    // the spikes come from the list, not from a walk of every survivor (a
+    // dense range holds thousands, a walk of them is a chain of dependent
+    // batches).  Survivors up to the budget's last candidate were stored by
+    // refrac_chunk; the ones after it are restored.
+    const bool listed = spec && C <= kCandCap && P < budget;
+    if (listed) {
+        const uint32_t k = (uint32_t)(budget - P);  // budget left, >= 1
+        const uint32_t nb = C < k ? C : k;          // candidates below the budget
+        const uint2* cl = d.cand_list + (uint64_t)r * kCandCap;
+        for (uint32_t i0 = 0; i0 < nb; i0 += 64) {  // wave-uniform
+            const uint32_t i = i0 + lane;
+            const uint2 c = i < nb ? cl[i] : make_uint2(0u, 0xFFFFFFFFu);
+            if (i < nb) record_spike(d, kp, ac, make_uint4(0u, 0u, 0u, c.y), P + i, region + c.x);
+            if (d.build_next) wave_set_next_dedup(d, i < nb, c.y, L.setc);  // this pass's spikes
+        }
+        // survivors below the budget: all, or through the k-th candidate
+        upd_rest = C < k ? S : wave_uniform(cl[k - 1].x) + 1u;
+        for (uint32_t q = upd_rest + lane; q < S; q += 64) {  // mispredicted tail: w stays (brain.metal:85-88)
+            const uint2 x = *reinterpret_cast<const uint2*>(d.g2x + region + q);  // {offset | cand, w}
+            __builtin_nontemporal_store(__uint_as_float(x.y), d.syn.w + region + (x.x & 0x7FFFFFFFu));
+        }
+    }
+    const bool walk = !listed && (spec ? !(C == 0 && P < budget) : P < budget);
     if (walk) load_batch(0, e);
-    else if (spec) upd_rest = S;
+    else if (spec && !listed) upd_rest = S;
     for (uint32_t b0 = 0; walk && b0 < S; b0 += RW * 64) {  // wave-uniform
         if (!spec && P >= budget) break;
         if (spec && P < budget && seen == C) {
@@ -871,10 +895,8 @@ __device__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t
         atomicAdd(&L.stat[3], wf);
         atomicAdd(&L.stat[4], wp);
         uint64_t* wc = d.wave_clock + (uint64_t)kWaveClock * r;  // diagnostics (tools/wave_clock.py)
-        wc[0] = t_start;
-        wc[1] = t_stream;
+        wc[1] = t_stream;  // wc[0], wc[3]: stored by k_gate at the stream's start
         wc[2] = t_tail;
-        wc[3] = t_entry;
         wc[4] = t_lb;
         wc[5] = t_walk;
         wc[8] = S;
@@ -999,16 +1021,19 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
     // fused: the pass-start reward and rBar (brain.metal:105-106; C1) for the
     // updated weights of the refractory stage
-    const float Rw = kFused ? *d.reward : 0.0f, rbw = kFused ? *d.rbar : 0.0f;
+    // (pass-start scalars are moved to SGPRs: held through the stream in
+    // VGPRs they would spill)
+    const float Rw = kFused ? __uint_as_float(wave_uniform(__float_as_uint(*d.reward))) : 0.0f;
+    const float rbw = kFused ? __uint_as_float(wave_uniform(__float_as_uint(*d.rbar))) : 0.0f;
     // fused: the pass index and epoch (workgroup 0 advances both at the end,
     // once every workgroup has read them), and whether this workgroup is
     // predicted below the budget cut (the previous pass's cut, less one); never
     // with pruning (a pruned record's src and dst change, which a restore would
     // have to undo too)
     const uint64_t pass_f = kFused ? *d.pass_index : 0;
-    const uint32_t epoch = kFused ? d.work->epoch : 0u;
+    const uint32_t epoch = kFused ? wave_uniform(d.work->epoch) : 0u;
     const bool spec = kFused && !(kp.w_prune > 0.0f) &&
-                      (d.spec_mode == 2 || (d.spec_mode == 1 && blockIdx.x < d.work->spec_wgs));
+                      (d.spec_mode == 2 || (d.spec_mode == 1 && blockIdx.x < wave_uniform(d.work->spec_wgs)));
     uint32_t* st_off = s_off[wid];
     uint32_t* st_src = s_src[wid];
     // Records in flight.  Sweep: the packed src stream (engine.h, SynArrays):
@@ -1080,6 +1105,10 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // (zeroing, stimulus) and the first records stay in flight
     lds_barrier();
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {  // diagnostics (tools/wave_clock.py): stored now, not held through the stream
+        d.wave_clock[kWaveClock * r] = t_start;
+        d.wave_clock[kWaveClock * r + 3] = t_entry;
+    }
     const uint64_t len = it_end - it_begin;
 
     const uint32_t nn = (uint32_t)d.n_nrn;  // N_NRN < 2^32 (checked at create)
@@ -1093,7 +1122,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     auto chunk_out = [&]() {
         const uint64_t at = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
         const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused>(d, kp, region, at, kChunk, now, pass, Rw, rbw,
-                                                                   spec, stage_at);
+                                                                   spec, r, tot.z, stage_at);
         if (!kFused && lane == 0) d.chunk_cnt[chunk_slot(region, nch)] = c;
         tot.x += c.x;
         tot.y += c.y;
@@ -1215,12 +1244,12 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // the range's last chunk: refractory stage by this wave
     const uint64_t tb = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
     const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
-                                                               stage_at);
+                                                               r, tot.z, stage_at);
     const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
     const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
     if constexpr (kFused) {
         fused_end<BLOCK, NW>(d, kp, r, region, tot.x + c.x, tot.y + c.y, tot.z + c.z, (uint32_t)gt, len == 0, spec,
-                             now, Rw, rbw, pass_f, epoch, s_fz, t_entry, t_start, t_stream);
+                             now, Rw, rbw, pass_f, epoch, s_fz, t_stream);
         return;
     }
     if (lane == 0) {
@@ -1235,10 +1264,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         d.range_info[r] = make_uint4(cost, tot.y + c.y, tot.z + c.z, nch);
         d.range_g1[r] = tot.x + c.x;
         // diagnostics (tools/wave_clock.py): 100 MHz wall clock
-        d.wave_clock[kWaveClock * r] = t_start;
         d.wave_clock[kWaveClock * r + 1] = t_stream;
         d.wave_clock[kWaveClock * r + 2] = __builtin_amdgcn_s_memrealtime();
-        d.wave_clock[kWaveClock * r + 3] = t_entry;
     }
 }
 

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build the HIP library from the working tree into tools/exp/<name>.so (an A/B
+# variant for tools/ab_variants.sh); the in-tree product library is untouched.
+set -e
+name=${1:?usage: tools/build_variant.sh NAME}
+cd "$(dirname "$0")/.."
+mkdir -p tools/exp
+python3 - "$name" <<'PY'
+import os, subprocess, sys
+from abnn_amd import build as b
+out = os.path.join("tools", "exp", sys.argv[1] + ".so")
+subprocess.check_call([b.HIPCC, *b.HIP_FLAGS, "-o", out, *b.HIP_SOURCES])
+print(out)
+PY
