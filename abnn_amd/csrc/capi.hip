@@ -679,6 +679,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
                                     p.mode == ABNN_MODE_RANDOM);
     if (per_cu <= 0) per_cu = 1;
     if (per_cu > 4) per_cu = 4;
+    // at most kFusedMaxRanges ranges (the fused pass's partition prefix in LDS)
+    per_cu = std::min<int>(per_cu, std::max<int>(1, (int)(kFusedMaxRanges / ((uint32_t)cus * (gate_block / 64)))));
     b->cus = cus;
     b->per_cu = per_cu;
     // partition A-B knobs: wave -> range map, adaptation gain

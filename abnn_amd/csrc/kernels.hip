@@ -270,18 +270,23 @@ __device__ __forceinline__ uint64_t range_begin(uint32_t b, uint32_t iters, uint
 }
 
 // ---------------------------------------------------------------------------
-// Pre-spike filter: two LDS images of the exact recent-spike
-// bitmap, each folded onto FW 32-bit words with its own word hash; bit i % 32
-// of word h(i / 32).  A neuron passes the filter iff its bit is set in both
-// (false positives ~0.5 % at config 3 with 2 x 32 KiB, no false negatives);
-// the exact bitmap confirms the staged events in the refractory stage.
-// Word hashes of j = neuron / 32: h1 = j mod FW; h2 mixes in the bits above
-// log2(FW) (those h1 drops) with a 24-bit multiply, so neurons that collide
-// in h1 mostly do not collide in h2.
-__device__ __forceinline__ uint32_t filter_word1(uint32_t j, uint32_t FW) { return j & (FW - 1); }
-__device__ __forceinline__ uint32_t filter_word2(uint32_t j, uint32_t FW, uint32_t lg)
+// Pre-spike filter: a blocked Bloom filter of the exact
+// recent-spike bitmap, FB 64-bit blocks {low, high} (2 FB u32 words, one LDS
+// image).  Bitmap word j (neurons 32 j .. 32 j + 31) is folded into block
+// g(j) = (j ^ t) mod FB, t = 0x9E5 (j >> log2 FB) (24-bit multiply): low |=
+// the word, high |= the word rotated left by r(j) = t mod 32.  Neuron n (word
+// j, bit b) passes iff low bit b and high bit (b + r) mod 32 are set -- one
+// 8-B LDS read per event.  Words of one j >> log2 FB share t, so two of them
+// never share a block and one other neuron never sets both bits: a false
+// positive needs two set neurons in the block (~0.2 % at config 3, 64 KiB),
+// no false negatives; the exact bitmap confirms the staged events in the
+// refractory stage.
+__device__ __forceinline__ uint32_t filter_t(uint32_t j, uint32_t lg) { return __umul24(j >> lg, 0x9E5u); }
+__device__ __forceinline__ void filter_set(uint32_t* f, uint32_t j, uint32_t bits, uint32_t FB, uint32_t lg)
 {
-    return (j ^ __umul24(j >> lg, 0x9E5u)) & (FW - 1);
+    const uint32_t t = filter_t(j, lg), g = (j ^ t) & (FB - 1), r = t & 31u;
+    atomicOr(f + 2 * g, bits);
+    atomicOr(f + 2 * g + 1, (bits << r) | (bits >> ((32u - r) & 31u)));
 }
 
 // ---------------------------------------------------------------------------
@@ -315,15 +320,12 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
         const uint64_t m = __ballot(bit);
         if (lane == 0 && (wave * 4 + q) * 64 < d.n_nrn) {
             reinterpret_cast<uint64_t*>(d.bitmap)[wave * 4 + q] = m;
-            // fold into the two LDS filter images (zeroed by k_apply of the
-            // previous pass; few words are non-zero)
-            const uint32_t w0 = (uint32_t)(wave * 4 + q) * 2u, FW = d.filter_words, lg = d.filter_log2;
+            // fold into the filter (zeroed by the pass before; few words are
+            // non-zero)
+            const uint32_t w0 = (uint32_t)(wave * 4 + q) * 2u;
             for (uint32_t h = 0; h < 2; ++h) {
                 const uint32_t part = (uint32_t)(m >> (32 * h));
-                if (part) {
-                    atomicOr(d.filter + filter_word1(w0 + h, FW), part);
-                    atomicOr(d.filter + FW + filter_word2(w0 + h, FW, lg), part);
-                }
+                if (part) filter_set(d.filter, w0 + h, part, d.filter_words, d.filter_log2);
             }
         }
     }
@@ -340,10 +342,8 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
 // so the build only sets bits: the order of the word atomics does not matter.
 __device__ __forceinline__ void recent_set_next_word(const DeviceState& d, uint32_t j, uint32_t bits)
 {
-    const uint32_t FW = d.filter_words, lg = d.filter_log2;
     atomicOr(d.bitmap_next + j, bits);
-    atomicOr(d.filter_next + filter_word1(j, FW), bits);
-    atomicOr(d.filter_next + FW + filter_word2(j, FW, lg), bits);
+    filter_set(d.filter_next, j, bits, d.filter_words, d.filter_log2);
 }
 
 // Wave-converged form: the lanes with act set neuron n.  The spike lists
@@ -760,7 +760,7 @@ struct FusedLds {
 // pass is done, and (workgroup 0) the pass's end.  Pass-start scalars (C1) as
 // read at kernel entry.
 template <int BLOCK, int NW>
-__device__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region, uint32_t g1,
+__device__ __forceinline__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region, uint32_t g1,
                           uint32_t S, uint32_t C, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
                           float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L, uint64_t t_stream)
 {
@@ -1005,19 +1005,29 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     static_assert(K % 4 == 0, "the packed src stream is read in 256-event groups");
     static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
     static_assert(!(kFused && kRandom), "the fused pass is sweep-mode only");
-    __shared__ uint32_t s_f1[FW], s_f2[FW];
+    __shared__ uint2 s_fb[FW];  // the filter's FW 64-bit blocks
     __shared__ uint32_t s_off[NW][SE], s_src[NW][SE];
     __shared__ FusedLds<NW> s_fz;            // fused: the pass end's workgroup state
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wid = wave_uniform(tid >> 6);
     const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();  // diagnostics: the prologue
+    // The filter goes global -> LDS directly (LDS-DMA), first: loads return
+    // in order, so behind the first records' HBM burst it would hold the
+    // prologue.  One wave-instruction copies 1 KiB (LDS: wave-uniform base +
+    // 16 B per lane); the first use of an ordinary load's result waits for it.
+    static_assert((FW / 2) % BLOCK == 0, "the filter copy is FW / 2 / BLOCK uint4 per thread");
+#pragma unroll
+    for (int c = 0; c < FW / 2 / BLOCK; ++c)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(d.filter) + c * BLOCK + tid,
+                                         reinterpret_cast<uint4*>(s_fb) + c * BLOCK + (tid & ~63u), 16, 0, 0);
     // range of this wave: blocked (a workgroup's waves sweep neighbouring
     // ranges) or interleaved (neighbouring ranges on different CUs / XCDs, so
     // a dense stretch of the graph does not land on one CU)
     const uint32_t r = (!kFused && d.range_map) ? wid * gridDim.x + blockIdx.x : blockIdx.x * NW + wid;
-    const uint64_t it_begin = d.range_bounds[r], it_end = d.range_bounds[r + 1];  // adaptive partition
-    const uint64_t region = it_begin * IE;
+    // (iteration counts < 2^31, checked at create; wave-uniform, held in SGPRs)
+    const uint32_t it_begin = wave_uniform(d.range_bounds[r]), it_end = wave_uniform(d.range_bounds[r + 1]);
+    const uint64_t region = (uint64_t)it_begin * IE;
     const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
     // fused: the pass-start reward and rBar (brain.metal:105-106; C1) for the
     // updated weights of the refractory stage
@@ -1041,18 +1051,24 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // + {0, 1}, kh = 0, 1) and one hi word (the same four events' bits
     // 16..23), 3 B per event.  Random mode: per event k (t = 64 k + lane) the
     // u32 src of its picked record (the src32 mirror).
-    uint32_t nxs[kRandom ? K : 2 * NG], nxh[NG], nxd[KD];
+    // kDepth iterations of records in flight per wave (sweep: two, ping-pong
+    // buffers A/B; a wave's memory-level parallelism bounds its stream rate)
+    constexpr int kDepth = (kRandom || kTrack) ? 1 : 2;
+    struct Recs {
+        uint32_t s[kRandom ? K : 2 * NG], h[NG], dd[KD];
+    };
+    Recs A, B;
     const uint64_t pass = kRandom ? *d.pass_index : 0;
-    auto issue = [&](uint64_t it, bool live) {
+    auto issue = [&](Recs& x, uint64_t it, bool live) __attribute__((always_inline)) {
         if constexpr (kRandom) {  // random-edge mode: a per-lane random record per event
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const uint64_t t = it * IE + k * 64 + lane;
                 const bool real = live && t < d.events;
                 const uint64_t e = real ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : 0;
-                nxs[k] = __builtin_nontemporal_load(d.syn.src32 + e);  // one access per pick
+                x.s[k] = __builtin_nontemporal_load(d.syn.src32 + e);  // one access per pick
                 if constexpr (kTrack)
-                    nxd[k] = __builtin_nontemporal_load(real ? d.syn.dst + e : d.dummy + (k * 64 + lane));
+                    x.dd[k] = __builtin_nontemporal_load(real ? d.syn.dst + e : d.dummy + (k * 64 + lane));
             }
         } else {
             // wave-uniform bases; past the range the zero dummy block
@@ -1060,30 +1076,24 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             const uint32_t* bh = live ? reinterpret_cast<const uint32_t*>(d.syn.hi) + it * (IE / 4) : d.dummy;
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
-                nxs[2 * g] = __builtin_nontemporal_load(bl + g * 128 + lane);
-                nxs[2 * g + 1] = __builtin_nontemporal_load(bl + g * 128 + 64 + lane);
-                nxh[g] = __builtin_nontemporal_load(bh + g * 64 + lane);
+                x.s[2 * g] = __builtin_nontemporal_load(bl + g * 128 + lane);
+                x.s[2 * g + 1] = __builtin_nontemporal_load(bl + g * 128 + 64 + lane);
+                x.h[g] = __builtin_nontemporal_load(bh + g * 64 + lane);
             }
             if constexpr (kTrack) {  // dst of the same events: one 8-B word per (g, kh)
                 const uint32_t* bd = live ? d.syn.dst + it * IE : d.dummy;
 #pragma unroll
                 for (int j = 0; j < 2 * NG; ++j) {
                     const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(bd + j * 128) + lane);
-                    nxd[2 * j] = (uint32_t)v;
-                    nxd[2 * j + 1] = (uint32_t)(v >> 32);
+                    x.dd[2 * j] = (uint32_t)v;
+                    x.dd[2 * j + 1] = (uint32_t)(v >> 32);
                 }
             }
         }
     };
-    issue(it_begin, it_begin < it_end);
+    issue(A, it_begin, it_begin < it_end);
+    if constexpr (kDepth == 2) issue(B, it_begin + 1, it_begin + 1 < it_end);
     {
-        const uint4* f = reinterpret_cast<const uint4*>(d.filter);
-        uint4* l1 = reinterpret_cast<uint4*>(s_f1);
-        uint4* l2 = reinterpret_cast<uint4*>(s_f2);
-        for (int i = tid; i < FW / 4; i += BLOCK) {
-            l1[i] = f[i];
-            l2[i] = f[FW / 4 + i];
-        }
         // the bitmap and images of the pass after next are zeroed here (the
         // next pass builds them: k_apply, the fused pass, or k_bitmap), a
         // slice per workgroup; this pass's stimulus is stamped by workgroup 0
@@ -1119,7 +1129,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // entries past it move to the front of the stage
     // survivors go to chunk c's slots (the walk of k_apply takes chunks as
     // work items), or, fused, right after the range's earlier survivors
+    uint32_t chunk_t = 0;  // diagnostics: 10-ns units spent in mid-stream refractory chunks
     auto chunk_out = [&]() {
+        const uint64_t tc = __builtin_amdgcn_s_memrealtime();
         const uint64_t at = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
         const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused>(d, kp, region, at, kChunk, now, pass, Rw, rbw,
                                                                    spec, r, tot.z, stage_at);
@@ -1139,8 +1151,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         }
         ++nch;
         pend = rest;
+        chunk_t += (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc);
     };
-    for (uint64_t it = it_begin; it < it_end; ++it) {
+    auto step = [&](Recs& x, uint32_t it) __attribute__((always_inline)) {
         // src[k] of event idx(k) of this iteration: sweep k = 4 g + 2 kh + s,
         // idx = 256 g + 128 kh + 2 lane + s (v_perm: lo half s, hi byte 2 kh + s);
         // random k: idx = 64 k + lane
@@ -1152,11 +1165,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if constexpr (kRandom) {
-                src[k] = nxs[k];
+                src[k] = x.s[k];
             } else {
                 const int g = k >> 2, kh = (k >> 1) & 1, sh = k & 1;
                 const uint32_t sel = 0x0C000000u | (uint32_t)(4 + 2 * kh + sh) << 16 | (uint32_t)(2 * sh + 1) << 8 | (uint32_t)(2 * sh);
-                src[k] = __builtin_amdgcn_perm(nxh[g], nxs[2 * g + kh], sel);
+                src[k] = __builtin_amdgcn_perm(x.h[g], x.s[2 * g + kh], sel);
             }
         }
         // The SIMD arbiter issues strictly by priority, then age: with a fixed
@@ -1171,9 +1184,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             set_priority((d.prio_clock ? (uint32_t)(__builtin_amdgcn_s_memrealtime() >> 10)
                                        : (uint32_t)((it - it_begin) >> 2)) + wid / 4u);
 #pragma unroll
-        for (int k = 0; k < KD; ++k) dst[k] = kTrack ? nxd[k] : 0u;
-        issue(it + 1, it + 1 < it_end);  // next iteration's records in flight first
-        const uint64_t base = it * IE;
+        for (int k = 0; k < KD; ++k) dst[k] = kTrack ? x.dd[k] : 0u;
+        issue(x, it + kDepth, it + kDepth < it_end);  // the buffer's next iteration in flight first
+        const uint64_t base = (uint64_t)it * IE;
         uint32_t vmask = (K == 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);  // events of this lane that exist
         if (base + IE > d.events) {  // only the sweep's last iteration
             vmask = 0;
@@ -1182,19 +1195,21 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 if (base + idx_of(k) < d.events) vmask |= 1u << k;
         }
 
-        // Pre-spike filter (brain.metal:73-77 pre-selection): both LDS words of
-        // every event read back to back; the word indices are masked, so any
-        // src (tombstones included) stays in bounds.
-        uint32_t f1[K], f2[K];
+        // Pre-spike filter (brain.metal:73-77 pre-selection): every event's
+        // block read back to back; the block index is masked, so any src
+        // (tombstones included) stays in bounds.  ubfe takes the bit offset
+        // mod 32: low bit src mod 32, high bit (src + t) mod 32 = (b + r) mod 32.
+        uint2 fb[K];
+        uint32_t ft[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            f1[k] = s_f1[src[k] >> 5 & (FW - 1)];
-            f2[k] = s_f2[((src[k] >> 5) ^ __umul24(src[k] >> (5 + LG), 0x9E5u)) & (FW - 1)];
+            ft[k] = filter_t(src[k] >> 5, LG);
+            fb[k] = s_fb[((src[k] >> 5) ^ ft[k]) & (FW - 1)];
         }
         uint32_t fm = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            fm |= (__builtin_amdgcn_ubfe(f1[k], src[k], 1) & __builtin_amdgcn_ubfe(f2[k], src[k], 1)) << k;
+            fm |= (__builtin_amdgcn_ubfe(fb[k].x, src[k], 1) & __builtin_amdgcn_ubfe(fb[k].y, src[k] + ft[k], 1)) << k;
         fm &= vmask;
 
         if constexpr (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
@@ -1202,7 +1217,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             for (int k = 0; k < K; ++k)
                 if (((vmask >> k) & 1u) && dst[k] < nn) d.last_visited[dst[k]] = now;
         }
-        if (__ballot(fm != 0) == 0) continue;
+        if (__ballot(fm != 0) == 0) return;
         const uint32_t rel = (uint32_t)(base - region);
         if constexpr (kRandom) {  // event order = (k, lane)
 #pragma unroll
@@ -1236,8 +1251,17 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 if (pend >= kChunk) chunk_out();  // a step stages at most 128
             }
         }
+    };
+    for (uint32_t it = it_begin; it < it_end; it += kDepth) {  // wave-uniform
+        step(A, it);
+        if constexpr (kDepth == 2)
+            if (it + 1 < it_end) step(B, it + 1);
     }
     const uint64_t t_stream = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {  // diagnostics (tools/wave_clock.py)
+        d.wave_clock[kWaveClock * r + 6] = chunk_t;
+        d.wave_clock[kWaveClock * r + 7] = nch;
+    }
     // the tail (latency-bound) runs at the issue priority tail_prio, not at
     // whatever rank the rotation left the wave in (4: keep)
     if (d.tail_prio < 4) set_priority(d.tail_prio);

@@ -30,3 +30,9 @@ print("  lag-1 correlation:", round(float(np.corrcoef(t[:-1], t[1:])[0, 1]), 3))
 print("  first 64:", " ".join(f"{v:.0f}" for v in t[:64]))
 slow = np.argsort(t)[-10:]
 print("  slowest (index:us):", " ".join(f"{i}:{t[i]:.0f}" for i in sorted(slow)))
+import torch  # noqa: E402
+
+pr = torch.cuda.get_device_properties(0)
+st = b.stats()
+print(f"  device {pr.name} CUs {pr.multi_processor_count}; stats over the timed passes: "
+      f"pre_gated {st['pre_gated'] / passes:.0f} post_gated {st['post_gated'] / passes:.0f} per pass")

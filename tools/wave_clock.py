@@ -50,6 +50,10 @@ for p in range(passes - 1 if b2b else 0, passes):
     print(f"  end         {q(en)}")
     print(f"  stream dur  {q(se - st)}")
     print(f"  tail dur    {q(en - se)}")
+    ct = w[:, 6] * 10e-3
+    print(f"  mid-stream refractory chunks: {int(w[:, 7].sum())} in total, per wave max {int(w[:, 7].max())}; "
+          f"time per wave {q(ct)}")
+    print(f"  stream dur less chunks {q(se - st - ct)}")
     if (w[:, 5] > 0).all():  # fused pass: look-back done, walk done
         lb, wk = (w[:, 4] - t0) * 10e-3, (w[:, 5] - t0) * 10e-3
         print(f"  lookback at {q(lb)}")
