@@ -724,6 +724,11 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.cand_list, (uint64_t)kFusedMaxRanges * kCandCap)) != ABNN_OK) return fail(s);
     if (const char* env = std::getenv("ABNN_FUSED")) b->use_fused = std::atoi(env) != 0;
     d.spec_mode = 1;
+    d.cost_tail = 1;
+    if (const char* env = std::getenv("ABNN_COST_TAIL")) d.cost_tail = std::atoi(env) ? 1u : 0u;
+    d.flush_at = kChunk;
+    if (const char* env = std::getenv("ABNN_FLUSH_AT"))
+        d.flush_at = (uint32_t)std::min<int>((int)kChunk, std::max(64, std::atoi(env)));
     if (const char* env = std::getenv("ABNN_SPEC")) d.spec_mode = (uint32_t)std::min(2, std::max(0, std::atoi(env)));
     d.bitmap = b->bitmap_buf[0];
     d.filter = b->filter_buf[0];

@@ -131,6 +131,9 @@ struct DeviceState {
     uint32_t* cost_out;
     uint2* cand_list;         // fused: per range its first kCandCap spike candidates {survivor index, dst}
                               // ([kFusedMaxRanges * kCandCap]; the walk reads these, not every survivor)
+    uint32_t cost_tail;       // fused: a range's partition cost includes its tail (default; ABNN_COST_TAIL=0: off)
+    uint32_t flush_at;        // fused: staged events that send a wave's stage through the refractory stage
+                              // (<= kChunk; ABNN_FLUSH_AT)
     uint32_t spec_mode;       // fused: speculative weight stores 0 off, 1 below the predicted cut (default),
                               // 2 everywhere (ABNN_SPEC; 2 exercises the restore path)
     uint32_t prologue_adapt;  // the previous pass was fused over the same ranges: its costs move the next

@@ -1153,6 +1153,19 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         pend = rest;
         chunk_t += (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc);
     };
+    // fused: every staged event through the refractory stage once flush_at
+    // are staged (survivors go right after the range's earlier ones)
+    auto flush_all = [&]() {
+        const uint64_t tc = __builtin_amdgcn_s_memrealtime();
+        const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused>(d, kp, region, region + tot.y, pend, now, pass, Rw,
+                                                                   rbw, spec, r, tot.z, stage_at);
+        tot.x += c.x;
+        tot.y += c.y;
+        tot.z += c.z;
+        nch += pend >= kChunk;
+        pend = 0;
+        chunk_t += (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc);
+    };
     auto step = [&](Recs& x, uint32_t it) __attribute__((always_inline)) {
         // src[k] of event idx(k) of this iteration: sweep k = 4 g + 2 kh + s,
         // idx = 256 g + 128 kh + 2 lane + s (v_perm: lo half s, hi byte 2 kh + s);
@@ -1248,7 +1261,10 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                     st_src[q + h0] = src[2 * j + 1];
                 }
                 pend += (uint32_t)(__popcll(b0) + __popcll(b1));
-                if (pend >= kChunk) chunk_out();  // a step stages at most 128
+                if (kFused ? pend >= d.flush_at : pend >= kChunk) {  // a step stages at most 128
+                    if constexpr (kFused) flush_all();
+                    else chunk_out();
+                }
             }
         }
     };
@@ -1272,7 +1288,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
     const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
     if constexpr (kFused) {
-        fused_end<BLOCK, NW>(d, kp, r, region, tot.x + c.x, tot.y + c.y, tot.z + c.z, (uint32_t)gt, len == 0, spec,
+        // fused: the look-back waits for stream + tail, so with cost_tail the
+        // partition balances that (the tail's length follows the range's
+        // staged events)
+        const uint64_t gf = d.cost_tail ? ((__builtin_amdgcn_s_memrealtime() - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty : gt;
+        fused_end<BLOCK, NW>(d, kp, r, region, tot.x + c.x, tot.y + c.y, tot.z + c.z, (uint32_t)gf, len == 0, spec,
                              now, Rw, rbw, pass_f, epoch, s_fz, t_stream);
         return;
     }
