@@ -712,8 +712,9 @@ __device__ void fused_next_bounds(const DeviceState& d, uint32_t* cc)
         if (mine) d.range_bounds_next[k] = d.range_bounds[k];
         return;
     }
-    // rows of 64 costs, coalesced, 8 rows of loads in flight per lane; each
-    // row scanned across the wave (DPP) on top of the rows before it
+    // the costs are in cc already (the prologue's LDS-DMA): rows of 64, 8
+    // rows read at once, each row scanned across the wave (DPP) on top of the
+    // rows before it, in place
     const uint32_t rows = (NR + 63) / 64;  // NR <= kFusedMaxRanges
     uint32_t run = 0;
     for (uint32_t j0 = 0; j0 < rows; j0 += 8) {  // wave-uniform
@@ -721,7 +722,7 @@ __device__ void fused_next_bounds(const DeviceState& d, uint32_t* cc)
 #pragma unroll
         for (uint32_t u = 0; u < 8; ++u) {
             const uint32_t q = (j0 + u) * 64 + lane;
-            v[u] = q < NR ? d.cost_in[q] : 0u;
+            v[u] = q < NR ? cc[q] : 0u;
         }
 #pragma unroll
         for (uint32_t u = 0; u < 8; ++u) {
@@ -743,7 +744,8 @@ __device__ void fused_next_bounds(const DeviceState& d, uint32_t* cc)
 template <int NW>
 struct FusedLds {
     uint64_t setc[kSetCache];          // wave_set_next_dedup's cache
-    uint32_t cc[kFusedMaxRanges + 1];  // fused_next_bounds
+    alignas(16) uint32_t cc[kFusedMaxRanges + 4];  // fused_next_bounds: the previous pass's range costs
+                                                   // (LDS-DMA in the prologue), scanned in place
     uint32_t cand[NW];                 // spike candidates of each wave's range (capped at the budget)
     uint32_t stat[5];                  // pre-gated, survivors, updated, fired, pruned
     uint32_t excl;                     // candidates of all lower workgroups (capped)
@@ -1021,6 +1023,17 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     for (int c = 0; c < FW / 2 / BLOCK; ++c)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(d.filter) + c * BLOCK + tid,
                                          reinterpret_cast<uint4*>(s_fb) + c * BLOCK + (tid & ~63u), 16, 0, 0);
+    // fused: the previous pass's range costs (the next partition's input,
+    // fused_next_bounds) go to LDS the same way
+    if constexpr (kFused) {
+        if (d.prologue_adapt && d.adapt_ranges && d.n_ranges >= 2) {
+            const uint32_t nq = (d.n_ranges + 3) / 4;  // cost_in holds a multiple of 16 ranges
+            for (uint32_t i0 = 0; i0 < nq; i0 += BLOCK)  // workgroup-uniform
+                if (i0 + tid < nq)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(d.cost_in) + i0 + tid,
+                                                     reinterpret_cast<uint4*>(s_fz.cc) + i0 + (tid & ~63u), 16, 0, 0);
+        }
+    }
     // range of this wave: blocked (a workgroup's waves sweep neighbouring
     // ranges) or interleaved (neighbouring ranges on different CUs / XCDs, so
     // a dense stretch of the graph does not land on one CU)
