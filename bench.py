@@ -256,8 +256,9 @@ def main():
             "median_launch_ms": round(float(np.median(launch_ms)), 4) if launches else None,
             "timing_every": every,
             # a launch cannot take longer than the pass it is part of: if the
-            # sample says so, the timed window still held the transient
-            "steady": bool(launches and avg_gate_ms <= dt / args.steps * 1e3),
+            # sample's median says so (beyond the few us an event pair adds to
+            # the launch it brackets), the timed window still held the transient
+            "steady": bool(launches and float(np.median(launch_ms)) <= 1.08 * dt / args.steps * 1e3),
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "bytes_formula": ("3*E (24-bit src stream: 2-B lo + 1-B hi per event; E visited events) -- "
                               "DESIGN.md §5" if mode == 0 else
