@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Per-wave timeline of the gate kernel (diagnostics, ABNN_WAVE_CLOCK).
+"""Per-wave timeline of the gate kernel (diagnostics, always recorded).
 
 Runs config 3 for `warm` passes, then reads the last pass's per-wave clocks
 {start, stream done, end} (100 MHz s_memrealtime) and prints the spread of
 start, stream-end and end times, the tail (refractory stage) durations and the
-latest waves.  usage: ABNN_WAVE_CLOCK=1 python tools/wave_clock.py [passes [first printed]]
+latest waves.  usage: [B2B=1] python tools/wave_clock.py [passes [first printed]]
 """
 import ctypes
 import os
@@ -13,7 +13,6 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("ABNN_WAVE_CLOCK", "1")
 from abnn_amd import CONFIGS, Brain  # noqa: E402
 
 wl = CONFIGS[os.environ.get("CFG", "c3")]
