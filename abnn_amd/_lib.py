@@ -69,7 +69,7 @@ class Scalars(C.Structure):
 
 
 MODE_SWEEP, MODE_RANDOM = 0, 1  # abnn_params.mode (include/abnn/abnn.h)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class Stats(C.Structure):
@@ -92,8 +92,7 @@ class State(C.Structure):
     _fields_ = [
         ("syn_src_lo", C.c_void_p),
         ("syn_src_hi", C.c_void_p),
-        ("syn_dst", C.c_void_p),
-        ("syn_w", C.c_void_p),
+        ("syn_dst_w", C.c_void_p),
         ("last_fired", C.c_void_p),
         ("last_visited", C.c_void_p),
         ("clock", C.c_void_p),
@@ -191,7 +190,9 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)  # AttributeError = the ABI is not exported
         fn.restype = res
         fn.argtypes = args
-    if lib.abnn_abi_version() != ABI_VERSION:
+    if lib.abnn_abi_version() != ABI_VERSION and not os.environ.get("ABNN_LIB"):
+        # (an ABNN_LIB build of another ABI version is accepted for A/B timing:
+        # the pass/timing entry points have not changed between versions)
         raise ImportError("libabnn_hip.so ABI version mismatch")
     _lib = lib
     return lib

@@ -124,8 +124,8 @@ void free_all(abnn_brain* b)
 {
     if (!b) return;
     (void)hipSetDevice(b->device);
-    void* ptrs[] = {b->d.syn.lo,    b->d.syn.hi,     b->d.syn.dst,    b->d.syn.w,   b->d.syn.src32,
-                    b->syn_alt.lo,  b->syn_alt.hi,   b->syn_alt.dst,  b->syn_alt.w, b->syn_alt.src32,
+    void* ptrs[] = {b->d.syn.lo,    b->d.syn.hi,     b->d.syn.dw,     b->d.syn.src32,
+                    b->syn_alt.lo,  b->syn_alt.hi,   b->syn_alt.dw,   b->syn_alt.src32,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->bitmap_buf[0], b->bitmap_buf[1], b->bitmap_buf[2], b->filter_buf[0], b->filter_buf[1],
                     b->filter_buf[2], b->cost_buf[0], b->cost_buf[1], b->d.lb_status, b->d.cand_list,
@@ -186,9 +186,8 @@ abnn_status alloc_syn(SynArrays* a, uint64_t count, bool random_mode)
 {
     ST_TRY(dalloc(&a->lo, count));
     ST_TRY(dalloc(&a->hi, hi_bytes(count)));
-    ST_TRY(dalloc(&a->dst, count));
     if (random_mode) ST_TRY(dalloc(&a->src32, count));
-    return dalloc(&a->w, count);
+    return dalloc(&a->dw, count);
 }
 
 // src values of records [first, first + m) <-> host u32 (interchange form),
@@ -203,45 +202,45 @@ constexpr uint64_t kXferRecs = 1u << 22;
 
 abnn_status records_d2h(const SynArrays& a, uint64_t first, uint64_t n, abnn_synapse* out)
 {
-    std::vector<uint32_t> s, t;
-    std::vector<float> w;
+    std::vector<uint32_t> s;
+    std::vector<uint2> dw;
     SrcStage st;
     if (n) ST_TRY(dalloc(&st.dev, std::min<uint64_t>(kXferRecs, n)));
     for (uint64_t i = 0; i < n; i += kXferRecs) {
         const uint64_t m = std::min<uint64_t>(kXferRecs, n - i);
         s.resize(m);
-        t.resize(m);
-        w.resize(m);
+        dw.resize(m);
         HIP_TRY(launch_unpack_src(a, st.dev, first + i, m, nullptr));
         HIP_TRY(hipMemcpy(s.data(), st.dev, m * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(t.data(), a.dst + first + i, m * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(w.data(), a.w + first + i, m * 4, hipMemcpyDeviceToHost));
-        for (uint64_t k = 0; k < m; ++k) out[i + k] = {s[k], t[k], w[k], 0.0f};
+        HIP_TRY(hipMemcpy(dw.data(), a.dw + first + i, m * 8, hipMemcpyDeviceToHost));
+        for (uint64_t k = 0; k < m; ++k) {
+            float w;
+            std::memcpy(&w, &dw[k].y, 4);
+            out[i + k] = {s[k], dw[k].x, w, 0.0f};
+        }
     }
     return ABNN_OK;
 }
 
 abnn_status records_h2d(const SynArrays& a, uint64_t first, uint64_t n, const abnn_synapse* in)
 {
-    std::vector<uint32_t> s, t;
-    std::vector<float> w;
+    std::vector<uint32_t> s;
+    std::vector<uint2> dw;
     SrcStage st;
     if (n) ST_TRY(dalloc(&st.dev, std::min<uint64_t>(kXferRecs, n)));
     for (uint64_t i = 0; i < n; i += kXferRecs) {
         const uint64_t m = std::min<uint64_t>(kXferRecs, n - i);
         s.resize(m);
-        t.resize(m);
-        w.resize(m);
+        dw.resize(m);
         for (uint64_t k = 0; k < m; ++k) {
             s[k] = in[i + k].src;
-            t[k] = in[i + k].dst;
-            w[k] = in[i + k].w;
+            dw[k].x = in[i + k].dst;
+            std::memcpy(&dw[k].y, &in[i + k].w, 4);
         }
         HIP_TRY(hipMemcpy(st.dev, s.data(), m * 4, hipMemcpyHostToDevice));
         HIP_TRY(launch_pack_src(a, st.dev, first + i, m, nullptr));
         HIP_TRY(hipDeviceSynchronize());  // the staging buffer is reused
-        HIP_TRY(hipMemcpy(a.dst + first + i, t.data(), m * 4, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(a.w + first + i, w.data(), m * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(a.dw + first + i, dw.data(), m * 8, hipMemcpyHostToDevice));
     }
     return ABNN_OK;
 }
@@ -756,7 +755,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.g2x, iters * iter_events)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.chunk_cnt, iters * iter_events / kChunkSlotDiv + 8)) != ABNN_OK) return fail(s);
     uint32_t* dummy = nullptr;
-    if ((s = dalloc(&dummy, kDummyRecords)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&dummy, 2 * kDummyRecords)) != ABNN_OK) return fail(s);
     d.dummy = dummy;
     if ((s = dalloc(&d.wg_stats, kWalkBlocks)) != ABNN_OK) return fail(s);
     if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, cap)) != ABNN_OK) return fail(s);
@@ -818,8 +817,7 @@ abnn_status abnn_state_ptrs(abnn_brain* b, abnn_state* out)
     b->ext_ptrs = true;
     out->syn_src_lo = b->d.syn.lo;
     out->syn_src_hi = b->d.syn.hi;
-    out->syn_dst = b->d.syn.dst;
-    out->syn_w = b->d.syn.w;
+    out->syn_dst_w = reinterpret_cast<abnn_dst_w*>(b->d.syn.dw);
     out->last_fired = b->d.last_fired;
     out->last_visited = b->d.last_visited;
     out->clock = b->d.clock;

@@ -25,6 +25,7 @@ constexpr int kMaxApplyBlocks = kWalkBlocks;
 static_assert(kMaxApplyBlocks <= kApplyThreads, "the finalizing workgroup reads one apply partial per thread");
 static_assert(kMaxRanges % kApplyThreads == 0, "range prefix: whole ranges per thread");
 constexpr int kDummyRecords = 64 * 32;  // >= 64 lanes x max events per lane; also the record-buffer padding
+                                         // (the dummy block itself holds 2x as many words: {dst, w} loads)
 constexpr uint32_t kFiredRing = 8;     // spike lists kept (the bitmap build needs window_pre < kFiredRing)
 constexpr uint32_t kChunk = 384;        // pre-gated events per chunk (staged in LDS by a gate wave)
 constexpr uint32_t kWaveClock = 12;     // diagnostics: u64 words per gate wave (wave_clock)
@@ -65,11 +66,14 @@ constexpr uint64_t kMaxNeurons = kSrcNone; // N_NRN < 2^24 - 1
 struct SynArrays {
     uint16_t* lo;
     uint8_t* hi;
-    uint32_t* dst;
-    float* w;
+    uint2* dw;        // {dst, w bits} of each record: the refractory stage gathers both
+                      // with one access (one DRAM line per event, not two)
     uint32_t* src32;  // random mode only: the same src as one u32 per record, so a pick is
                       // one random DRAM access, not two (kept in step by set_src)
 };
+
+// w of record i inside its {dst, w} pair
+__host__ __device__ inline float* w_ptr(const SynArrays& a, uint64_t i) { return reinterpret_cast<float*>(a.dw + i) + 1; }
 
 __host__ __device__ inline uint64_t hi_pos(uint64_t i)
 {

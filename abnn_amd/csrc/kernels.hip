@@ -508,8 +508,9 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
             const bool g1 = (bw[j] >> (src[j] & 31u)) & 1u;  // brain.metal:73-77, exact
             bw[j] = g1;
             const uint64_t ri = g1 ? record_of(rel[j]) : 0;
-            dst[j] = g1 ? d.syn.dst[ri] : 0xFFFFFFFFu;  // tombstones (dst = 0xFFFFFFFF) never pass
-            w[j] = g1 ? d.syn.w[ri] : 0.0f;
+            const uint2 dw = g1 ? d.syn.dw[ri] : make_uint2(0xFFFFFFFFu, 0u);  // one access for both
+            dst[j] = dw.x;  // tombstones (dst = 0xFFFFFFFF) never pass
+            w[j] = __uint_as_float(dw.y);
         }
 #pragma unroll
         // the stimulus of this pass is stamped `now` (brain.cpp:82) by k_bitmap
@@ -530,7 +531,7 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
                     const float wn = updated_weight(kp, w[j], cand, Rw, rbw, (float)(now - ld[j]));
                     d.g2x[o] = make_uint4(rel[j] | (cand ? 0x80000000u : 0u), __float_as_uint(w[j]),
                                           __float_as_uint(wn), dst[j]);
-                    if (spec) __builtin_nontemporal_store(wn, d.syn.w + region + rel[j]);  // brain.metal:122
+                    if (spec) __builtin_nontemporal_store(wn, w_ptr(d.syn, region + rel[j]));  // brain.metal:122
                     const uint32_t ci = c0 + n_cand + mbcnt64(bcd);  // the range's candidate index
                     if (cand && ci < kCandCap)
                         d.cand_list[crange * kCandCap + ci] = make_uint2((uint32_t)(base - region) + n_g2 + mbcnt64(bg), dst[j]);
@@ -604,12 +605,12 @@ __device__ __forceinline__ void apply_event(const DeviceState& d, const KernelPa
     // tools/exp_variants.py).
     if (store && c.prune && w < kp.w_prune) {  // README §5: the synapse is removed
         set_src(d.syn, ri, kSrcNone);
-        __builtin_nontemporal_store(0xFFFFFFFFu, d.syn.dst + ri);
-        __builtin_nontemporal_store(w, d.syn.w + ri);
+        __builtin_nontemporal_store((uint64_t)__float_as_uint(w) << 32 | 0xFFFFFFFFull,
+                                    reinterpret_cast<uint64_t*>(d.syn.dw + ri));  // {dst, w} as one 8-B store
         if (d.dead) atomicAdd(d.dead + ri / kCompactChunk, 1u);  // tally for the structural update
         ++c.npr;
     } else if (store) {
-        __builtin_nontemporal_store(w, d.syn.w + ri);
+        __builtin_nontemporal_store(w, w_ptr(d.syn, ri));
     }
     ++c.upd;
     if (f) record_spike(d, kp, c, e, pre, slot);
@@ -850,7 +851,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         upd_rest = C < k ? S : wave_uniform(cl[k - 1].x) + 1u;
         for (uint32_t q = upd_rest + lane; q < S; q += 64) {  // mispredicted tail: w stays (brain.metal:85-88)
             const uint2 x = *reinterpret_cast<const uint2*>(d.g2x + region + q);  // {offset | cand, w}
-            __builtin_nontemporal_store(__uint_as_float(x.y), d.syn.w + region + (x.x & 0x7FFFFFFFu));
+            __builtin_nontemporal_store(__uint_as_float(x.y), w_ptr(d.syn, region + (x.x & 0x7FFFFFFFu)));
         }
     }
     const bool walk = !listed && (spec ? !(C == 0 && P < budget) : P < budget);
@@ -879,7 +880,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
                 ++ac.upd;
                 if (cand) record_spike(d, kp, ac, x, pre, region + q);
             } else if (v) {  // mispredicted: past the budget, w stays (brain.metal:85-88)
-                __builtin_nontemporal_store(__uint_as_float(x.y), d.syn.w + region + x.x);
+                __builtin_nontemporal_store(__uint_as_float(x.y), w_ptr(d.syn, region + x.x));
             }
             if (d.build_next) wave_set_next_dedup(d, cand && pre < budget, x.w, L.setc);  // this pass's spikes
             P += (uint64_t)__popcll(bc);
@@ -1081,7 +1082,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 const uint64_t e = real ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : 0;
                 x.s[k] = __builtin_nontemporal_load(d.syn.src32 + e);  // one access per pick
                 if constexpr (kTrack)
-                    x.dd[k] = __builtin_nontemporal_load(real ? d.syn.dst + e : d.dummy + (k * 64 + lane));
+                    x.dd[k] = __builtin_nontemporal_load(real ? reinterpret_cast<const uint32_t*>(d.syn.dw + e)
+                                                              : d.dummy + (k * 64 + lane));
             }
         } else {
             // wave-uniform bases; past the range the zero dummy block
@@ -1093,13 +1095,15 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 x.s[2 * g + 1] = __builtin_nontemporal_load(bl + g * 128 + 64 + lane);
                 x.h[g] = __builtin_nontemporal_load(bh + g * 64 + lane);
             }
-            if constexpr (kTrack) {  // dst of the same events: one 8-B word per (g, kh)
-                const uint32_t* bd = live ? d.syn.dst + it * IE : d.dummy;
+            if constexpr (kTrack) {  // dst of the same events: one 16-B {dst, w} pair per (g, kh)
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4* bd = reinterpret_cast<const u32x4*>(live ? reinterpret_cast<const uint32_t*>(d.syn.dw + (uint64_t)it * IE)
+                                                                      : d.dummy);
 #pragma unroll
                 for (int j = 0; j < 2 * NG; ++j) {
-                    const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(bd + j * 128) + lane);
-                    x.dd[2 * j] = (uint32_t)v;
-                    x.dd[2 * j + 1] = (uint32_t)(v >> 32);
+                    const u32x4 v = __builtin_nontemporal_load(bd + j * 64 + lane);
+                    x.dd[2 * j] = v.x;
+                    x.dd[2 * j + 1] = v.z;
                 }
             }
         }
@@ -1832,15 +1836,14 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint
     static_assert(kCompactThreads == kScanThreads, "block_exclusive_scan is sized for kScanThreads");
     __shared__ uint64_t s_wave[kCompactThreads / 64];
     const uint64_t base = (uint64_t)blockIdx.x * kCompactChunk;
-    uint32_t rs[4], rd[4];
-    float rw[4];
+    uint32_t rs[4];
+    uint64_t rdw[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {  // all loads in flight first
         const uint64_t i = base + (uint64_t)j * kCompactThreads + threadIdx.x;
         const bool in = i < n;
         rs[j] = in ? src_of(syn, i) : kSrcNone;
-        rd[j] = in ? __builtin_nontemporal_load(syn.dst + i) : 0u;
-        rw[j] = in ? __builtin_nontemporal_load(syn.w + i) : 0.0f;
+        rdw[j] = in ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(syn.dw + i)) : 0ull;
     }
     uint64_t o = offsets[blockIdx.x];
 #pragma unroll
@@ -1850,8 +1853,7 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint
         const uint64_t pre = block_exclusive_scan(live ? 1u : 0u, &tot, s_wave);
         if (live) {
             set_src(dst, o + pre, rs[j]);
-            __builtin_nontemporal_store(rd[j], dst.dst + o + pre);
-            __builtin_nontemporal_store(rw[j], dst.w + o + pre);
+            __builtin_nontemporal_store(rdw[j], reinterpret_cast<uint64_t*>(dst.dw + o + pre));
         }
         o += tot;
     }
@@ -1900,8 +1902,7 @@ __global__ __launch_bounds__(256) void k_generate(DeviceState d, uint32_t n_in, 
             w = 0.1f + unit24(x2) * (0.2f - 0.1f);
         }
         set_src(d.syn, k, src);
-        d.syn.dst[k] = dst;
-        d.syn.w[k] = w;
+        d.syn.dw[k] = make_uint2(dst, __float_as_uint(w));
     }
 }
 
@@ -1912,8 +1913,9 @@ __global__ __launch_bounds__(256) void k_checksum(DeviceState d, uint64_t* out)
     uint64_t acc = 0;
     for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < d.n_syn; k += stride) {
         const uint64_t i = d.syn_offset + k;
-        const uint64_t a = ((uint64_t)src32(src_of(d.syn, k)) << 32) | d.syn.dst[k];
-        const uint64_t b = (uint64_t)__float_as_uint(d.syn.w[k]) << 32;  // pad = 0
+        const uint2 dw = d.syn.dw[k];
+        const uint64_t a = ((uint64_t)src32(src_of(d.syn, k)) << 32) | dw.x;
+        const uint64_t b = (uint64_t)dw.y << 32;  // pad = 0
         acc += mix64(a ^ mix64(b + i * 0x9E3779B97F4A7C15ull));
     }
     acc = wave_sum(acc);

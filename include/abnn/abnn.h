@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ABNN_ABI_VERSION 5
+#define ABNN_ABI_VERSION 6
 
 typedef enum abnn_status {
     ABNN_OK = 0,
@@ -181,9 +181,16 @@ typedef struct abnn_stats {
     uint64_t grown;          /* synapses appended by structural updates          */
 } abnn_stats;
 
+/* {dst, w} of one record, adjacent on the device: the pass gathers both for
+ * an event that passed the pre-spike gate with one DRAM access. */
+typedef struct abnn_dst_w {
+    uint32_t dst;
+    float w;
+} abnn_dst_w;
+
 /* Borrowed device pointers (brain.h:54-58 buffer getters).  bufSyn_ is held
- * as a structure of arrays: record i is {src(i), syn_dst[i], syn_w[i], 0}
- * with the 24-bit src split in two streams (N_NRN < 2^24 - 1):
+ * as arrays: record i is {src(i), syn_dst_w[i].dst, syn_dst_w[i].w, 0} with
+ * the 24-bit src split in two streams (N_NRN < 2^24 - 1):
  *   src(i) = syn_src_lo[i] | syn_src_hi[hp(i)] << 16,
  *   hp(i)  = 256 (i / 256) + 4 ((i % 128) / 2) + 2 ((i % 256) / 128) + i % 2,
  * 0xFFFFFF for a removed synapse (downloads report 0xFFFFFFFF).  Random mode
@@ -194,8 +201,7 @@ typedef struct abnn_stats {
 typedef struct abnn_state {
     uint16_t* syn_src_lo;    /* n_syn: src bits 0..15                    */
     uint8_t* syn_src_hi;     /* n_syn rounded up to 256: src bits 16..23 */
-    uint32_t* syn_dst;       /* n_syn (bufSyn_ .dst)                     */
-    float* syn_w;            /* n_syn (bufSyn_ .w)                       */
+    abnn_dst_w* syn_dst_w;   /* n_syn (bufSyn_ .dst, .w)                 */
     uint64_t* last_fired;    /* N_NRN (bufLastFire_)                     */
     uint64_t* last_visited;  /* N_NRN (bufLastVisit_)                    */
     uint64_t* clock;         /* 1 (bufClock_)                            */

@@ -134,13 +134,12 @@ public:
     struct SynapseArrays {
         uint16_t* src_lo;
         uint8_t* src_hi;
-        uint32_t* dst;
-        float* w;
+        abnn_dst_w* dst_w;  // {dst, w} of each record
     };
     SynapseArrays synapse_buffer() const
     {
         const abnn_state s = state();
-        return {s.syn_src_lo, s.syn_src_hi, s.syn_dst, s.syn_w};
+        return {s.syn_src_lo, s.syn_src_hi, s.syn_dst_w};
     }
     uint64_t* last_fired_buffer() const { return state().last_fired; }
     uint64_t* clock_buffer() const { return state().clock; }
