@@ -84,7 +84,8 @@ def test_config2_full_state(gpu):
 
 @pytest.mark.parametrize("over", [
     dict(max_spikes=1), dict(max_spikes=0), dict(max_spikes=200_000),
-    dict(refractory=0, window_pre=0), dict(events=777_777), dict(events=3_000_000),
+    dict(refractory=0, window_pre=0), dict(refractory=6, window_pre=2), dict(refractory=5, window_pre=5),
+    dict(events=777_777), dict(events=3_000_000),
     dict(events=100), dict(renorm_thresh=5), dict(track_visits=1),
     dict(a_ltp=0.5, a_ltd=0.3, eta_home=1e-3, base_scale=3.0),
 ])
