@@ -69,7 +69,7 @@ class Scalars(C.Structure):
 
 
 MODE_SWEEP, MODE_RANDOM = 0, 1  # abnn_params.mode (include/abnn/abnn.h)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class Stats(C.Structure):

@@ -703,7 +703,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (const char* env = std::getenv("ABNN_RANGE_MAP")) d.range_map = std::atoi(env) ? 1u : 0u;
     d.adapt_gain = 2;
     if (const char* env = std::getenv("ABNN_ADAPT_GAIN")) d.adapt_gain = (uint32_t)std::min(4, std::max(1, std::atoi(env)));
-    d.chunk_penalty = 25;  // 1 us per full chunk (~15 % of its refractory stage)
+    d.chunk_penalty = 350;  // 14 us per full chunk: the dense input->output stretch spread over more
+                            // ranges (tools/knob_sweep.sh ABNN_CHUNK_PENALTY: 25 -> 350 measured -6 us per pass)
     d.tail_prio = 4;
     d.apply_blocks = kWalkBlocks;
     if (const char* env = std::getenv("ABNN_APPLY_BLOCKS"))

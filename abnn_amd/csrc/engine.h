@@ -53,15 +53,38 @@ constexpr uint32_t kLbSpinLimit = 1u << 22;  // ~1 s of polls: then error, never
 // i is {src[i], dst[i], w[i]} (SynapsePacked without its never-read pad).
 // src is held in 24 bits (N_NRN < 2^24 - 1, checked at create; the tombstone
 // src is kSrcNone) as two streams, so the sweep's gate reads 3 B per visited
-// event: lo[i] = bits 0..15 (u16, natural order) and hi = bits 16..23 (u8)
-// permuted within every 256-record group so that the one 4-B hi word a gate
-// lane loads per group holds the four records of its two lo words:
+// event: a u16 word lo[i] and a u8 byte hi[hi_pos(i)], together the *filter
+// code* of src -- a bijection of the 24 bits laid out so that the gate's
+// pre-spike filter test (kernels.hip, filter_t / filter_set) needs no hashing:
+// neuron n = 32 j + b sits in filter block g = (j ^ t) mod 8192,
+// t = 0x9E5 (j >> 13), at low bit lb = b and high bit hb = (b + t) mod 32;
+//   lo = g << 3 | hb[2:0]                 (lo & 0xFFF8 = the block's LDS byte address)
+//   hi = lb | x << 5 | hb[4:3] << 6       (x = bit 5 of j >> 13, i.e. n >= 2^23)
+// lo is in natural order, hi permuted within every 256-record group so that
+// the one 4-B hi word a gate lane loads per group holds the four records of
+// its two lo words:
 //   group G = i / 256, r = i % 256, kh = r / 128, lane = (r % 128) / 2, s = r % 2
 //   hi byte at 256 G + 4 lane + 2 kh + s                           (hi_pos)
 // Each array holds capacity + kDummyRecords entries (zero padding: the gate's
 // last iteration reads past the sweep; hi rounded up to whole groups).
 constexpr uint32_t kSrcNone = 0xFFFFFFu;   // 24-bit tombstone src (downloads as 0xFFFFFFFF)
 constexpr uint64_t kMaxNeurons = kSrcNone; // N_NRN < 2^24 - 1
+constexpr uint32_t kCodeFilterWords = 8192; // the filter the code is laid out for (sweep gate shapes)
+
+__host__ __device__ inline uint32_t src_code(uint32_t n)  // 24-bit src -> lo | hi << 16
+{
+    const uint32_t b = n & 31u, j = (n >> 5) & 0x7FFFFu, jh = j >> 13;
+    const uint32_t t = jh * 0x9E5u, g = (j ^ t) & 8191u, hb = (b + t) & 31u;
+    return (g << 3 | (hb & 7u)) | (b | (jh >> 5) << 5 | (hb >> 3) << 6) << 16;
+}
+
+__host__ __device__ inline uint32_t code_src(uint32_t lo, uint32_t hi)  // inverse of src_code
+{
+    const uint32_t g = (lo >> 3) & 8191u, lb = hi & 31u, hb = (lo & 7u) | ((hi >> 6) & 3u) << 3;
+    const uint32_t jh = (((hb - lb) * 13u) & 31u) | ((hi >> 5) & 1u) << 5;  // 13 = 0x9E5^-1 mod 32
+    const uint32_t j = ((g ^ jh * 0x9E5u) & 8191u) | jh << 13;
+    return j << 5 | lb;
+}
 
 struct SynArrays {
     uint16_t* lo;

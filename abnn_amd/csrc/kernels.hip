@@ -154,15 +154,16 @@ __device__ __forceinline__ uint64_t pick_record(uint64_t seed, uint64_t stream, 
 // tombstone; src32 widens it to the interchange value (0xFFFFFFFF).
 __device__ __forceinline__ uint32_t src_of(const SynArrays& a, uint64_t i)
 {
-    return (uint32_t)a.lo[i] | (uint32_t)a.hi[hi_pos(i)] << 16;
+    return code_src(a.lo[i], a.hi[hi_pos(i)]);
 }
 
 __device__ __forceinline__ uint32_t src32(uint32_t v) { return v == kSrcNone ? 0xFFFFFFFFu : v; }
 
 __device__ __forceinline__ void set_src(const SynArrays& a, uint64_t i, uint32_t v)
 {
-    a.lo[i] = (uint16_t)v;
-    a.hi[hi_pos(i)] = (uint8_t)(v >> 16);
+    const uint32_t c = src_code(v);
+    a.lo[i] = (uint16_t)c;
+    a.hi[hi_pos(i)] = (uint8_t)(c >> 16);
     if (a.src32) a.src32[i] = v;
 }
 
@@ -282,6 +283,44 @@ __device__ __forceinline__ uint64_t range_begin(uint32_t b, uint32_t iters, uint
 // no false negatives; the exact bitmap confirms the staged events in the
 // refractory stage.
 __device__ __forceinline__ uint32_t filter_t(uint32_t j, uint32_t lg) { return __umul24(j >> lg, 0x9E5u); }
+
+// The sweep's filter test on the stored code v = lo | hi << 16 of one record
+// (engine.h, src_code): the LDS block at v & 0xFFF8, its low half shifted by
+// lb = v[20:16] (SDWA: the shift amount is bits [4:0] of v's high word), its
+// high half by hb = v[2:0] | v[23:22] << 3 (a shift and a bit-field insert);
+// SDWA puts each shift's low byte (bit 0 = the test) into byte DB of the
+// accumulators HA (low halves) and HB (high halves), keeping their other
+// bytes (DB == 0 starts them): the record passes iff bit 0 of byte DB is set
+// in both.  6 VALU per record (the hashed form took 11-12: a multiply, four
+// shifts, an xor and the bit extracts).
+#define ABNN_SHR_BYTE(acc, amt, val, DST, SRC, KEEP)                                              \
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:" DST " dst_unused:" KEEP " src0_sel:" SRC        \
+        " src1_sel:DWORD"                                                                         \
+        : "+v"(acc)                                                                               \
+        : "v"(amt), "v"(val))
+
+template <int DB>
+__device__ __forceinline__ void filter_test(const uint2* s_fb, uint32_t v, uint32_t& HA, uint32_t& HB)
+{
+    const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s_fb) + (v & 0xFFF8u));
+    uint32_t hb;  // v's bits 0..2 over (v >> 19)'s: bits 3..4 = v[23:22]
+    asm("v_bfi_b32 %0, 7, %1, %2" : "=v"(hb) : "v"(v), "v"(v >> 19));
+    if constexpr (DB == 0) {
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+            : "=v"(HA) : "v"(v), "v"(f.x));
+        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD"
+            : "=v"(HB) : "v"(hb), "v"(f.y));
+    } else if constexpr (DB == 1) {
+        ABNN_SHR_BYTE(HA, v, f.x, "BYTE_1", "WORD_1", "UNUSED_PRESERVE");
+        ABNN_SHR_BYTE(HB, hb, f.y, "BYTE_1", "DWORD", "UNUSED_PRESERVE");
+    } else if constexpr (DB == 2) {
+        ABNN_SHR_BYTE(HA, v, f.x, "BYTE_2", "WORD_1", "UNUSED_PRESERVE");
+        ABNN_SHR_BYTE(HB, hb, f.y, "BYTE_2", "DWORD", "UNUSED_PRESERVE");
+    } else {
+        ABNN_SHR_BYTE(HA, v, f.x, "BYTE_3", "WORD_1", "UNUSED_PRESERVE");
+        ABNN_SHR_BYTE(HB, hb, f.y, "BYTE_3", "DWORD", "UNUSED_PRESERVE");
+    }
+}
 __device__ __forceinline__ void filter_set(uint32_t* f, uint32_t j, uint32_t bits, uint32_t FB, uint32_t lg)
 {
     const uint32_t t = filter_t(j, lg), g = (j ^ t) & (FB - 1), r = t & 31u;
@@ -500,7 +539,8 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
             const uint32_t q = b0 + j * 64 + lane;
             const uint2 e = q < n ? at(q) : make_uint2(0u, 0xFFFFFFFFu);
             rel[j] = e.x;
-            src[j] = e.y;
+            // the sweep stages the record's code (engine.h, src_code), random mode its src
+            src[j] = kRandom || q >= n ? e.y : code_src(e.y & 0xFFFFu, e.y >> 16);
             bw[j] = src[j] < nn ? d.bitmap[src[j] >> 5] : 0u;
         }
 #pragma unroll
@@ -1006,6 +1046,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     constexpr uint32_t LG = __builtin_ctz(FW);
     constexpr uint32_t SE = kChunk + 128;              // a chunk + one staging step (<= 128 events)
     static_assert(K % 4 == 0, "the packed src stream is read in 256-event groups");
+    static_assert(kRandom || FW == kCodeFilterWords, "the sweep tests the stored code (engine.h, src_code)");
     static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
     static_assert(!(kFused && kRandom), "the fused pass is sweep-mode only");
     __shared__ uint2 s_fb[FW];  // the filter's FW 64-bit blocks
@@ -1225,27 +1266,58 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 if (base + idx_of(k) < d.events) vmask |= 1u << k;
         }
 
-        // Pre-spike filter (brain.metal:73-77 pre-selection): every event's
-        // block read back to back; the block index is masked, so any src
-        // (tombstones included) stays in bounds.  ubfe takes the bit offset
-        // mod 32: low bit src mod 32, high bit (src + t) mod 32 = (b + r) mod 32.
-        uint2 fb[K];
-        uint32_t ft[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            ft[k] = filter_t(src[k] >> 5, LG);
-            fb[k] = s_fb[((src[k] >> 5) ^ ft[k]) & (FW - 1)];
-        }
+        // Pre-spike filter (brain.metal:73-77 pre-selection).  Random mode:
+        // every event's block read back to back; the block index is masked,
+        // so any src (tombstones included) stays in bounds; ubfe takes the bit
+        // offset mod 32: low bit src mod 32, high bit (src + t) mod 32 =
+        // (b + r) mod 32.  Sweep: src[k] is the record's code, tested by
+        // filter_test (every block address is below 64 KiB); the hit of event
+        // k is bit 0 of byte k % 4 of H[k / 4] (fm is not formed).
         uint32_t fm = 0;
+        uint32_t H[kRandom ? 1 : K / 4];
+        if constexpr (kRandom) {
+            uint2 fb[K];
+            uint32_t ft[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            fm |= (__builtin_amdgcn_ubfe(fb[k].x, src[k], 1) & __builtin_amdgcn_ubfe(fb[k].y, src[k] + ft[k], 1)) << k;
-        fm &= vmask;
+            for (int k = 0; k < K; ++k) {
+                ft[k] = filter_t(src[k] >> 5, LG);
+                fb[k] = s_fb[((src[k] >> 5) ^ ft[k]) & (FW - 1)];
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                fm |= (__builtin_amdgcn_ubfe(fb[k].x, src[k], 1) & __builtin_amdgcn_ubfe(fb[k].y, src[k] + ft[k], 1)) << k;
+            fm &= vmask;
+        } else {
+#pragma unroll
+            for (int g = 0; g < K / 4; ++g) {
+                uint32_t HA, HB;
+                filter_test<0>(s_fb, src[4 * g], HA, HB);
+                filter_test<1>(s_fb, src[4 * g + 1], HA, HB);
+                filter_test<2>(s_fb, src[4 * g + 2], HA, HB);
+                filter_test<3>(s_fb, src[4 * g + 3], HA, HB);
+                H[g] = HA & HB & 0x01010101u;
+            }
+            if (base + IE > d.events) {  // only the sweep's last iteration (wave-uniform)
+#pragma unroll
+                for (int g = 0; g < K / 4; ++g) {
+                    const uint32_t m = vmask >> (4 * g);
+                    H[g] &= (m & 1u) | (m & 2u) << 7 | (m & 4u) << 14 | (m & 8u) << 21;
+                }
+            }
+        }
+        auto hit = [&](int k) -> bool {
+            if constexpr (kRandom) return (fm >> k) & 1u;
+            else return (H[k >> 2] >> (8 * (k & 3))) & 1u;
+        };
 
         if constexpr (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 if (((vmask >> k) & 1u) && dst[k] < nn) d.last_visited[dst[k]] = now;
+        }
+        if constexpr (!kRandom) {
+#pragma unroll
+            for (int g = 0; g < K / 4; ++g) fm |= H[g];
         }
         if (__ballot(fm != 0) == 0) return;
         const uint32_t rel = (uint32_t)(base - region);
@@ -1265,7 +1337,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         } else {  // event order = (lane, s) within each (g, kh) step of 128 events
 #pragma unroll
             for (int j = 0; j < 2 * NG; ++j) {
-                const bool h0 = (fm >> (2 * j)) & 1u, h1 = (fm >> (2 * j + 1)) & 1u;
+                const bool h0 = hit(2 * j), h1 = hit(2 * j + 1);
                 const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
                 if ((b0 | b1) == 0) continue;  // wave-uniform
                 const uint32_t q = pend + mbcnt64(b0) + mbcnt64(b1);
@@ -1989,7 +2061,6 @@ int occupancy_shape(bool track, bool random)
     X(1024, 16, 8192)       \
     X(512, 8, 8192)         \
     X(512, 16, 8192)        \
-    X(512, 8, 16384)        \
     X(256, 16, 8192)
 
 constexpr uint64_t shape_key(uint32_t b, uint32_t k, uint32_t fw) { return ((uint64_t)b << 40) | ((uint64_t)k << 32) | fw; }

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ABNN_ABI_VERSION 6
+#define ABNN_ABI_VERSION 7
 
 typedef enum abnn_status {
     ABNN_OK = 0,
@@ -190,17 +190,22 @@ typedef struct abnn_dst_w {
 
 /* Borrowed device pointers (brain.h:54-58 buffer getters).  bufSyn_ is held
  * as arrays: record i is {src(i), syn_dst_w[i].dst, syn_dst_w[i].w, 0} with
- * the 24-bit src split in two streams (N_NRN < 2^24 - 1):
- *   src(i) = syn_src_lo[i] | syn_src_hi[hp(i)] << 16,
- *   hp(i)  = 256 (i / 256) + 4 ((i % 128) / 2) + 2 ((i % 256) / 128) + i % 2,
- * 0xFFFFFF for a removed synapse (downloads report 0xFFFFFFFF).  Random mode
+ * the 24-bit src (N_NRN < 2^24 - 1) stored as its filter code c (a
+ * bijection of the 24 bits, laid out for the pass's pre-spike filter) in two
+ * streams: lo = syn_src_lo[i], hi = syn_src_hi[hp(i)],
+ *   hp(i) = 256 (i / 256) + 4 ((i % 128) / 2) + 2 ((i % 256) / 128) + i % 2, and
+ *   b = src % 32, j = src / 32, t = 0x9E5 (j >> 13), g = (j ^ t) % 8192,
+ *   hb = (b + t) % 32:  lo = g << 3 | hb % 8,  hi = b | (j >> 18) % 2 << 5 | hb / 8 << 6;
+ * inverse: g = lo >> 3, b = hi % 32, hb = lo % 8 | (hi >> 6) << 3,
+ *   jh = ((hb - b) 13) % 32 | ((hi >> 5) % 2) << 5, j = ((g ^ 0x9E5 jh) % 8192) | jh << 13.
+ * src 0xFFFFFF marks a removed synapse (downloads report 0xFFFFFFFF).  Random mode
  * keeps an internal u32 copy of src for its picks: write records through
  * abnn_upload_synapses there, not through these pointers.  Taking the
  * pointers makes every later pass rebuild the recent-spike bitmap from
  * lastFired (the caller may write it behind the handle's back). */
 typedef struct abnn_state {
-    uint16_t* syn_src_lo;    /* n_syn: src bits 0..15                    */
-    uint8_t* syn_src_hi;     /* n_syn rounded up to 256: src bits 16..23 */
+    uint16_t* syn_src_lo;    /* n_syn: lo word of the src code          */
+    uint8_t* syn_src_hi;     /* n_syn rounded up to 256: hi byte of it   */
     abnn_dst_w* syn_dst_w;   /* n_syn (bufSyn_ .dst, .w)                 */
     uint64_t* last_fired;    /* N_NRN (bufLastFire_)                     */
     uint64_t* last_visited;  /* N_NRN (bufLastVisit_)                    */

@@ -6,6 +6,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -62,7 +63,7 @@ def test_abi_version_and_status_strings():
     from abnn_amd import _lib
 
     lib = _lib.load()
-    assert lib.abnn_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.abnn_abi_version() == _lib.ABI_VERSION == 7
     assert lib.abnn_status_string(0) == b"ok"
     assert lib.abnn_status_string(4) == b"size mismatch"
 
@@ -103,3 +104,38 @@ def test_shard_partition_helpers():
     assert global_events(1_000_000_000, 150_000_000, 1) == 150_000_128
     assert global_events(1_000_000_000, 150_000_000, 8) == 1_000_000_000
     assert global_events(1_000_000_000, 150_000_000, 2) == 2 * 150_000_128
+
+
+def _src_code(n):
+    """abnn.h (abnn_state): the filter code of a 24-bit src, as (lo, hi)."""
+    n = n.astype(np.uint64)
+    b, j = n & 31, (n >> 5) & 0x7FFFF
+    jh = j >> 13
+    t = jh * 0x9E5
+    g, hb = (j ^ t) & 8191, (b + t) & 31
+    return (g << 3 | (hb & 7)), (b | (jh >> 5) << 5 | (hb >> 3) << 6)
+
+
+def _code_src(lo, hi):
+    g, b = lo >> 3, hi & 31
+    hb = (lo & 7) | (hi >> 6) << 3
+    jh = (((hb - b) * 13) & 31) | ((hi >> 5) & 1) << 5
+    j = ((g ^ jh * 0x9E5) & 8191) | jh << 13
+    return j << 5 | b
+
+
+def test_src_code_is_a_bijection_matching_the_filter():
+    """The stored src layout (abnn.h, ABI 7): every 24-bit src has a distinct
+    (lo, hi), the documented inverse restores it, lo >> 3 is the src's filter
+    block, hi & 31 its low bit and lo & 7 | hi >> 6 << 3 its high bit (the
+    word hash filter_t / filter_set of kernels.hip)."""
+    n = np.arange(1 << 24, dtype=np.uint64)
+    lo, hi = _src_code(n)
+    assert lo.max() < 1 << 16 and hi.max() < 1 << 8
+    assert np.unique(lo | hi << 16).size == 1 << 24
+    assert np.array_equal(_code_src(lo, hi), n)
+    j, b = n >> 5, n & 31
+    t = (j >> 13) * 0x9E5
+    assert np.array_equal(lo >> 3, (j ^ t) & 8191)
+    assert np.array_equal(hi & 31, b)
+    assert np.array_equal((lo & 7) | (hi >> 6) << 3, (b + t) & 31)
