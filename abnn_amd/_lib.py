@@ -69,7 +69,8 @@ class Scalars(C.Structure):
 
 
 MODE_SWEEP, MODE_RANDOM = 0, 1  # abnn_params.mode (include/abnn/abnn.h)
-ABI_VERSION = 7
+ABI_VERSION = 8
+LAYOUT_VERSION = 3
 
 
 class Stats(C.Structure):
@@ -90,14 +91,38 @@ class Stats(C.Structure):
 
 class State(C.Structure):
     _fields_ = [
-        ("syn_src_lo", C.c_void_p),
-        ("syn_src_hi", C.c_void_p),
-        ("syn_dst_w", C.c_void_p),
+        ("synapses", C.c_void_p),  # opaque device records (abnn_synapse_layout)
         ("last_fired", C.c_void_p),
         ("last_visited", C.c_void_p),
         ("clock", C.c_void_p),
         ("reward", C.c_void_p),
         ("rbar", C.c_void_p),
+    ]
+
+
+LAYOUT_MAX_ARRAYS = 4
+
+
+class ArrayDesc(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("bytes", C.c_uint64), ("elem_bytes", C.c_uint32), ("name", C.c_char * 20)]
+
+
+class Layout(C.Structure):
+    """abnn_layout -- the device record layout behind abnn_state.synapses (versioned apart from the ABI)."""
+
+    _fields_ = [("version", C.c_uint32), ("n_arrays", C.c_uint32), ("arrays", ArrayDesc * LAYOUT_MAX_ARRAYS)]
+
+
+class TraversalArgs(C.Structure):
+    """abnn_traversal_args -- monte_carlo_traversal's 14 buffers (brain.metal:42-58), caller-owned."""
+
+    _fields_ = [
+        ("syn", C.c_void_p), ("last_fired", C.c_void_p), ("last_visited", C.c_void_p), ("clock", C.c_void_p),
+        ("n_syn", C.c_uint32), ("tau_vis", C.c_uint32), ("tau_pre", C.c_uint32),
+        ("a_ltp", C.c_float), ("a_ltd", C.c_float), ("w_min", C.c_float), ("w_max", C.c_float),
+        ("budget", C.c_void_p), ("reward", C.c_void_p), ("rbar", C.c_void_p),
+        ("n_nrn", C.c_uint32), ("events", C.c_uint32), ("knobs", C.c_void_p),
+        ("workspace", C.c_void_p), ("workspace_bytes", C.c_uint64),
     ]
 
 
@@ -121,6 +146,7 @@ SIGNATURES = [
     ("abnn_get_dims", C.c_int, [_VP, C.POINTER(Dims)]),
     ("abnn_get_params", C.c_int, [_VP, C.POINTER(Params)]),
     ("abnn_state_ptrs", C.c_int, [_VP, C.POINTER(State)]),
+    ("abnn_synapse_layout", C.c_int, [_VP, C.POINTER(Layout)]),
     ("abnn_n_neuron", C.c_uint64, [_VP]),
     ("abnn_upload_synapses", C.c_int, [_VP, _U64, _VP, _U64]),
     ("abnn_download_synapses", C.c_int, [_VP, _U64, _VP, _U64]),
@@ -144,6 +170,11 @@ SIGNATURES = [
     ("abnn_shard_gate", C.c_int, [_VP, _VP, _VP]),
     ("abnn_shard_apply", C.c_int, [_VP, _VP, _U32, _U32, _VP]),
     ("abnn_shard_commit", C.c_int, [_VP, _VP, _U32, _VP]),
+    ("abnn_get_budget", C.c_int, [_VP, _PU32]),
+    ("abnn_structural_updates", C.c_uint64, [_VP]),
+    ("abnn_traversal_workspace_bytes", C.c_uint64, [_U32, _U32]),
+    ("abnn_launch_traversal", C.c_int, [C.POINTER(TraversalArgs), _VP]),
+    ("abnn_launch_renormalise", C.c_int, [_VP, _VP, _VP, _U32, _VP]),
     ("abnn_get_stats", C.c_int, [_VP, C.POINTER(Stats)]),
     ("abnn_reset_stats", C.c_int, [_VP]),
     ("abnn_enable_timing", C.c_int, [_VP, C.c_int]),
@@ -190,10 +221,16 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)  # AttributeError = the ABI is not exported
         fn.restype = res
         fn.argtypes = args
-    if lib.abnn_abi_version() != ABI_VERSION and not os.environ.get("ABNN_LIB"):
-        # (an ABNN_LIB build of another ABI version is accepted for A/B timing:
-        # the pass/timing entry points have not changed between versions)
-        raise ImportError("libabnn_hip.so ABI version mismatch")
+    got = lib.abnn_abi_version()
+    if got != ABI_VERSION:
+        # an A/B timing build of another ABI version only with an explicit
+        # opt-in: its state layout and record encoding may differ
+        if not os.environ.get("ABNN_LIB_ANY_ABI"):
+            raise ImportError(f"{LIB_PATH}: ABI version {got}, this binding is {ABI_VERSION} "
+                              "(ABNN_LIB_ANY_ABI=1 accepts it for pass timing only)")
+        import warnings
+
+        warnings.warn(f"{LIB_PATH}: ABI version {got} != {ABI_VERSION}; use pass/timing entry points only")
     _lib = lib
     return lib
 

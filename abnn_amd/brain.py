@@ -111,9 +111,28 @@ class Brain:
         return visited_events(self._dims.events_per_pass, self.n_syn(), self._params.mode)
 
     def state_ptrs(self) -> dict:
+        """Borrowed device pointers (brain.h:54-58); ``synapses`` is opaque."""
         s = State()
         call("abnn_state_ptrs", self._h, C.byref(s))
         return {k: int(getattr(s, k) or 0) for k, _ in State._fields_}
+
+    def synapse_layout(self) -> dict:
+        """The device record layout behind state_ptrs()['synapses'] (versioned apart from the ABI)."""
+        lay = _lib.Layout()
+        call("abnn_synapse_layout", self._h, C.byref(lay))
+        arrays = {lay.arrays[i].name.decode(): (int(lay.arrays[i].ptr or 0), int(lay.arrays[i].bytes),
+                                                int(lay.arrays[i].elem_bytes)) for i in range(lay.n_arrays)}
+        return {"version": int(lay.version), "arrays": arrays}
+
+    def budget(self) -> int:
+        """Spike budget left by the last pass (bufBudget_, brain.h:58)."""
+        v = C.c_uint32()
+        call("abnn_get_budget", self._h, C.byref(v))
+        return int(v.value)
+
+    def structural_updates(self) -> int:
+        """Structural updates run so far (host count, no synchronisation)."""
+        return int(self._lib.abnn_structural_updates(self._h))
 
     # ---- synapses ------------------------------------------------------------------------------
     def upload_synapses(self, syn: np.ndarray, first: int = 0) -> None:

@@ -16,8 +16,8 @@ import subprocess
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "abnn_amd")
 CSRC = os.path.join(PKG, "csrc")
-HIP_SOURCES = [os.path.join(CSRC, "kernels.hip"), os.path.join(CSRC, "capi.hip")]
-HIP_DEPS = HIP_SOURCES + [os.path.join(CSRC, "engine.h"),
+HIP_SOURCES = [os.path.join(CSRC, "kernels.hip"), os.path.join(CSRC, "capi.hip"), os.path.join(CSRC, "raw.hip")]
+HIP_DEPS = HIP_SOURCES + [os.path.join(CSRC, "engine.h"), os.path.join(CSRC, "device.h"),
                           os.path.join(ROOT, "include", "abnn", "abnn.h")]
 LIB = os.path.join(PKG, "libabnn_hip.so")
 ORACLE_DIR = os.path.join(ROOT, "oracle")

@@ -96,6 +96,11 @@ struct abnn_brain {
     // compaction writes into (swapped with d.syn), and its scan scratch
     SynArrays syn_alt{};
     uint64_t* compact_offsets = nullptr;
+    uint64_t structural_updates = 0;  // run so far (abnn_structural_updates)
+    uint64_t last_pass = ~0ull;       // pass_index of the last pass (its spike list: abnn_get_budget)
+    // host-mapped error word: a fused pass whose look-back wait gave up sets it
+    // (kernels.hip wg_poll); abnn_traverse sees it without synchronising
+    uint32_t* err_host = nullptr;
 };
 
 namespace {
@@ -103,21 +108,25 @@ namespace {
 // Pass functions run on the caller's stream (NULL = the default stream).
 hipStream_t pick(abnn_brain*, void* s) { return static_cast<hipStream_t>(s); }
 
+// A fused pass whose look-back wait gave up (never expected: every gate
+// workgroup is resident, checked at create) reports it once, here, instead of
+// hanging the GPU; the word is re-armed, so only that failure is reported.
+abnn_status pass_error(abnn_brain* b)
+{
+    if (!b->err_host || __atomic_load_n(b->err_host, __ATOMIC_ACQUIRE) == 0) return ABNN_OK;
+    __atomic_store_n(b->err_host, 0u, __ATOMIC_RELEASE);
+    set_err("fused pass: a look-back wait timed out; the state after that pass is invalid "
+            "(reload it: abnn_load_bnn / abnn_load_flat)");
+    return ABNN_ERR_HIP;
+}
+
 // State accessors are synchronous: they wait for all work on the handle's
 // device (whatever stream it was enqueued on), then copy on the default stream.
 abnn_status sync_all(abnn_brain* b)
 {
     HIP_TRY(hipSetDevice(b->device));
     HIP_TRY(hipDeviceSynchronize());
-    // a fused pass whose look-back gave up waiting (never expected: every
-    // gate workgroup is resident) reports it here instead of hanging the GPU
-    uint32_t err = 0;
-    if (b->d.work) HIP_TRY(hipMemcpy(&err, &b->d.work->error, 4, hipMemcpyDeviceToHost));
-    if (err) {
-        set_err("fused pass: a look-back wait timed out (results of that pass are invalid)");
-        return ABNN_ERR_HIP;
-    }
-    return ABNN_OK;
+    return pass_error(b);
 }
 
 void free_all(abnn_brain* b)
@@ -142,6 +151,7 @@ void free_all(abnn_brain* b)
         (void)hipEventDestroy(e.a);
         (void)hipEventDestroy(e.b);
     }
+    if (b->err_host) (void)hipHostFree(b->err_host);
 }
 
 template <typename T>
@@ -275,6 +285,10 @@ uint64_t tick_events(const abnn_brain* b)
     return b->dims.global_events ? b->dims.global_events : b->d.events;
 }
 
+// renormalise_if_needed (brain.cpp:127-128) on the pass-start clock: the
+// reference's clock is a u32, so the test is on its low 32 bits
+bool renorm_due(const abnn_brain* b) { return (uint64_t)(uint32_t)b->clock_host > b->params.renorm_thresh; }
+
 void host_tick(abnn_brain* b)
 {
     if (tick_events(b) > 0) b->clock_host += b->params.clock_inc;  // brain.metal:129
@@ -381,6 +395,7 @@ abnn_status structural_update(abnn_brain* b)
     b->syn_alt = d.syn;
     d.syn = dst;
     b->dims.n_syn = live + added;
+    b->structural_updates += 1;
     uint64_t grown = 0;
     HIP_TRY(hipMemcpy(&grown, &d.work->stats.grown, 8, hipMemcpyDeviceToHost));
     grown += added;
@@ -426,7 +441,8 @@ bool build_next_ok(const abnn_brain* b)
 {
     const uint64_t W = b->params.window_pre;
     return !b->ext_ptrs && !b->force_full_bitmap && b->params.clock_inc == 1 && W >= 1 && W < kFiredRing &&
-           b->clean_passes + 1 >= W && b->clock_host >= b->max_host_stamp + W;
+           b->clean_passes + 1 >= W && b->clock_host >= b->max_host_stamp + W &&
+           b->clock_host + W < (1ull << 32);  // ages are u32 (age32): the stamp order above holds below 2^32
 }
 
 // This pass's recent-spike buffers (triple-buffered by pass % 3) and, unless
@@ -550,6 +566,7 @@ abnn_status run_commit(abnn_brain* b, const int32_t* gathered, uint32_t world, b
         b->next_built = false;
         b->clock_host = 0;
     }
+    b->last_pass = b->pass_host;
     b->pass_host += 1;
     b->rot += 1;
     const uint32_t ce = b->params.compact_every;
@@ -713,6 +730,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (const char* env = std::getenv("ABNN_PRIO_CLOCK")) d.prio_clock = std::atoi(env) ? 1u : 0u;
     if (const char* env = std::getenv("ABNN_TAIL_PRIO")) d.tail_prio = (uint32_t)std::min(4, std::max(0, std::atoi(env)));
     if (const char* env = std::getenv("ABNN_CHUNK_PENALTY")) d.chunk_penalty = (uint32_t)std::max(0, std::atoi(env));
+    d.fused_max_blocks = (uint32_t)std::max(0, fused_blocks_per_cu(gate_block, gate_k, filter_words, p.track_visits != 0)) *
+                         (uint32_t)cus;
     configure(b);  // sweep partition for the creation size
     const uint64_t max_ranges = (uint64_t)std::min<int>(kMaxGateBlocks, cus * per_cu) * (gate_block / 64);
     d.n_bitmap_words = (uint32_t)(2 * ((n_nrn + 63) / 64));
@@ -771,6 +790,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
         if ((s = dalloc(&d.grown, (uint64_t)p.compact_every * p.max_spikes)) != ABNN_OK) return fail(s);
     }
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
+    if (hipHostMalloc(reinterpret_cast<void**>(&b->err_host), 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d.err_word), b->err_host, 0) != hipSuccess) {
+        set_err("hipHostMalloc (error word) failed");
+        return fail(ABNN_ERR_OOM);
+    }
+    *b->err_host = 0;
     if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.wave_clock, (uint64_t)kWaveClock * kMaxRanges + 32)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.apply_clock, 8 * (uint64_t)kWalkBlocks)) != ABNN_OK) return fail(s);
@@ -816,9 +841,7 @@ abnn_status abnn_state_ptrs(abnn_brain* b, abnn_state* out)
     // the caller may write lastFired or the clock behind the handle's back:
     // rebuild the recent-spike bitmap from lastFired every pass from now on
     b->ext_ptrs = true;
-    out->syn_src_lo = b->d.syn.lo;
-    out->syn_src_hi = b->d.syn.hi;
-    out->syn_dst_w = reinterpret_cast<abnn_dst_w*>(b->d.syn.dw);
+    out->synapses = b->d.syn.lo;  // opaque (abnn_synapse_layout describes the arrays)
     out->last_fired = b->d.last_fired;
     out->last_visited = b->d.last_visited;
     out->clock = b->d.clock;
@@ -827,7 +850,45 @@ abnn_status abnn_state_ptrs(abnn_brain* b, abnn_state* out)
     return ABNN_OK;
 }
 
+// The device record layout (layout 3): the 24-bit src as its
+// filter code in two streams (lo u16 in record order, hi u8 permuted within
+// every 256-record group) and the {dst, w} pairs; random mode adds the u32 src
+// mirror.  Each array holds capacity + padding entries.
+abnn_status abnn_synapse_layout(abnn_brain* b, abnn_layout* out)
+{
+    REQUIRE(b && out, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    b->ext_ptrs = true;  // as abnn_state_ptrs: the caller may write behind the handle's back
+    const uint64_t n = b->dims.syn_capacity + kDummyRecords;
+    auto put = [&](void* p, uint64_t bytes, uint32_t eb, const char* name) {
+        abnn_array_desc& a = out->arrays[out->n_arrays++];
+        a.ptr = p;
+        a.bytes = bytes;
+        a.elem_bytes = eb;
+        std::strncpy(a.name, name, sizeof(a.name) - 1);
+    };
+    out->version = ABNN_LAYOUT_VERSION;
+    put(b->d.syn.lo, n * 2, 2, "src_code_lo");
+    put(b->d.syn.hi, hi_bytes(n), 1, "src_code_hi");
+    put(b->d.syn.dw, n * 8, 8, "dst_w");
+    if (b->d.syn.src32) put(b->d.syn.src32, n * 4, 4, "src32");
+    return ABNN_OK;
+}
+
 uint64_t abnn_n_neuron(const abnn_brain* b) { return b ? b->n_nrn : 0; }
+
+abnn_status abnn_get_budget(abnn_brain* b, uint32_t* remaining)
+{
+    REQUIRE(b && remaining, "null argument");
+    ST_TRY(sync_all(b));
+    uint32_t used = 0;
+    if (b->last_pass != ~0ull)  // spikes of the last pass (its spike list's length, in fired_ring)
+        HIP_TRY(hipMemcpy(&used, b->d.n_fired_ring + (b->last_pass & (kFiredRing - 1)), 4, hipMemcpyDeviceToHost));
+    *remaining = b->params.max_spikes - std::min(used, b->params.max_spikes);
+    return ABNN_OK;
+}
+
+uint64_t abnn_structural_updates(const abnn_brain* b) { return b ? b->structural_updates : 0; }
 
 abnn_status abnn_upload_synapses(abnn_brain* b, uint64_t first, const abnn_synapse* src, uint64_t n)
 {
@@ -992,12 +1053,13 @@ abnn_status abnn_read_outputs(abnn_brain* b, uint8_t* out, uint32_t n)
     REQUIRE(n == b->dims.n_output, "read_outputs: size must equal n_output");
     ST_TRY(sync_all(b));
     std::vector<uint64_t> lf(n);
-    uint64_t now = 0;
+    uint64_t clk = 0;
     if (n) HIP_TRY(hipMemcpy(lf.data(), b->d.last_fired + b->dims.n_input, n * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&now, b->d.clock, 8, hipMemcpyDeviceToHost));
-    const uint64_t start = now > 1 ? now - 1 : 0;  // brain.cpp:151
+    HIP_TRY(hipMemcpy(&clk, b->d.clock, 8, hipMemcpyDeviceToHost));
+    // u32 timestamps, as the reference's (brain.cpp:149-153): the low 32 bits
+    const uint32_t now = (uint32_t)clk, start = now > 1 ? now - 1 : 0;  // brain.cpp:151
     for (uint32_t o = 0; o < n; ++o) {
-        const uint64_t ts = lf[o];
+        const uint32_t ts = (uint32_t)lf[o];
         out[o] = (ts != 0 && ts >= start && ts < now) ? 1 : 0;  // brain.cpp:153-154
     }
     return ABNN_OK;
@@ -1015,11 +1077,12 @@ abnn_status abnn_set_auto_stimulus(abnn_brain* b, uint64_t first, uint64_t count
 abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream)
 {
     REQUIRE(b, "null argument");
+    ST_TRY(pass_error(b));  // a pass already completed failed: enqueue nothing more
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
     for (uint32_t i = 0; i < passes; ++i) {
         // the host reads the clock at encode time, before the pass (brain.cpp:127-128)
-        const bool renorm = b->clock_host > b->params.renorm_thresh;
+        const bool renorm = renorm_due(b);
         if (b->use_fused && fused_pass_supported(b->d)) {
             ST_TRY(run_fused(b, s));
         } else {
@@ -1057,7 +1120,7 @@ abnn_status abnn_shard_gate(abnn_brain* b, void* xchg_dev, void* stream)
     REQUIRE(((uintptr_t)xchg_dev & 7u) == 0, "exchange record must be 8-B aligned");
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
-    b->pending_renorm = b->clock_host > b->params.renorm_thresh;
+    b->pending_renorm = renorm_due(b);
     return run_gate(b, static_cast<int32_t*>(xchg_dev), s);
 }
 

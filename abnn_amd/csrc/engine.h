@@ -36,7 +36,7 @@ struct alignas(16) PassWork {
     uint32_t t0_g2;        // global event 0 passed both gates this pass (re-armed by finalize_pass)
     uint32_t ticket;       // k_apply (fused pass: gate) workgroups done this pass (the last one finalizes, re-arms it)
     uint32_t epoch;        // fused passes run so far: tags this pass's look-back words (never set by the host)
-    uint32_t error;        // fused pass: a look-back wait gave up (abnn_synchronize reports it)
+    uint32_t error;        // unused (the error word is host-mapped: DeviceState::err_word)
     uint32_t spec_wgs;     // fused pass: gate workgroups predicted below the budget cut (the last pass's, less one)
     uint32_t pad[3];
     abnn_stats stats;      // host-kept counters (grown); the device ones live in DeviceState::wg_stats
@@ -135,6 +135,7 @@ struct DeviceState {
     uint32_t* dead;           // pruning on: tombstones per kCompactChunk records (structural update)
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     PassWork* work;
+    uint32_t* err_word;       // host-mapped: a fused pass's look-back wait gave up (capi.hip pass_error)
     uint64_t* wave_clock;     // [kWaveClock * n_ranges] per-wave gate times {start, stream done, refractory
                               // tail done, entry, (fused) look-back done, walk done} (100 MHz, diagnostics)
     uint32_t* fired_ring;     // [kFiredRing * max_spikes] spike list of pass q at (q % kFiredRing), budget order
@@ -181,6 +182,7 @@ struct DeviceState {
     uint32_t iter_events;     // 64 * gate_k events per wave iteration
     uint32_t gate_block;      // threads per gate workgroup
     uint32_t gate_k;          // events per thread per iteration
+    uint32_t fused_max_blocks;  // fused-pass workgroups resident at once (all must be: the look-back)
 };
 
 struct KernelParams {
@@ -217,6 +219,8 @@ hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t
 // weight update + stamps + pass end).  fused_pass_supported: the shape and
 // range count it is compiled for.
 bool fused_pass_supported(const DeviceState& d);
+// Resident fused-pass workgroups per CU (occupancy API; 0 on failure or an uncompiled shape).
+int fused_blocks_per_cu(uint32_t block, uint32_t k, uint32_t filter_words, bool track);
 hipError_t launch_fused_pass(const DeviceState& d, const KernelParams& kp, hipStream_t s);
 // Sharded passes: this shard's exchange record (summary + local spike list).
 hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out, hipStream_t s);

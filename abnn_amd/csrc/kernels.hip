@@ -1,44 +1,52 @@
-// kernels.hip -- CDNA4 (gfx950) kernels of one C1 traversal pass.
+// kernels.hip -- CDNA4 (gfx950) kernels of one C1 traversal pass (handle API).
 //
 // Reference hot path: monte_carlo_traversal (abnn/src/core/kernels/brain.metal:41-130)
-// and renormalise_clock_and_times (brain.metal:135-145).  One single-GPU pass =
-// four launches:
+// and renormalise_clock_and_times (brain.metal:135-145).  DESIGN.md §5 has the
+// measured story; in short:
 //
-//   k_bitmap   : lastFired (u64, 8 B/neuron, read once) -> exact recent-spike
-//                bitmap, bit i = (now - lastFired[i]) <= WINDOW_PRE, OR-folded
-//                into the two LDS filter images; the per-pass stimulus stamp
-//                is fused here.  Only after host writes and in the first
-//                passes: in steady state k_apply builds the next pass's bitmap
-//                from the last passes' spike lists (one pass = two launches).
-//   k_gate     : THE streaming kernel.  Persistent workgroups whose waves each
-//                sweep one contiguous range of events (adaptive partition),
-//                loading only the src word of every record (4 B per event).
-//                Pre-spike filter (brain.metal:73-77) = two LDS bits per event;
-//                events that pass are staged in LDS and, per chunk, run
-//                through the refractory stage by the same wave: exact pre-gate
-//                on the bitmap, record re-read, lastFired[dst] gather,
-//                refractory gate (brain.metal:79-83), spike-candidate test
-//                (brain.metal:91-92), isi.  Random-edge mode: the same loop on
-//                Philox-picked records.
-//   k_apply    : the ordered spike budget of schedule C1 (brain.metal:85-98
-//                without its races) walked over the chunks, weight update
-//                (brain.metal:101-122, non-temporal stores; pruning,
-//                synaptogenesis) and the deferred stamps (brain.metal:125-126).
-//                k_claim precedes it in random mode (highest event wins).
-//                Its last workgroup ends the pass: rBar EWMA
-//                (brain.metal:110-113), one clock tick (brain.metal:129),
-//                statistics; every workgroup also computes a slice of the
-//                next pass's partition.
-//   k_renorm   : brain.metal:135-145 with the base read once (no race).
-//   Sharded passes add k_scan + k_spikes (the exchange record) after the gate;
-//   k_apply then stamps every rank's spikes from the gathered records.
+//   k_gate<..., kFused> : THE pass of a single-GPU sweep, one launch.
+//                Persistent workgroups (one per CU) whose waves each sweep one
+//                contiguous range of events (adaptive partition).  Per event
+//                the 3-B packed src code (engine.h: a u16 lo and a u8 hi
+//                stream) is tested against one 64-bit block of an LDS
+//                blocked Bloom filter of the recent-spike bitmap (the
+//                pre-spike gate, brain.metal:73-77, pre-selected); hits are
+//                staged in LDS and run through the refractory stage by the
+//                same wave (exact bitmap bit, {dst, w} gather, lastFired[dst],
+//                brain.metal:79-83, candidate test brain.metal:91-92, the
+//                updated weight brain.metal:101-121).  A workgroup-level
+//                decoupled look-back resolves the ordered spike budget of
+//                schedule C1 (brain.metal:85-98 without its races); every wave
+//                walks its own survivors, the workgroups owning spikes stamp
+//                them once every look-back word is published
+//                (brain.metal:125-126), workgroup 0 ends the pass (rBar
+//                brain.metal:110-113, clock brain.metal:129).  The next pass's
+//                bitmap and filter are built on the way (set-only atomics).
+//   k_gate<..., !kFused> + k_apply : the two-kernel pass (sharded passes,
+//                random-edge mode, ABNN_FUSED=0): the gate writes per-chunk
+//                survivor slots, k_apply walks the budget over them, updates
+//                weights (non-temporal stores; pruning, synaptogenesis), stamps,
+//                builds the next bitmap and partition, and its last workgroup
+//                ends the pass.  Sharded passes add k_scan + k_spikes (the
+//                exchange record) after the gate; k_apply then stamps every
+//                rank's spikes from the gathered records.  k_claim precedes
+//                k_apply in random mode (highest event wins).
+//   k_bitmap   : lastFired (8 B/neuron, read once) -> the exact recent-spike
+//                bitmap and the filter, with the stimulus stamp; only when the
+//                bitmap cannot come from the last passes' spike lists (the
+//                first passes, host writes).
+//   k_renorm   : brain.metal:135-145 with the base passed by the host (no race).
+//   k_compact / k_tally_dead : the structural update (README §5).
 //
 // All fp32 arithmetic is compiled with -ffp-contract=off and written operation
 // for operation like the oracle, so weights are bit-identical to the CPU.
+// Timestamps are u64; every decision on them is u32 arithmetic (age32,
+// device.h), as the reference's `uint` buffers.
 #include <algorithm>
 #include <type_traits>
 
 #include "engine.h"
+#include "device.h"
 
 #pragma clang fp contract(off)
 
@@ -69,51 +77,6 @@ KernelParams to_kernel_params(const abnn_params& p)
 }
 
 namespace {
-
-// rand01, brain.metal:15-19.
-__device__ __forceinline__ float rand01(uint32_t s)
-{
-    s ^= s << 13;
-    s ^= s >> 17;
-    s ^= s << 5;
-    return (float)(s & 0xFFFFFFu) * (1.0f / 16777216.0f);
-}
-
-// Metal clamp(x, lo, hi) = min(max(x, lo), hi), written as selects so the
-// result is bit-identical to the C oracle (no NaN canonicalisation).
-__device__ __forceinline__ float clampf(float x, float lo, float hi)
-{
-    float m = x > lo ? x : lo;
-    return m < hi ? m : hi;
-}
-
-__device__ __forceinline__ bool spike_candidate(const KernelParams& kp, float w, uint64_t tg,
-                                                uint64_t now)
-{
-    float prob = clampf((w * w) * kp.base_scale, 0.0f, 1.0f);      // brain.metal:91
-    return prob > rand01((uint32_t)tg ^ (uint32_t)now);             // brain.metal:92
-}
-
-__device__ __forceinline__ float updated_weight(const KernelParams& kp, float w, bool fired,
-                                                float R, float rb, float isi)
-{
-    float dW = fired ? kp.a_ltp * (1.0f - w) : (-kp.a_ltd) * w;     // brain.metal:101-102
-    dW = dW + (kp.eta_reward * (R - rb)) * (fired ? 1.0f : 0.0f);   // brain.metal:105-107
-    float est_hz = isi > 0.0f ? 1e6f / isi : 0.0f;                  // brain.metal:116-117
-    dW = dW + (kp.eta_home * (kp.target_rate_hz - est_hz)) * w;     // brain.metal:118
-    return clampf(w + dW, kp.w_min, kp.w_max);                      // brain.metal:121
-}
-
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
-{
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-__device__ __forceinline__ uint32_t wave_uniform(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
 
 // Global-memory views for agent-scope atomics (sc1 loads and stores).
 typedef __attribute__((address_space(1))) uint32_t gu32;
@@ -191,20 +154,6 @@ __device__ __forceinline__ T wave_sum(T v)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
-}
-
-// Inclusive wave scan on DPP (row_shr within 16-lane rows, then the gfx9
-// row broadcasts): six VALU ops, no LDS crossbar round trips.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
-{
-    int v = (int)x;
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-    return (uint32_t)v;
 }
 
 __device__ __forceinline__ uint32_t wave_total(uint32_t x)
@@ -354,7 +303,7 @@ __global__ __launch_bounds__(256) void k_bitmap(DeviceState d, KernelParams kp,
                 L[q] = now;
                 d.last_fired[i] = now;          // Brain::inject_inputs, brain.cpp:82
             }
-            bit = (now - L[q]) <= (uint64_t)kp.window_pre;
+            bit = age32(now, L[q]) <= kp.window_pre;
         }
         const uint64_t m = __ballot(bit);
         if (lane == 0 && (wave * 4 + q) * 64 < d.n_nrn) {
@@ -561,14 +510,14 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
         for (int j = 0; j < R; ++j) {
             if (b0 + (uint32_t)j * 64 >= n) break;  // wave-uniform
             n_g1 += (uint32_t)__popcll(__ballot(bw[j] != 0u));
-            const bool g2 = dst[j] < nn && (now - ld[j]) > (uint64_t)kp.refractory;  // brain.metal:79-83
+            const bool g2 = dst[j] < nn && age32(now, ld[j]) > kp.refractory;  // brain.metal:79-83
             const uint64_t tg = d.syn_offset + region + rel[j];
             const bool cand = g2 && spike_candidate(kp, w[j], tg, now);
             const uint64_t bg = __ballot(g2), bcd = __ballot(cand);
             if (g2) {
                 const uint64_t o = base + n_g2 + mbcnt64(bg);
                 if constexpr (kFused) {
-                    const float wn = updated_weight(kp, w[j], cand, Rw, rbw, (float)(now - ld[j]));
+                    const float wn = updated_weight(kp, w[j], cand, Rw, rbw, (float)age32(now, ld[j]));
                     d.g2x[o] = make_uint4(rel[j] | (cand ? 0x80000000u : 0u), __float_as_uint(w[j]),
                                           __float_as_uint(wn), dst[j]);
                     if (spec) __builtin_nontemporal_store(wn, w_ptr(d.syn, region + rel[j]));  // brain.metal:122
@@ -576,12 +525,17 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
                     if (cand && ci < kCandCap)
                         d.cand_list[crange * kCandCap + ci] = make_uint2((uint32_t)(base - region) + n_g2 + mbcnt64(bg), dst[j]);
                 } else {
-                    const uint32_t isi = __float_as_uint((float)(now - ld[j])) | (cand ? 0x80000000u : 0u);
+                    const uint32_t isi = __float_as_uint((float)age32(now, ld[j])) | (cand ? 0x80000000u : 0u);
                     d.g2x[o] = make_uint4(rel[j], isi, __float_as_uint(w[j]), dst[j]);
                 }
                 if (d.g2src) d.g2src[o] = src[j];  // synaptogenesis keeps src
-                if (tg == 0)  // read by the pass's last workgroup (fused pass): write-through
+                if (tg == 0) {  // read by workgroup 0 at the pass's end (fused pass): write-through,
+                                // drained before this wave reaches the barrier its workgroup's
+                                // look-back word is published behind (the sc1 hand-off form,
+                                // MI355X_MICROARCH.md §inter-workgroup visibility); once per pass
                     __hip_atomic_store((gu32*)&d.work->t0_g2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             }
             n_g2 += (uint32_t)__popcll(bg);
             n_cand += (uint32_t)__popcll(bcd);
@@ -729,7 +683,7 @@ __device__ uint32_t wg_poll(const DeviceState& d, uint32_t n, uint32_t tag, uint
         const uint64_t tot = wave_sum<uint64_t>(sum);
         if (__ballot(!ok) == 0 || (stop_at_budget && tot >= budget)) return (uint32_t)(tot < budget ? tot : budget);
         if (spins >= kLbSpinLimit) {  // never hang the GPU: report and go on
-            if (lane == 0) __hip_atomic_store((gu32*)&d.work->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(d.err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return budget;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -1008,17 +962,17 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
 // ---------------------------------------------------------------------------
 // k_gate: the streaming kernel (see file header).  Every wave owns one
 // contiguous range of events.  The pre-spike gate needs only the src of each
-// record, and the records are held as arrays (SynArrays), so the sweep
-// streams 4 B per event: a wave keeps K events per lane in flight in K VGPRs,
-// each load one coalesced 256-B line segment; the next iteration's loads are
-// issued before this one is examined.  Loads use a wave-uniform base: the
-// arrays are padded by kDummyRecords, so the sweep's last iteration reads past
-// its end instead of masking lanes, and the prefetch after a range's last
-// iteration reads the zero dummy block.  Per event: two LDS filter reads and a
-// few VALU ops, no global load; events that pass both filters (~0.7 % at
-// config 3 in steady state, a third of them real) are staged in LDS as
-// {offset, src}; every chunk of them goes through the refractory stage in
-// the wave itself (a full one at once, the last one after the stream).
+// record, held as a 3-B filter code in two streams (engine.h, SynArrays): per
+// 256-event group a lane loads two lo words and one hi word (wave-uniform
+// bases, non-temporal, two iterations in flight), assembles each record's
+// code with one v_perm and tests it against ONE 8-B block of the LDS filter
+// (filter_test: 6 VALU per event, no global load).  The arrays are padded by
+// kDummyRecords, so the sweep's last iteration reads past its end instead of
+// masking lanes, and the prefetch after a range's last iteration reads the
+// zero dummy block.  Events that pass the filter (under 1 % at config 3 in
+// steady state; the exact bitmap decides) are staged in LDS as {offset, code}; every
+// chunk of them goes through the refractory stage in the wave itself (a full
+// one at once, the last one -- the range's tail -- after the stream).
 // Instruction-issue priority (s_setprio takes an immediate).
 __device__ __forceinline__ void set_priority(uint32_t p)
 {
@@ -2055,6 +2009,15 @@ int occupancy_shape(bool track, bool random)
     return e == hipSuccess ? n : 0;
 }
 
+template <int BLOCK, int K, int FW>
+int occupancy_fused_shape(bool track)
+{
+    int n = 0;
+    const hipError_t e = track ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, false, true>, BLOCK, 0)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, false, true>, BLOCK, 0);
+    return e == hipSuccess ? n : 0;
+}
+
 // Compiled gate shapes: threads per workgroup x events per lane x filter words.
 #define ABNN_GATE_SHAPES(X) \
     X(1024, 8, 8192)        \
@@ -2115,6 +2078,16 @@ hipError_t launch_gate(const DeviceState& d, const KernelParams& kp, hipStream_t
     X(1024, 8, 8192)         \
     X(1024, 16, 8192)
 
+int fused_blocks_per_cu(uint32_t block, uint32_t k, uint32_t fw, bool track)
+{
+    switch (shape_key(block, k, fw)) {
+#define X(B, K, F) case shape_key(B, K, F): return occupancy_fused_shape<B, K, F>(track);
+        ABNN_FUSED_SHAPES(X)
+#undef X
+    }
+    return 0;
+}
+
 bool fused_pass_supported(const DeviceState& d)
 {
     bool shape = false;
@@ -2123,8 +2096,10 @@ bool fused_pass_supported(const DeviceState& d)
         ABNN_FUSED_SHAPES(X)
 #undef X
     }
+    // the look-back waits on other workgroups of the launch: every one must be
+    // resident at once (fused_max_blocks: the occupancy of the fused kernel)
     return shape && d.mode == ABNN_MODE_SWEEP && d.range_map == 0 && d.gate_blocks > 0 &&
-           d.gate_blocks <= kLbMaxWords * 64 && d.n_ranges <= kFusedMaxRanges;
+           d.gate_blocks <= kLbMaxWords * 64 && d.n_ranges <= kFusedMaxRanges && d.gate_blocks <= d.fused_max_blocks;
 }
 
 hipError_t launch_fused_pass(const DeviceState& d, const KernelParams& kp, hipStream_t s)

@@ -137,13 +137,15 @@ class ShardedBrain:
         self.gathered = torch.zeros(words * self.world, dtype=torch.int32, device=dev)
         self.engine = _GpuEngine(self.brain, lambda: torch.cuda.current_stream(dev))
         self.compact_every = int(self.brain.params.compact_every)
-        self._passes = 0
+        self._updates = self.brain.structural_updates()
 
     def step(self, passes: int = 1) -> None:
         for _ in range(passes):
             sharded_pass(self.engine, self.comm, self.xchg, self.gathered)
-            self._passes += 1
-            if self.compact_every and self._passes % self.compact_every == 0:
+            # every rank runs its structural update after the same pass (the
+            # pass index is replicated): re-sum the visited events after one
+            if self.compact_every and self.brain.structural_updates() != self._updates:
+                self._updates = self.brain.structural_updates()
                 self.refresh_global_events()
 
     def refresh_global_events(self) -> None:

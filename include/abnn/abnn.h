@@ -27,7 +27,12 @@
  * Semantics: every pass executes the deterministic legal schedule "C1" of the
  * reference kernel: events in increasing tid order, an
  * ordered global spike budget, all reads of lastFired/clock/rBar observe the
- * pass-start values, stores become visible at pass end.
+ * pass-start values, stores become visible at pass end.  Timestamps are
+ * stored as u64 (README lastFiredNS) and every decision on them is the
+ * reference's u32 arithmetic on their low 32 bits (brain.metal:43-45 declare
+ * them `uint`): ages `now - ts` wrap at 2^32 (brain.metal:74,80,116),
+ * read_outputs and the renormalisation test compare u32 values
+ * (brain.cpp:127-128,149-154).
  */
 #ifndef ABNN_ABNN_H
 #define ABNN_ABNN_H
@@ -39,7 +44,7 @@
 extern "C" {
 #endif
 
-#define ABNN_ABI_VERSION 7
+#define ABNN_ABI_VERSION 8
 
 typedef enum abnn_status {
     ABNN_OK = 0,
@@ -162,7 +167,8 @@ typedef struct abnn_params {
 /* Scalar state (brain.cpp:57-60): clock, reward, running-average reward,
  * plus the pass counter that keys the random-mode picks. */
 typedef struct abnn_scalars {
-    uint64_t clock;          /* u64 (u32 in brain.cpp:57; identical < 2^32) */
+    uint64_t clock;          /* u64 storage; decisions use its low 32 bits (the
+                                reference's u32 clock, brain.cpp:57)          */
     float reward;
     float rbar;
     uint64_t pass_index;     /* passes run by this handle (+1 per pass; not
@@ -181,38 +187,44 @@ typedef struct abnn_stats {
     uint64_t grown;          /* synapses appended by structural updates          */
 } abnn_stats;
 
-/* {dst, w} of one record, adjacent on the device: the pass gathers both for
- * an event that passed the pre-spike gate with one DRAM access. */
-typedef struct abnn_dst_w {
-    uint32_t dst;
-    float w;
-} abnn_dst_w;
-
-/* Borrowed device pointers (brain.h:54-58 buffer getters).  bufSyn_ is held
- * as arrays: record i is {src(i), syn_dst_w[i].dst, syn_dst_w[i].w, 0} with
- * the 24-bit src (N_NRN < 2^24 - 1) stored as its filter code c (a
- * bijection of the 24 bits, laid out for the pass's pre-spike filter) in two
- * streams: lo = syn_src_lo[i], hi = syn_src_hi[hp(i)],
- *   hp(i) = 256 (i / 256) + 4 ((i % 128) / 2) + 2 ((i % 256) / 128) + i % 2, and
- *   b = src % 32, j = src / 32, t = 0x9E5 (j >> 13), g = (j ^ t) % 8192,
- *   hb = (b + t) % 32:  lo = g << 3 | hb % 8,  hi = b | (j >> 18) % 2 << 5 | hb / 8 << 6;
- * inverse: g = lo >> 3, b = hi % 32, hb = lo % 8 | (hi >> 6) << 3,
- *   jh = ((hb - b) 13) % 32 | ((hi >> 5) % 2) << 5, j = ((g ^ 0x9E5 jh) % 8192) | jh << 13.
- * src 0xFFFFFF marks a removed synapse (downloads report 0xFFFFFFFF).  Random mode
- * keeps an internal u32 copy of src for its picks: write records through
- * abnn_upload_synapses there, not through these pointers.  Taking the
- * pointers makes every later pass rebuild the recent-spike bitmap from
- * lastFired (the caller may write it behind the handle's back). */
+/* Borrowed device pointers (brain.h:54-58 buffer getters).  The neuron state
+ * and the scalars are plain arrays (u64 timestamps, README lastFiredNS; every
+ * decision takes their low 32 bits, as the reference's `uint` arithmetic,
+ * brain.metal:43-45,74,80,116).  The synapse records (bufSyn_) are held in a
+ * kernel-specific device layout: `synapses` is opaque.  Read and write
+ * records through abnn_upload_synapses / abnn_download_synapses (the
+ * SynapsePacked interchange format), or describe the layout with
+ * abnn_synapse_layout (versioned separately from the ABI: a layout change
+ * does not change this header).  Taking the pointers makes every later pass
+ * rebuild the recent-spike bitmap from lastFired (the caller may write it
+ * behind the handle's back). */
 typedef struct abnn_state {
-    uint16_t* syn_src_lo;    /* n_syn: lo word of the src code          */
-    uint8_t* syn_src_hi;     /* n_syn rounded up to 256: hi byte of it   */
-    abnn_dst_w* syn_dst_w;   /* n_syn (bufSyn_ .dst, .w)                 */
+    void* synapses;          /* opaque: the device record arrays (abnn_synapse_layout) */
     uint64_t* last_fired;    /* N_NRN (bufLastFire_)                     */
     uint64_t* last_visited;  /* N_NRN (bufLastVisit_)                    */
     uint64_t* clock;         /* 1 (bufClock_)                            */
     float* reward;           /* 1 (bufReward_)                           */
     float* rbar;             /* 1 (bufRBar_)                             */
 } abnn_state;
+
+/* The device record layout behind abnn_state.synapses, for tools that must
+ * address it directly (profilers, debuggers, custom kernels).  `version`
+ * names the layout (DESIGN.md §4 documents each; ABNN_LAYOUT_VERSION is the
+ * one this library writes); arrays[i] = {device pointer, bytes, element
+ * bytes, name}.  A caller that does not know `version` must not touch them. */
+#define ABNN_LAYOUT_VERSION 3
+#define ABNN_LAYOUT_MAX_ARRAYS 4
+typedef struct abnn_array_desc {
+    void* ptr;
+    uint64_t bytes;
+    uint32_t elem_bytes;
+    char name[20];
+} abnn_array_desc;
+typedef struct abnn_layout {
+    uint32_t version;
+    uint32_t n_arrays;
+    abnn_array_desc arrays[ABNN_LAYOUT_MAX_ARRAYS];
+} abnn_layout;
 
 typedef struct abnn_brain abnn_brain;
 
@@ -238,6 +250,7 @@ abnn_status abnn_brain_destroy(abnn_brain* b);
 abnn_status abnn_get_dims(const abnn_brain* b, abnn_dims* out);
 abnn_status abnn_get_params(const abnn_brain* b, abnn_params* out);
 abnn_status abnn_state_ptrs(abnn_brain* b, abnn_state* out);
+abnn_status abnn_synapse_layout(abnn_brain* b, abnn_layout* out);
 /* n_neuron() = n_input + n_output + n_hidden (brain.h:51). */
 uint64_t abnn_n_neuron(const abnn_brain* b);
 
@@ -321,6 +334,57 @@ abnn_status abnn_shard_apply(abnn_brain* b, const void* gathered_dev, uint32_t w
                              uint32_t rank, void* stream);
 abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t world,
                               void* stream);
+
+/* Spike budget left by the last pass: max_spikes minus the spikes it emitted
+ * (the reference's bufBudget_ after a pass, brain.h:58; the host resets it to
+ * kMaxSpikes before every pass, brain.cpp:90, here the max_spikes knob; C1 never
+ * lets it wrap).  max_spikes before the first pass (brain.cpp:66). */
+abnn_status abnn_get_budget(abnn_brain* b, uint32_t* remaining);
+/* Structural updates run by this handle (host-side count, no synchronisation):
+ * a sharded caller re-sums abnn_dims.global_events when it changes. */
+uint64_t abnn_structural_updates(const abnn_brain* b);
+
+/* ---- buffer-index launcher (the reference's kernel ABI) ---------------------
+ * monte_carlo_traversal's 14 buffers (brain.metal:42-58, bound by
+ * Brain::encode_traversal at brain.cpp:93-118) as CALLER-OWNED device memory
+ * in the reference's own layouts: 16-B SynapsePacked records and u32
+ * lastF / clock / budget (brain.cpp:54-60).  One call enqueues one pass of
+ * schedule C1 over the first min(roundup(events,256), n_syn) records on
+ * `stream`: gates, ordered budget (the first *budget spike candidates fire;
+ * *budget is left at the remainder), STDP + reward + homeostasis, write-back
+ * (the whole 16-B record, brain.metal:122), deferred stamps, rBar and one
+ * clock tick.  The knobs the reference compiles in (#define BASE_SCALE ...,
+ * brain.metal:22-31) come from `knobs` (NULL = the reference defaults; only
+ * the #define fields are read -- aLTP..wMax are the buffer arguments).
+ * Scratch: `workspace` of at least abnn_traversal_workspace_bytes(n_syn,
+ * events) bytes of device memory (any contents; reused every pass).  This is
+ * the reference's memory layout, so it streams 16 B per visited event and
+ * gathers lastF for every one (the handle API's layout moves 3).
+ * renormalise_clock_and_times (brain.metal:135-145) on the same buffers:
+ * lastF[i] -= *clock for i < n_nrn, then *clock = 0 (the host decides when,
+ * brain.cpp:127-128).                                                         */
+typedef struct abnn_traversal_args {
+    abnn_synapse* syn;          /* buffer(0)  SynapsePacked[n_syn]           rw */
+    uint32_t* last_fired;       /* buffer(1)  atomic_uint lastF[n_nrn]       rw */
+    uint32_t* last_visited;     /* buffer(2)  unused (brain.metal:44)           */
+    uint32_t* clock;            /* buffer(3)  atomic_uint                    rw */
+    uint32_t n_syn;             /* buffer(4)                                    */
+    uint32_t tau_vis, tau_pre;  /* buffer(5,6) unused (brain.metal:47-48)       */
+    float a_ltp, a_ltd;         /* buffer(7,8)                                  */
+    float w_min, w_max;         /* buffer(9,10)                                 */
+    uint32_t* budget;           /* buffer(11) atomic_uint                    rw */
+    const float* reward;        /* buffer(12)                                   */
+    float* rbar;                /* buffer(13) atomic_float                   rw */
+    uint32_t n_nrn;             /* lastF length (src/dst >= n_nrn never pass)    */
+    uint32_t events;            /* EVENTS_PER_PASS: grid roundup(events,256)    */
+    const abnn_params* knobs;   /* #define knobs, NULL = reference defaults     */
+    void* workspace;            /* device scratch                               */
+    uint64_t workspace_bytes;
+} abnn_traversal_args;
+uint64_t abnn_traversal_workspace_bytes(uint32_t n_syn, uint32_t events);
+abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream);
+abnn_status abnn_launch_renormalise(uint32_t* last_fired, uint32_t* last_visited, uint32_t* clock,
+                                    uint32_t n_nrn, void* stream);
 
 /* ---- statistics / timing ---------------------------------------------------- */
 abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out);   /* synchronises */

@@ -1,0 +1,32 @@
+/*
+ * abnn_debug.h -- diagnostics exported by libabnn_hip.so beside the C-ABI of
+ * abnn.h.  NOT part of the stable boundary: their layouts follow the kernels
+ * (abnn_amd/csrc/engine.h) and change without an ABI version bump.  Used by
+ * tools/ (wave_clock.py, apply_clock.py, pass_stats.py) and the GPU tests.
+ * Every call is synchronous (waits for the device) and copies at most n words.
+ */
+#ifndef ABNN_ABNN_DEBUG_H
+#define ABNN_ABNN_DEBUG_H
+
+#include "abnn.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The last pass's per-wave gate timeline: 12 u64 per range (100-MHz ticks:
+ * start, stream done, tail done, entry, look-back done, walk done, ...). */
+abnn_status abnn_debug_wave_clock(abnn_brain* b, uint64_t* out, uint64_t n);
+/* The last two-kernel pass's per-workgroup k_apply timeline, 8 u64 each. */
+abnn_status abnn_debug_apply_clock(abnn_brain* b, uint64_t* out, uint64_t n);
+/* The recent-spike bitmap the last pass read (bit i: neuron i recent at its
+ * start), and whether the next pass's was built in-pass (1) or will be
+ * rebuilt from lastFired (0). */
+abnn_status abnn_debug_bitmap(abnn_brain* b, uint32_t* out, uint64_t n, int* incremental_next);
+/* The current sweep partition: n_ranges + 1 iteration bounds. */
+abnn_status abnn_debug_range_bounds(abnn_brain* b, uint32_t* out, uint64_t n);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+#endif /* ABNN_ABNN_DEBUG_H */

@@ -185,7 +185,7 @@ public:
         for (uint32_t o = 0; o < n_out_; ++o) {
             const float p = expected[o] * teacher_rate;
             const float u = uni();  // drawn for every output, as in the reference
-            if (u < p && now - lf[o] > 1) teach.push_back(n_in_ + o);
+            if (u < p && (uint32_t)now - (uint32_t)lf[o] > 1u) teach.push_back(n_in_ + o);  // u32 ages (ENG:123-130)
         }
         if (!teach.empty()) brain_.set_timestamps(teach, now);
         teach_ = !teach_;

@@ -64,6 +64,13 @@ uint64_t oracle_splitmix64_at(uint64_t seed, uint64_t k)
     return z ^ (z >> 31);
 }
 
+/* Timestamp arithmetic of the reference: lastF and clock are `uint` (MSL:43,45;
+ * BR:55-57), so every age `now - ts` (MSL:74,80,116) and the renormalisation
+ * test (BR:127-128) are u32 wrap-around.  The build stores u64 timestamps
+ * (README lastFiredNS) and takes every decision on their low 32 bits, so a
+ * stamp ahead of the clock ages like the reference's (2^32 - k, not 2^64 - k). */
+static inline uint32_t age32(uint64_t now, uint64_t ts) { return (uint32_t)now - (uint32_t)ts; }
+
 static inline float clampf(float x, float lo, float hi)
 {
     /* Metal clamp(x, lo, hi) = min(max(x, lo), hi) */
@@ -217,10 +224,10 @@ void oracle_inject_inputs(oracle_state* s, const float* v, uint32_t n, float hz)
 /* Brain::read_outputs, BR:145-157. */
 void oracle_read_outputs(const oracle_state* s, uint8_t* out, uint32_t n)
 {
-    uint64_t now = s->clock;
-    uint64_t start = now > 1 ? now - 1 : 0;
+    uint32_t now = (uint32_t)s->clock;          /* u32 (BR:149-153) */
+    uint32_t start = now > 1 ? now - 1 : 0;
     for (uint32_t o = 0; o < n && o < s->dims.n_output; ++o) {
-        uint64_t ts = s->last_fired[s->dims.n_input + o];
+        uint32_t ts = (uint32_t)s->last_fired[s->dims.n_input + o];
         out[o] = (ts != 0 && ts >= start && ts < now) ? 1 : 0;
     }
 }
@@ -356,7 +363,7 @@ static int pass_begin(oracle_state* s)
     uint64_t now = s->clock;
     for (uint64_t i = 0; i < s->stim_count; ++i)
         if (s->stim_first + i < s->n_nrn) s->last_fired[s->stim_first + i] = now;
-    return now > s->p.renorm_thresh;
+    return (uint64_t)(uint32_t)now > s->p.renorm_thresh;  /* u32 clock, BR:127-128 */
 }
 
 /* Pass end: deferred stamps, rBar, clock tick (MSL:110-113,125-129), then the
@@ -403,17 +410,17 @@ void oracle_pass_serial(oracle_state* s)
         uint64_t tg = s->dims.syn_offset + t;
         if (p->track_visits && sy.dst < s->n_nrn) s->last_visited[sy.dst] = now;  /* README §4 */
         if (sy.src >= s->n_nrn) continue;                       /* removed synapse (README §5) */
-        if (now - L[sy.src] > p->window_pre) continue;          /* MSL:73-77 */
+        if (age32(now, L[sy.src]) > p->window_pre) continue;    /* MSL:73-77 */
         s->stats.pre_gated++;
         uint64_t ld = L[sy.dst];                                /* MSL:79 */
-        if (now - ld <= p->refractory) continue;                /* MSL:80-83 */
+        if (age32(now, ld) <= p->refractory) continue;          /* MSL:80-83 */
         s->stats.post_gated++;
         if (budget == 0) continue;                              /* MSL:85-88 */
         s->stats.updated++;
         int f = spike_candidate(p, sy.w, tg, now);              /* MSL:91-92 */
         if (f) budget -= 1;                                     /* MSL:95-98 (C1: never loses) */
         if (tg == 0) t0_updated = 1;                            /* MSL:110-113 */
-        float isi = (float)(now - ld);                          /* MSL:116 */
+        float isi = (float)age32(now, ld);                      /* MSL:116 (u32) */
         float w = updated_weight(p, sy.w, f, R, rb, isi);       /* MSL:101-121 */
         if (!random) s->stats.pruned += store_weight(s, t, w);  /* MSL:122 (+ pruning) */
         else pend_push(&pend, e, w);
@@ -473,17 +480,17 @@ static void gate_range(const oracle_state* s, uint64_t t0, uint64_t t1, g2vec* o
          * the same value `now` from every thread */
         if (p->track_visits && sy.dst < s->n_nrn) s->last_visited[sy.dst] = now;
         if (sy.src >= s->n_nrn) continue;  /* removed synapse */
-        if (now - L[sy.src] > p->window_pre) continue;
+        if (age32(now, L[sy.src]) > p->window_pre) continue;
         c->g1++;
         uint64_t ld = L[sy.dst];
-        if (now - ld <= p->refractory) continue;
+        if (age32(now, ld) <= p->refractory) continue;
         c->g2++;
         uint64_t tg = s->dims.syn_offset + t;
         if (tg == 0) c->t0 = 1;
         if (c->cand >= p->max_spikes) continue;
         oracle_g2 e;
         e.t = t;
-        e.isi = (float)(now - ld);
+        e.isi = (float)age32(now, ld);
         e.pre = (uint32_t)c->cand;
         e.cand = (uint32_t)spike_candidate(p, sy.w, tg, now);
         e.w = sy.w;
@@ -578,7 +585,7 @@ void oracle_shard_commit(oracle_state* s, const int32_t* gathered, uint32_t worl
     const uint64_t budget = s->p.max_spikes;
     uint64_t events = 0, off = 0;
     int64_t t0 = 0;
-    int renorm = s->clock > s->p.renorm_thresh;
+    int renorm = (uint64_t)(uint32_t)s->clock > s->p.renorm_thresh;
     uint64_t now = s->clock;
     for (uint32_t r = 0; r < world; ++r) {
         const int64_t* sm = (const int64_t*)(gathered + r * words);

@@ -38,14 +38,58 @@ int main()
         } catch (const abnn::size_mismatch&) {
             mismatch_thrown = true;
         }
+        // The reference caller's own code shapes (brain-engine.cpp:31-53,
+        // 119-134, 180-182) through the MTL::Buffer-like views: records
+        // written into synapse_buffer()->contents() + didModifyRange,
+        // teacher spikes poked into the u32 lastFired view, the reward through
+        // its view, the budget read after every pass (brain.h:54-58).
+        uint64_t views_checksum = 0, budget_sum = 0, views_outputs = 0;
+        {
+            abnn::Brain vb(256, 256, 488, 10'000, 100'000);
+            vb.build_pipeline();
+            vb.build_buffers();
+            auto* syn = reinterpret_cast<abnn::SynapsePacked*>(vb.synapse_buffer()->contents());
+            const uint32_t max = vb.n_syn();
+            for (uint32_t i = 0; i < max; ++i)  // a reproducible graph (tests/test_cpp_api.py restates it)
+                syn[i] = {(i * 7919u) % vb.n_neuron(), (i * 104729u + 13u) % vb.n_neuron(),
+                          0.1f + (float)(i % 1000) / 1000.0f, 0.0f};
+            vb.synapse_buffer()->didModifyRange(abnn::Range(0, (uint64_t)max * sizeof(abnn::SynapsePacked)));
+            for (int pass = 0; pass < 24; ++pass) {
+                vb.inject_inputs(in, 1000.0f);
+                uint32_t* lf = (uint32_t*)vb.last_fired_buffer()->contents();
+                const uint32_t now = *(uint32_t*)vb.clock_buffer()->contents();
+                if (pass % 2 == 0)
+                    for (uint32_t o = 0; o < vb.n_output(); ++o)
+                        if (o % 5 == (uint32_t)pass % 5 && now - lf[vb.n_input() + o] > 1) lf[vb.n_input() + o] = now;
+                if (pass == 12) {
+                    float* r = (float*)vb.reward_buffer()->contents();
+                    *r = 0.25f;
+                    vb.reward_buffer()->didModifyRange(abnn::Range(0, 4));
+                }
+                vb.encode_traversal();
+                vb.synchronize();
+                budget_sum += *(uint32_t*)vb.budget_buffer()->contents();
+                for (bool b : vb.read_outputs()) views_outputs += b ? 1 : 0;
+            }
+            views_checksum = vb.checksum();
+            bool threw = false;
+            try {
+                *(uint32_t*)vb.budget_buffer()->contents() = 7;
+                vb.budget_buffer()->didModifyRange(abnn::Range(0, 4));
+            } catch (const std::logic_error&) {
+                threw = true;
+            }
+            if (!threw) throw std::runtime_error("budget_buffer() accepted a write");
+        }
         const abnn_scalars sc = brain.scalars();
         uint64_t lf_sum = 0;
         for (uint64_t v : brain.last_fired()) lf_sum += v;
         std::printf("{\"clock\": %" PRIu64 ", \"rbar\": %.9g, \"checksum\": %" PRIu64
                     ", \"copy_checksum\": %" PRIu64 ", \"last_fired_sum\": %" PRIu64
-                    ", \"outputs_fired\": %" PRIu64 ", \"mismatch_thrown\": %s}\n",
+                    ", \"outputs_fired\": %" PRIu64 ", \"mismatch_thrown\": %s, \"views_checksum\": %" PRIu64
+                    ", \"budget_sum\": %" PRIu64 ", \"views_outputs\": %" PRIu64 "}\n",
                     sc.clock, (double)sc.rbar, brain.checksum(), copy.checksum(), lf_sum,
-                    outputs_fired, mismatch_thrown ? "true" : "false");
+                    outputs_fired, mismatch_thrown ? "true" : "false", views_checksum, budget_sum, views_outputs);
         return 0;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());

@@ -133,11 +133,11 @@ class MetalEmu:
                 ticked |= tid == 0
                 continue                            # removed synapse (README §5)
             lp = lastF[self.src[e]].load()
-            if (now - lp) & U64 > p["window_pre"]:
+            if (now - lp) & U32 > p["window_pre"]:   # uint arithmetic, MSL:74
                 ticked |= tid == 0
                 continue
             ld = lastF[self.dst[e]].load()
-            if (now - ld) & U64 <= p["refractory"]:
+            if (now - ld) & U32 <= p["refractory"]:  # MSL:80
                 ticked |= tid == 0
                 continue
             if budget == 0:
@@ -160,7 +160,7 @@ class MetalEmu:
             dW = F(dW + F(F(F(p["eta_reward"]) * F(R - rb)) * F(1.0 if fired else 0.0)))
             if tid == 0:
                 rbar.store(F(rb + F(F(p["alpha_rbar"]) * F(R - rb))))
-            isi = F((now - ld) & U64)
+            isi = F((now - ld) & U32)                # float(uint), MSL:116
             est = F(F(1e6) / isi) if isi > F(0.0) else F(0.0)
             dW = F(dW + F(F(F(p["eta_home"]) * F(F(p["target_rate_hz"]) - est)) * w))
             nw = metal_clamp(F(w + dW), F(p["w_min"]), F(p["w_max"]))
@@ -216,7 +216,7 @@ class MetalEmu:
         first, count = self.stim
         for i in range(first, first + count):
             self.lastF[i] = self.clock
-        renorm = self.clock > self.p["renorm_thresh"]   # host read before the pass
+        renorm = (self.clock & U32) > self.p["renorm_thresh"]   # host read (u32) before the pass
         self.kernel()
         if renorm:                                      # brain.metal:135-145
             base = self.clock

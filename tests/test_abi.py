@@ -11,10 +11,11 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "abnn", "abnn.h")
+DEBUG_HEADER = os.path.join(ROOT, "include", "abnn", "abnn_debug.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*(abnn_[a-z0-9_]+)\s*\(",
                                  src, flags=re.M)))
@@ -32,20 +33,35 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == bound, set(names) ^ bound
 
 
+def test_exported_symbols_are_exactly_the_declared_ones():
+    """Every abnn_* function the library exports is declared in abnn.h (the
+    boundary) or abnn_debug.h (diagnostics, outside the stable ABI)."""
+    from abnn_amd import _lib
+
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if re.search(r" T abnn_", ln)}
+    declared = set(declared_functions()) | set(declared_functions(DEBUG_HEADER))
+    assert exported == declared, exported ^ declared
+    assert not set(declared_functions()) & set(declared_functions(DEBUG_HEADER))
+
+
 def test_struct_layouts_match_c(tmp_path):
     from abnn_amd import _lib
     from oracle import oracle as O
 
     prog = tmp_path / "sz.c"
     prog.write_text('#include "abnn/abnn.h"\n#include <stdio.h>\n#include <stddef.h>\n'
-                    'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(abnn_synapse),'
+                    'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(abnn_synapse),'
                     'sizeof(abnn_dims), sizeof(abnn_params), sizeof(abnn_scalars), sizeof(abnn_stats),'
-                    'sizeof(abnn_state), offsetof(abnn_params, renorm_thresh));return 0;}\n')
+                    'sizeof(abnn_state), offsetof(abnn_params, renorm_thresh), sizeof(abnn_layout),'
+                    'sizeof(abnn_traversal_args), offsetof(abnn_traversal_args, workspace));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(prog)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [16, C.sizeof(_lib.Dims), C.sizeof(_lib.Params), C.sizeof(_lib.Scalars),
-            C.sizeof(_lib.Stats), C.sizeof(_lib.State), _lib.Params.renorm_thresh.offset]
+            C.sizeof(_lib.Stats), C.sizeof(_lib.State), _lib.Params.renorm_thresh.offset,
+            C.sizeof(_lib.Layout), C.sizeof(_lib.TraversalArgs), _lib.TraversalArgs.workspace.offset]
     assert got == want
     assert C.sizeof(O.Params) == C.sizeof(_lib.Params) and C.sizeof(O.Dims) == C.sizeof(_lib.Dims)
 
@@ -63,7 +79,7 @@ def test_abi_version_and_status_strings():
     from abnn_amd import _lib
 
     lib = _lib.load()
-    assert lib.abnn_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.abnn_abi_version() == _lib.ABI_VERSION == 8
     assert lib.abnn_status_string(0) == b"ok"
     assert lib.abnn_status_string(4) == b"size mismatch"
 
@@ -125,7 +141,7 @@ def _code_src(lo, hi):
 
 
 def test_src_code_is_a_bijection_matching_the_filter():
-    """The stored src layout (abnn.h, ABI 7): every 24-bit src has a distinct
+    """The stored src layout (layout 3): every 24-bit src has a distinct
     (lo, hi), the documented inverse restores it, lo >> 3 is the src's filter
     block, hi & 31 its low bit and lo & 7 | hi >> 6 << 3 its high bit (the
     word hash filter_t / filter_set of kernels.hip)."""
@@ -139,3 +155,24 @@ def test_src_code_is_a_bijection_matching_the_filter():
     assert np.array_equal(lo >> 3, (j ^ t) & 8191)
     assert np.array_equal(hi & 31, b)
     assert np.array_equal((lo & 7) | (hi >> 6) << 3, (b + t) & 31)
+
+
+def test_workspace_bytes_of_the_buffer_index_launcher():
+    """abnn_traversal_workspace_bytes: header + per-tile counts + a 16-B survivor
+    slot per visited event (min(roundup(events, 256), n_syn)), tiles of 2048."""
+    from abnn_amd import _lib
+
+    lib = _lib.load()
+    ws = lib.abnn_traversal_workspace_bytes
+    assert ws(0, 100) == 64
+    tiles = (10_000 + 2047) // 2048
+    assert ws(10_000, 100_000) == 64 + ((12 * tiles + 15) & ~15) + 16 * 2048 * tiles
+    assert ws(1_000_000_000, 150_000_000) == ws(150_000_128, 150_000_000)  # only visited events
+
+
+def test_launcher_rejects_bad_arguments():
+    from abnn_amd import _lib
+
+    lib = _lib.load()
+    a = _lib.TraversalArgs()
+    assert lib.abnn_launch_traversal(C.byref(a), None) == 1  # ABNN_ERR_INVALID: null buffers

@@ -43,3 +43,31 @@ def test_cpp_brain_matches_oracle(gpu):
     assert got["last_fired_sum"] == int(ob.last_fired.sum())
     assert got["outputs_fired"] == fired
     assert got["mismatch_thrown"] is True
+
+    # the reference caller's code shapes through the buffer views (brain_cpp_test.cpp)
+    vb = O.OracleBrain(256, 256, 488, 10_000, 100_000)
+    n_nrn = vb.n_neuron()
+    i = np.arange(10_000, dtype=np.uint64)
+    syn = np.zeros(10_000, dtype=O.SYN_DTYPE)
+    syn["src"] = (i * 7919) % n_nrn
+    syn["dst"] = (i * 104729 + 13) % n_nrn
+    syn["w"] = np.float32(0.1) + (i % 1000).astype(np.float32) / np.float32(1000.0)
+    vb.set_synapses(syn)
+    budget_sum = outputs = 0
+    for k in range(24):
+        vb.inject_inputs(v, 1000.0)
+        now = vb.clock & 0xFFFFFFFF
+        if k % 2 == 0:
+            for o in range(256):
+                lf = int(vb.last_fired[256 + o]) & 0xFFFFFFFF
+                if o % 5 == k % 5 and ((now - lf) & 0xFFFFFFFF) > 1:
+                    vb.last_fired[256 + o] = now
+        if k == 12:
+            vb.set_reward(0.25)
+        before = vb.stats()["fired"]
+        vb.pass_serial()
+        budget_sum += 2560 - (vb.stats()["fired"] - before)
+        outputs += int(vb.read_outputs().sum())
+    assert got["views_checksum"] == vb.checksum()
+    assert got["budget_sum"] == budget_sum
+    assert got["views_outputs"] == outputs

@@ -1,0 +1,184 @@
+"""GPU parity of the buffer-index launcher (abnn_launch_traversal /
+abnn_launch_renormalise): the reference kernel's 14 buffers (brain.metal:42-58)
+as caller-owned device memory in the reference's own layouts -- 16-B
+SynapsePacked records, u32 lastF / clock / budget -- against the CPU oracle,
+bit-exact, pass by pass.  Device memory comes from torch (plumbing); every pass
+runs through the C-ABI.  The host side of each pass restates
+Brain::encode_traversal (brain.cpp:87-122): budget = kMaxSpikes, then one
+dispatch; inputs are stamped `now` by the host before it (inject_inputs with
+every input firing, brain.cpp:73-83)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class RawBrain:
+    """Caller-owned buffers, as Brain::build_buffers allocates them (brain.cpp:52-69)."""
+
+    def __init__(self, syn: np.ndarray, n_nrn: int, events: int, max_spikes: int = 2560, knobs=None):
+        import torch
+
+        from abnn_amd import _lib
+
+        self.lib = _lib.load()
+        self.t = torch
+        dev = torch.device("cuda", 0)
+        self.syn = torch.from_numpy(syn.view(np.uint32).reshape(-1, 4).copy()).to(dev)
+        self.lastF = torch.zeros(n_nrn, dtype=torch.int32, device=dev)
+        self.lastV = torch.zeros(n_nrn, dtype=torch.int32, device=dev)
+        self.scal = torch.zeros(4, dtype=torch.int32, device=dev)  # clock, budget, reward, rBar
+        self.n_syn, self.n_nrn, self.events, self.max_spikes = syn.shape[0], n_nrn, events, max_spikes
+        nb = int(self.lib.abnn_traversal_workspace_bytes(self.n_syn, events))
+        self.ws = torch.zeros(max(16, nb), dtype=torch.uint8, device=dev)
+        self.knobs = knobs
+        a = _lib.TraversalArgs()
+        p = self.scal.data_ptr()
+        a.syn, a.last_fired, a.last_visited, a.clock = self.syn.data_ptr(), self.lastF.data_ptr(), \
+            self.lastV.data_ptr(), p
+        a.n_syn, a.tau_vis, a.tau_pre = self.n_syn, 50_000, 50_000
+        kp = knobs if knobs is not None else _lib.default_params()
+        a.a_ltp, a.a_ltd, a.w_min, a.w_max = kp.a_ltp, kp.a_ltd, kp.w_min, kp.w_max
+        a.budget, a.reward, a.rbar = p + 4, p + 8, p + 12
+        a.n_nrn, a.events = n_nrn, events
+        a.knobs = C.cast(C.pointer(knobs), C.c_void_p) if knobs is not None else None
+        a.workspace, a.workspace_bytes = self.ws.data_ptr(), nb
+        self.args = a
+
+    def set_clock(self, v: int) -> None:
+        self.scal[0] = np.int32(np.uint32(v).view(np.int32))
+
+    def set_reward(self, r: float) -> None:
+        self.scal[2] = int(np.float32(r).view(np.int32))
+
+    def one_pass(self, stim: int = 256) -> None:
+        t = self.t
+        if stim:  # inject_inputs with every input firing: lastF[i] = clock (brain.cpp:82)
+            self.lastF[:stim] = self.scal[0]
+        self.scal[1] = self.max_spikes  # encode_traversal resets the budget (brain.cpp:90)
+        assert self.lib.abnn_launch_traversal(C.byref(self.args), None) == 0
+        t.cuda.synchronize()
+
+    def renormalise(self) -> None:
+        assert self.lib.abnn_launch_renormalise(self.lastF.data_ptr(), self.lastV.data_ptr(), self.scal.data_ptr(),
+                                                self.n_nrn, None) == 0
+        self.t.cuda.synchronize()
+
+    def records(self) -> np.ndarray:
+        return self.syn.cpu().numpy().reshape(-1).view(np.uint32)
+
+    def last_fired(self) -> np.ndarray:
+        return self.lastF.cpu().numpy().view(np.uint32)
+
+    def scalars(self):
+        s = self.scal.cpu().numpy()
+        return int(s[0].view(np.uint32)), int(s[1].view(np.uint32)), float(s[3].view(np.float32))
+
+
+def _run(n_hidden, n_syn, events, passes, seed=1, max_spikes=2560, reward_at=None, tombstones=0, renorm_at=None,
+         clock0=0, knobs=None):
+    from oracle import oracle as O
+
+    n_nrn = 512 + n_hidden
+    over = {} if knobs is None else {k: getattr(knobs, k) for k, _ in O.Params._fields_}
+    over["max_spikes"] = max_spikes
+    over["renorm_thresh"] = 2**64 - 1  # the raw launcher's host decides renormalisation (renorm_at below)
+    o = O.OracleBrain(256, 256, n_hidden, n_syn, events, **over)
+    o.build_random_graph(seed, nthreads=8)
+    if tombstones:  # pruned records {0xFFFFFFFF, 0xFFFFFFFF} (abnn.h): never pass
+        idx = np.arange(0, n_syn, max(1, n_syn // tombstones))[:tombstones]
+        s = o.syn.copy()
+        s["src"][idx] = 0xFFFFFFFF
+        s["dst"][idx] = 0xFFFFFFFF
+        o.set_synapses(s)
+    o.set_scalars(clock0, 0.0, 0.0)
+    r = RawBrain(o.syn.copy(), n_nrn, events, max_spikes, knobs)
+    r.set_clock(clock0)
+    for k in range(passes):
+        if reward_at is not None and k == reward_at:
+            o.set_reward(0.5)
+            r.set_reward(0.5)
+        o.set_timestamps(range(256), o.clock)
+        before = o.stats()["fired"]
+        o.pass_serial()
+        r.one_pass()
+        if renorm_at is not None and k == renorm_at:  # the host's decision (brain.cpp:127-128)
+            base = o.clock
+            o.last_fired[:] = (o.last_fired - np.uint64(base)) & np.uint64(0xFFFFFFFF)
+            o.set_scalars(0, o.s.reward, o.s.rbar)
+            r.renormalise()
+        clock, budget, rbar = r.scalars()
+        assert clock == o.clock & 0xFFFFFFFF, k
+        assert budget == max_spikes - (o.stats()["fired"] - before), k
+        assert np.float32(rbar) == np.float32(o.s.rbar), k
+        assert np.array_equal(r.last_fired(), (o.last_fired & np.uint64(0xFFFFFFFF)).astype(np.uint32)), k
+        assert np.array_equal(r.records(), o.syn.view(np.uint32)), k
+    return o
+
+
+def test_raw_config1_every_pass(gpu):
+    o = _run(488, 10_000, 100_000, 40, reward_at=15)  # BASELINE configs[0]
+    assert o.stats()["fired"] > 0
+
+
+def test_raw_c2lite_budget_saturated(gpu):
+    # 100k neurons, 1M synapses: all-gated passes 3-5, then the budget-saturated steady state
+    o = _run(99_488, 1_000_000, 1_000_000, 14, reward_at=7)
+    st = o.stats()
+    assert st["fired"] >= 2560 * 4 and st["updated"] > st["fired"]
+
+
+@pytest.mark.parametrize("max_spikes", [0, 1, 37, 10**8])
+def test_raw_budgets(gpu, max_spikes):
+    _run(9_488, 200_000, 150_000, 8, max_spikes=max_spikes)
+
+
+def test_raw_partial_sweep_tombstones_and_odd_events(gpu):
+    # events not a multiple of 256 (grid rounds up, brain.cpp:116-118), fewer
+    # records than the grid for one, tombstoned records
+    _run(9_488, 100_000, 54_321, 8, tombstones=500)
+    _run(9_488, 3_000, 4_097, 8)
+
+
+def test_raw_renormalise_and_clock_near_wrap(gpu):
+    _run(9_488, 100_000, 100_000, 10, renorm_at=6, clock0=3_999_990)
+    _run(9_488, 100_000, 100_000, 8, clock0=0xFFFFFFFF - 3)  # u32 clock wraps mid-run (brain.metal:45)
+
+
+def test_raw_knobs(gpu):
+    from abnn_amd import _lib
+
+    k = _lib.default_params(base_scale=1.7, refractory=0, window_pre=2, eta_home=1e-4, a_ltp=0.08, w_min=0.05)
+    _run(9_488, 100_000, 100_000, 8, knobs=k, reward_at=2)
+
+
+def test_raw_full_size_c3_sample_is_fast_enough(gpu):
+    """The reference layout at config 3's visited events (150M of 1B records:
+    the sweep reads only those): a few passes bit-exact on the property side
+    (clock, budget left, stamps only at the clock) -- the full-state oracle
+    comparison runs at the smaller sizes above."""
+    import time
+
+    import torch
+
+    n_nrn, n_syn, events = 5_000_512, 150_000_128, 150_000_000
+    from oracle import oracle as O
+
+    o = O.OracleBrain(256, 256, n_nrn - 512, n_syn, events)
+    o.build_random_graph(1, nthreads=16)
+    r = RawBrain(o.syn, n_nrn, events)
+    del o
+    for k in range(8):
+        r.one_pass()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(4):
+        r.one_pass()
+    dt = (time.perf_counter() - t0) / 4
+    clock, budget, _ = r.scalars()
+    assert clock == 12 and 0 <= budget <= 2560
+    lf = r.last_fired()
+    assert lf.max() <= 11
+    print(f"raw launcher at c3: {dt * 1e3:.2f} ms per pass, {events / dt / 1e9:.1f} G events/s")

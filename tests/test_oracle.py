@@ -377,3 +377,48 @@ def test_structural_shard_world1_equals_serial(mode):
         oracle_shard_pass([b])
     assert np.array_equal(a.syn.view(np.uint32), b.syn.view(np.uint32))
     assert a.stats() == b.stats()
+
+
+def test_stamp_ahead_of_clock_ages_in_u32():
+    """lastF/clock are `uint` in the reference (brain.metal:43,45): a dst stamp
+    ahead of the clock (a host write of now + 3) is 2^32 - 3 ticks old, not
+    2^64 - 3 (brain.metal:80,116).  isi = float(2^32 - 3) = 2^32, so the
+    homeostatic term 1000 - 1e6/isi is 999.99976f (not 1000.0f)."""
+    f = np.float32
+    isi = f(2**32 - 3)
+    assert isi == f(2**32)
+    est = f(f(1e6) / isi)
+    assert f(f(1000.0) - est) == f(999.99976)
+    assert f(f(1000.0) - f(f(1e6) / f(2.0**64))) == f(1000.0)  # what u64 ages would give
+
+    now = 100
+    ob = O.OracleBrain(1, 1, 1, 1, 1)
+    ob.set_synapses(np.array([(0, 1, 0.3, 0.0)], dtype=O.SYN_DTYPE))
+    ob.set_scalars(now, 0.0, 0.0, 0)
+    ob.last_fired[:] = [now, now + 3, 0]        # pre-spike recent; dst stamped ahead of the clock
+    w = f(0.3)
+    cand = f(f(w * w) * f(0.8)) > f(O.rand01(0 ^ now))
+    ob.pass_serial(1)
+    st = ob.stats()
+    assert (st["pre_gated"], st["post_gated"], st["updated"]) == (1, 1, 1)  # 2^32-3 > REFRACTORY
+    dW = f(f(0.04) * f(f(1.0) - w)) if cand else f(f(-0.02) * w)
+    dW = f(dW + f(f(f(1e-3) * f(0.0)) * f(1.0 if cand else 0.0)))
+    dW = f(dW + f(f(f(1e-6) * f(999.99976)) * w))
+    expect = min(max(f(w + dW), f(0.001)), f(1.0))
+    assert ob.syn["w"][0].view(np.uint32) == np.float32(expect).view(np.uint32)
+    # the emulator (per-thread Metal semantics) agrees
+    emu = _emu_from(O.OracleBrain(1, 1, 1, 1, 1), 1)
+    emu.src, emu.dst, emu.w = [0], [1], [f(0.3)]
+    emu.clock = now
+    emu.lastF = [now, now + 3, 0]
+    emu.one_pass()
+    assert np.float32(emu.w[0]).view(np.uint32) == np.float32(expect).view(np.uint32)
+
+
+def test_read_outputs_and_renorm_use_u32_clock():
+    """read_outputs (brain.cpp:149-154) and the renormalisation test
+    (brain.cpp:127-128) compare u32 values."""
+    ob = O.OracleBrain(1, 2, 0, 1, 1)
+    ob.set_scalars((1 << 32) + 5, 0.0, 0.0, 0)
+    ob.last_fired[:] = [0, 4, (1 << 33) + 4]  # both outputs stamped at (u32) now - 1
+    assert list(ob.read_outputs()) == [True, True]
