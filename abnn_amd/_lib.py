@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ABNN_LIB") or os.path.join(_HERE, "libabnn_hip.so")
 
 SUMMARY_WORDS = 4
+COMM_ID_BYTES = 128
 
 
 class Dims(C.Structure):
@@ -175,6 +176,11 @@ SIGNATURES = [
     ("abnn_traversal_workspace_bytes", C.c_uint64, [_U32, _U32]),
     ("abnn_launch_traversal", C.c_int, [C.POINTER(TraversalArgs), _VP]),
     ("abnn_launch_renormalise", C.c_int, [_VP, _VP, _VP, _U32, _VP]),
+    ("abnn_comm_unique_id", C.c_int, [_VP]),
+    ("abnn_comm_create", C.c_int, [_VP, _U32, _U32, C.c_int, C.POINTER(_VP)]),
+    ("abnn_comm_destroy", C.c_int, [_VP]),
+    ("abnn_shard_traverse", C.c_int, [_VP, _VP, _U32, _VP]),
+    ("abnn_comm_sync_visits", C.c_int, [_VP, _VP, _VP]),
     ("abnn_get_stats", C.c_int, [_VP, C.POINTER(Stats)]),
     ("abnn_reset_stats", C.c_int, [_VP]),
     ("abnn_enable_timing", C.c_int, [_VP, C.c_int]),

@@ -31,7 +31,20 @@ ENGINE_HOST_BIN = os.path.join(ROOT, "tests", "cpp", "engine_host_test")
 
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-             "-ffp-contract=off", "-Wall", "-Werror=return-type"]
+             "-ffp-contract=off", "-Wall", "-Werror=return-type", "-ldl"]
+
+
+def kernel_source_sha() -> str:
+    """sha256 (16 hex) of the HIP library's sources: ties a committed
+    measurement (profiles/traffic_*.json) to the kernels it was taken on."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in sorted(HIP_DEPS):
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def _stale(target: str, deps: list[str]) -> bool:

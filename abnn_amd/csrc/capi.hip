@@ -1,6 +1,10 @@
 // capi.hip -- implementation of the C-ABI (include/abnn/abnn.h) over the HIP
 // kernels of kernels.hip.  Replaces the Metal host class Brain
 // (abnn/src/core/brain/brain.{h,cpp}); each function cites what it replaces.
+#include <dlfcn.h>
+#include <link.h>
+#include <rccl/rccl.h>  // types only: the entry points are resolved at run time (rccl_api)
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -101,6 +105,9 @@ struct abnn_brain {
     // host-mapped error word: a fused pass whose look-back wait gave up sets it
     // (kernels.hip wg_poll); abnn_traverse sees it without synchronising
     uint32_t* err_host = nullptr;
+    // a sharded pass on the fused path: its first launch (k_gate in shard
+    // mode) ran, k_shard_walk follows the exchange (abnn_shard_apply)
+    bool pending_walk = false;
 };
 
 namespace {
@@ -488,10 +495,20 @@ void plan_build(abnn_brain* b)
     }
 }
 
+// A sharded pass takes the fused path (two launches around the exchange:
+// k_gate in shard mode, k_shard_walk) where a single-GPU pass would.
+bool shard_fused(const abnn_brain* b)
+{
+    return b->use_fused && fused_pass_supported(b->d) && b->d.gate_block == 1024;
+}
+
+abnn_status run_shard_fused_gate(abnn_brain* b, int32_t* xchg, hipStream_t s);
+
 // bitmap + streaming gate (with the refractory stage) [+ the exchange record
 // of a sharded pass]: the first half of every pass.
 abnn_status run_gate(abnn_brain* b, int32_t* xchg_out, hipStream_t s)
 {
+    if (xchg_out && shard_fused(b)) return run_shard_fused_gate(b, xchg_out, s);
     ST_TRY(pass_buffers(b, s));
     b->last_pass_fused = false;
     EventPair* ev = nullptr;
@@ -518,6 +535,15 @@ void rotate_bounds(abnn_brain* b)
 abnn_status run_apply(abnn_brain* b, const int32_t* gathered, uint32_t world, uint32_t rank, hipStream_t s)
 {
     DeviceState& d = b->d;
+    if (b->pending_walk) {  // the sharded fused pass's second launch
+        b->pending_walk = false;
+        HIP_TRY(launch_shard_walk(d, b->kp, gathered, world, rank, s));
+        b->next_built = d.build_next != 0;
+        b->built_stim[0] = b->stim_first;
+        b->built_stim[1] = b->stim_count;
+        rotate_bounds(b);
+        return ABNN_OK;
+    }
     plan_build(b);
     HIP_TRY(launch_apply(d, b->kp, gathered, world, rank, s));
     b->next_built = d.build_next != 0;
@@ -552,6 +578,33 @@ abnn_status run_fused(abnn_brain* b, hipStream_t s)
     return ABNN_OK;
 }
 
+// The first launch of a sharded pass on the fused path: gate, refractory
+// stage, look-back over this shard's workgroups with local budget positions,
+// this shard's exchange record (kernels.hip fused_end, shard mode).  Like
+// run_fused, but the walk, the stamps and the pass end wait for the exchange.
+abnn_status run_shard_fused_gate(abnn_brain* b, int32_t* xchg, hipStream_t s)
+{
+    DeviceState& d = b->d;
+    ST_TRY(pass_buffers(b, s));
+    plan_build(b);
+    d.prologue_adapt = b->last_pass_fused && d.adapt_ranges ? 1u : 0u;
+    d.cost_in = b->cost_buf[b->cost_parity ^ 1u];
+    d.cost_out = b->cost_buf[b->cost_parity];
+    d.shard_mode = 1;
+    d.xchg = xchg;
+    EventPair* ev = nullptr;
+    ST_TRY(time_begin(b, s, &ev));
+    const hipError_t e = launch_fused_pass(d, b->kp, s);
+    d.shard_mode = 0;
+    d.xchg = nullptr;
+    HIP_TRY(e);
+    if (ev) HIP_TRY(hipEventRecord(ev->b, s));
+    b->cost_parity ^= 1u;
+    b->last_pass_fused = true;
+    b->pending_walk = true;
+    return ABNN_OK;
+}
+
 abnn_status run_commit(abnn_brain* b, const int32_t* gathered, uint32_t world, bool renorm,
                        hipStream_t s)
 {
@@ -573,6 +626,59 @@ abnn_status run_commit(abnn_brain* b, const int32_t* gathered, uint32_t world, b
     if (ce != 0 && b->pass_host % ce == 0) ST_TRY(structural_update(b));  // README §5
     return ABNN_OK;
 }
+
+// RCCL entry points, resolved once: the librccl already loaded in the process
+// (torch's, when the caller imported it: one RCCL per process), else the
+// system's librccl.so.1.
+struct RcclApi {
+    ncclResult_t (*get_unique_id)(ncclUniqueId*);
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+    ncclResult_t (*comm_destroy)(ncclComm_t);
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+    const char* (*error_string)(ncclResult_t);
+    bool ok;
+};
+
+int find_loaded_rccl(struct dl_phdr_info* info, size_t, void* out)
+{
+    if (info->dlpi_name && std::strstr(info->dlpi_name, "librccl.so")) {
+        *static_cast<std::string*>(out) = info->dlpi_name;
+        return 1;
+    }
+    return 0;
+}
+
+const RcclApi& rccl_api()
+{
+    static RcclApi api = [] {
+        RcclApi a{};
+        std::string loaded;
+        dl_iterate_phdr(find_loaded_rccl, &loaded);
+        void* h = loaded.empty() ? nullptr : dlopen(loaded.c_str(), RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return a;
+        a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        a.comm_init_rank = reinterpret_cast<decltype(a.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        a.all_gather = reinterpret_cast<decltype(a.all_gather)>(dlsym(h, "ncclAllGather"));
+        a.all_reduce = reinterpret_cast<decltype(a.all_reduce)>(dlsym(h, "ncclAllReduce"));
+        a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
+        a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_gather && a.all_reduce && a.error_string;
+        return a;
+    }();
+    return api;
+}
+
+#define RCCL_TRY(expr)                                                                 \
+    do {                                                                               \
+        ncclResult_t _r = (expr);                                                      \
+        if (_r != ncclSuccess) {                                                       \
+            set_err(std::string(#expr) + ": " + rccl_api().error_string(_r));          \
+            return ABNN_ERR_HIP;                                                       \
+        }                                                                              \
+    } while (0)
 
 // Chunked host<->device copies for the file formats.
 constexpr uint64_t kIoRecs = 1u << 22;  // 4M records (64 MiB) per piece
@@ -1143,6 +1249,121 @@ abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t 
     const bool renorm = b->pending_renorm;
     b->pending_renorm = false;
     return run_commit(b, static_cast<const int32_t*>(gathered_dev), world, renorm, s);
+}
+
+// ---- sharded passes over RCCL ------------------------------------------------
+
+struct abnn_comm {
+    ncclComm_t comm = nullptr;
+    uint32_t world = 1, rank = 0;
+    int device = 0;
+    char* gathered = nullptr;   // world exchange records, rank order
+    uint64_t rec_bytes = 0;
+    uint64_t* scratch = nullptr;  // visited-events all-reduce
+};
+
+abnn_status abnn_comm_unique_id(void* id_out)
+{
+    REQUIRE(id_out, "null argument");
+    const RcclApi& r = rccl_api();
+    if (!r.ok) {
+        set_err("RCCL (librccl) not found");
+        return ABNN_ERR_NO_DEVICE;
+    }
+    ncclUniqueId id;
+    RCCL_TRY(r.get_unique_id(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+    return ABNN_OK;
+}
+
+abnn_status abnn_comm_create(const void* id, uint32_t world, uint32_t rank, int device, abnn_comm** out)
+{
+    REQUIRE(id && out && world >= 1 && rank < world, "bad argument");
+    static_assert(sizeof(ncclUniqueId) == ABNN_COMM_ID_BYTES, "unique id size");
+    *out = nullptr;
+    const RcclApi& r = rccl_api();
+    if (!r.ok) {
+        set_err("RCCL (librccl) not found");
+        return ABNN_ERR_NO_DEVICE;
+    }
+    HIP_TRY(hipSetDevice(device));
+    abnn_comm* c = new (std::nothrow) abnn_comm();
+    if (!c) return ABNN_ERR_OOM;
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    const ncclResult_t e = r.comm_init_rank(&c->comm, (int)world, uid, (int)rank);
+    if (e != ncclSuccess) {
+        set_err(std::string("ncclCommInitRank: ") + r.error_string(e));
+        delete c;
+        return ABNN_ERR_HIP;
+    }
+    c->world = world;
+    c->rank = rank;
+    c->device = device;
+    if (dalloc(&c->scratch, 1) != ABNN_OK) {
+        abnn_comm_destroy(c);
+        return ABNN_ERR_OOM;
+    }
+    *out = c;
+    return ABNN_OK;
+}
+
+abnn_status abnn_comm_destroy(abnn_comm* c)
+{
+    if (!c) return ABNN_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    if (c->comm) rccl_api().comm_destroy(c->comm);
+    if (c->gathered) (void)hipFree(c->gathered);
+    if (c->scratch) (void)hipFree(c->scratch);
+    delete c;
+    return ABNN_OK;
+}
+
+abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, void* stream)
+{
+    REQUIRE(b && c, "null argument");
+    REQUIRE(c->device == b->device, "communicator and handle are on different devices");
+    ST_TRY(pass_error(b));
+    HIP_TRY(hipSetDevice(b->device));
+    const RcclApi& r = rccl_api();
+    hipStream_t s = pick(b, stream);
+    const uint64_t rec = abnn_exchange_bytes(b);
+    if (rec != c->rec_bytes) {  // the records' size follows the budget: sized on first use
+        if (c->gathered) HIP_TRY(hipFree(c->gathered));
+        c->gathered = nullptr;
+        ST_TRY(dalloc(&c->gathered, rec * c->world));
+        c->rec_bytes = rec;
+    }
+    char* mine = c->gathered + rec * c->rank;
+    for (uint32_t i = 0; i < passes; ++i) {
+        ST_TRY(abnn_shard_gate(b, mine, s));
+        RCCL_TRY(r.all_gather(mine, c->gathered, rec, ncclInt8, c->comm, s));  // in place, rank order
+        ST_TRY(abnn_shard_apply(b, c->gathered, c->world, c->rank, s));
+        const uint64_t updates = b->structural_updates;
+        ST_TRY(abnn_shard_commit(b, c->gathered, c->world, s));
+        if (b->structural_updates != updates) {
+            // every shard's record count changed (all ranks update after the
+            // same pass): re-sum the visited events for the clock-tick rule
+            uint64_t mine_ev = visited_events(b->dims, b->params.mode), tot = 0;
+            HIP_TRY(hipMemcpyAsync(c->scratch, &mine_ev, 8, hipMemcpyHostToDevice, s));
+            RCCL_TRY(r.all_reduce(c->scratch, c->scratch, 1, ncclUint64, ncclSum, c->comm, s));
+            HIP_TRY(hipMemcpyAsync(&tot, c->scratch, 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            b->dims.global_events = tot;
+        }
+    }
+    return ABNN_OK;
+}
+
+abnn_status abnn_comm_sync_visits(abnn_brain* b, abnn_comm* c, void* stream)
+{
+    REQUIRE(b && c, "null argument");
+    ST_TRY(sync_all(b));
+    hipStream_t s = pick(b, stream);
+    RCCL_TRY(rccl_api().all_reduce(b->d.last_visited, b->d.last_visited, b->n_nrn, ncclUint64, ncclMax, c->comm, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return ABNN_OK;
 }
 
 // Diagnostics (not part of abnn.h): the last pass's per-wave gate times,

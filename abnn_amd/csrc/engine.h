@@ -38,7 +38,8 @@ struct alignas(16) PassWork {
     uint32_t epoch;        // fused passes run so far: tags this pass's look-back words (never set by the host)
     uint32_t error;        // unused (the error word is host-mapped: DeviceState::err_word)
     uint32_t spec_wgs;     // fused pass: gate workgroups predicted below the budget cut (the last pass's, less one)
-    uint32_t pad[3];
+    uint32_t pad;
+    unsigned long long shard_g2;  // sharded fused pass: refractory survivors of the shard (the summary's word 3)
     abnn_stats stats;      // host-kept counters (grown); the device ones live in DeviceState::wg_stats
 };
 
@@ -164,6 +165,8 @@ struct DeviceState {
                               // (<= kChunk; ABNN_FLUSH_AT)
     uint32_t spec_mode;       // fused: speculative weight stores 0 off, 1 below the predicted cut (default),
                               // 2 everywhere (ABNN_SPEC; 2 exercises the restore path)
+    uint32_t shard_mode;      // fused pass = the first launch of a sharded pass (k_gate: no stamps, exchange record)
+    int32_t* xchg;            // ... its exchange record (abnn.h: summary + local spike list)
     uint32_t prologue_adapt;  // the previous pass was fused over the same ranges: its costs move the next
                               // pass's partition (computed in this one's prologue)
     uint64_t n_syn;           // local records
@@ -222,6 +225,12 @@ bool fused_pass_supported(const DeviceState& d);
 // Resident fused-pass workgroups per CU (occupancy API; 0 on failure or an uncompiled shape).
 int fused_blocks_per_cu(uint32_t block, uint32_t k, uint32_t filter_words, bool track);
 hipError_t launch_fused_pass(const DeviceState& d, const KernelParams& kp, hipStream_t s);
+// Sharded passes on the fused path: the first launch is launch_fused_pass with
+// d.shard_mode = 1 (writes d.xchg); after the all-gather, this one walks every
+// range from its global budget position, stamps every rank's spikes and ends
+// the pass.
+hipError_t launch_shard_walk(const DeviceState& d, const KernelParams& kp, const int32_t* gathered, uint32_t world,
+                             uint32_t rank, hipStream_t s);
 // Sharded passes: this shard's exchange record (summary + local spike list).
 hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out, hipStream_t s);
 // The rest of the pass: budget walk, weight update, stamps and, in its last

@@ -735,79 +735,19 @@ __device__ void fused_next_bounds(const DeviceState& d, uint32_t* cc)
     if (mine) d.range_bounds_next[k] = adapted_bound(d, cc, d.range_bounds_prev, NR, k, total, d.range_bounds[k]);
 }
 
-// LDS of the fused pass's end (per workgroup).
-template <int NW>
-struct FusedLds {
-    uint64_t setc[kSetCache];          // wave_set_next_dedup's cache
-    alignas(16) uint32_t cc[kFusedMaxRanges + 4];  // fused_next_bounds: the previous pass's range costs
-                                                   // (LDS-DMA in the prologue), scanned in place
-    uint32_t cand[NW];                 // spike candidates of each wave's range (capped at the budget)
-    uint32_t stat[5];                  // pre-gated, survivors, updated, fired, pruned
-    uint32_t excl;                     // candidates of all lower workgroups (capped)
-    uint32_t done;                     // waves through their refractory stage
-    uint32_t total;                    // candidates of the pass (capped; workgroup 0)
-};
-
-// Fused pass: range r's wave after its refractory stage (g1 pre-gated, S
-// survivors -- contiguous from g2x[region] -- and C spike candidates; its
-// stream took `stream_cost` 40-ns units, the next pass's partition cost): the
-// next partition (first wave of the workgroup), its share of the next bitmap
-// build, the workgroup look-back, the walk of its own survivors, statistics,
-// the stamps of the workgroup's spikes once every refractory stage of the
-// pass is done, and (workgroup 0) the pass's end.  Pass-start scalars (C1) as
-// read at kernel entry.
-template <int BLOCK, int NW>
-__device__ __forceinline__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region, uint32_t g1,
-                          uint32_t S, uint32_t C, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
-                          float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L, uint64_t t_stream)
+// The walk of one range's survivors (the fused pass's g2x entries, contiguous
+// from g2x[region]; C of them spike candidates) in event order from budget
+// position P: the ordered budget of C1 (brain.metal:85-98), the weight update
+// (brain.metal:101-122; stored by refrac_chunk already when spec) and the
+// spikes (brain.metal:125-126: spike list, synaptogenesis; set_next: into the
+// next pass's bitmap).  Returns the survivors below the budget that were
+// stored by refrac_chunk and not visited (wave-uniform); ac counts the rest.
+__device__ __forceinline__ uint32_t range_walk(const DeviceState& d, const KernelParams& kp, ApplyCtx& ac, uint32_t r,
+                                               uint64_t region, uint32_t S, uint32_t C, uint64_t P, bool spec,
+                                               bool set_next, uint64_t* setc)
 {
     constexpr uint32_t RW = 4;  // rounds of survivors per walk batch (two batches in flight)
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
-    const uint32_t tag = epoch + 1u;
-    const uint64_t t_tail = __builtin_amdgcn_s_memrealtime();
-    uint32_t order = 0;
-    if (lane == 0) {
-        L.cand[wid] = C < budget ? C : budget;
-        const uint32_t cost = stream_cost;
-        d.cost_out[r] = empty ? 0u : (cost < 1 ? 1u : (cost > 0xFFFFu ? 0xFFFFu : cost));
-        order = atomicAdd(&L.done, 1u);
-    }
-    if (wave_uniform(order) == 0) fused_next_bounds<NW>(d, L.cc);
-    // this wave's share of the next pass's bitmap build that does not depend
-    // on this pass (the spike lists of passes p+1-W..p-1, the stimulus): it
-    // fills the wait for the workgroup's other ranges
-    if (d.build_next) {
-        const uint64_t nitems = next_items(d, kp), step = (uint64_t)d.n_ranges * 64;
-        for (uint64_t x0 = (uint64_t)r * 64; x0 < nitems; x0 += step) {  // wave-uniform
-            const uint64_t x = x0 + lane;
-            const NextItem it = x < nitems ? next_item_load(d, kp, pass, x) : NextItem{0u, 0u, 0u};
-            wave_set_next_dedup(d, it.i < it.lim, it.n, L.setc);
-        }
-    }
-    lds_barrier();  // every range of the workgroup through its refractory stage
-    uint32_t vals[kLbMaxWords];
-    if (wid == 0) {
-        uint32_t c = lane < (uint32_t)NW ? L.cand[lane] : 0u;
-        c = wave_sum(c);
-        if (lane == 0)
-            __hip_atomic_store((gu64*)(d.lb_status + blockIdx.x),
-                               (uint64_t)tag << 32 | (uint64_t)kLbAggregate << 30 | (c < budget ? c : budget),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t e = wg_poll(d, blockIdx.x, tag, budget, true, vals);
-        if (lane == 0) L.excl = e;
-    }
-    lds_barrier();
-    const uint32_t excl_wg = L.excl;
-    uint64_t P = excl_wg;
-    uint64_t c_wg = 0;  // the workgroup's candidates
-    for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
-        if (w < wid) P += L.cand[w];
-        c_wg += L.cand[w];
-    }
-    const uint64_t t_lb = __builtin_amdgcn_s_memrealtime();
-    // the budget walk of k_apply over this range alone, in event order
-    ApplyCtx ac{R, rb, now, pass, false, false, true, false, kp.w_prune > 0.0f, d.grown != nullptr && kp.p_new > 0.0f,
-                true, 0u, 0u, 0u};
+    const uint32_t lane = threadIdx.x & 63, budget = kp.max_spikes;
     // batches of RW x 64 survivors; the next batch's loads are issued before
     // this one's stores (gfx9's vmcnt also counts stores: a load issued after
     // them would wait for them)
@@ -839,7 +779,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
             const uint32_t i = i0 + lane;
             const uint2 c = i < nb ? cl[i] : make_uint2(0u, 0xFFFFFFFFu);
             if (i < nb) record_spike(d, kp, ac, make_uint4(0u, 0u, 0u, c.y), P + i, region + c.x);
-            if (d.build_next) wave_set_next_dedup(d, i < nb, c.y, L.setc);  // this pass's spikes
+            if (set_next) wave_set_next_dedup(d, i < nb, c.y, setc);  // this pass's spikes
         }
         // survivors below the budget: all, or through the k-th candidate
         upd_rest = C < k ? S : wave_uniform(cl[k - 1].x) + 1u;
@@ -876,12 +816,146 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
             } else if (v) {  // mispredicted: past the budget, w stays (brain.metal:85-88)
                 __builtin_nontemporal_store(__uint_as_float(x.y), w_ptr(d.syn, region + x.x));
             }
-            if (d.build_next) wave_set_next_dedup(d, cand && pre < budget, x.w, L.setc);  // this pass's spikes
+            if (set_next) wave_set_next_dedup(d, cand && pre < budget, x.w, setc);  // this pass's spikes
             P += (uint64_t)__popcll(bc);
             seen += (uint32_t)__popcll(bc);
         }
 #pragma unroll
         for (uint32_t j = 0; j < RW; ++j) e[j] = en[j];
+    }
+    return upd_rest;
+}
+
+// Sharded pass, first launch: the dst of this range's spike candidates whose
+// LOCAL budget position P + i is below the budget, in that order, into the
+// exchange record's spike list (the lower ranks' offset is added by every
+// rank when it stamps: stamp_gathered).  From cand_list when the range listed
+// all its candidates, else by a walk of its survivors.
+__device__ __forceinline__ void range_spikes_local(const DeviceState& d, const KernelParams& kp, uint32_t r,
+                                                   uint64_t region, uint32_t S, uint32_t C, uint64_t P, int32_t* spikes)
+{
+    constexpr uint32_t RW = 4;
+    const uint32_t lane = threadIdx.x & 63, budget = kp.max_spikes;
+    if (P >= budget || C == 0) return;
+    if (C <= kCandCap) {
+        const uint32_t k = (uint32_t)(budget - P), nb = C < k ? C : k;
+        const uint2* cl = d.cand_list + (uint64_t)r * kCandCap;
+        for (uint32_t i = lane; i < nb; i += 64) spikes[P + i] = (int32_t)cl[i].y;
+        return;
+    }
+    for (uint32_t b0 = 0; b0 < S && P < budget; b0 += RW * 64) {  // wave-uniform
+        uint4 e[RW];
+#pragma unroll
+        for (uint32_t j = 0; j < RW; ++j) {
+            const uint32_t q = b0 + j * 64 + lane;
+            e[j] = q < S ? d.g2x[region + q] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < RW; ++j) {
+            const bool cand = b0 + j * 64 + lane < S && (e[j].x >> 31);
+            const uint64_t bc = __ballot(cand);
+            const uint64_t pre = P + mbcnt64(bc);
+            if (cand && pre < budget) spikes[pre] = (int32_t)e[j].w;
+            P += (uint64_t)__popcll(bc);
+        }
+    }
+}
+
+// LDS of the fused pass's end (per workgroup).
+template <int NW>
+struct FusedLds {
+    uint64_t setc[kSetCache];          // wave_set_next_dedup's cache
+    alignas(16) uint32_t cc[kFusedMaxRanges + 4];  // fused_next_bounds: the previous pass's range costs
+                                                   // (LDS-DMA in the prologue), scanned in place
+    uint32_t cand[NW];                 // spike candidates of each wave's range (capped at the budget)
+    uint32_t stat[5];                  // pre-gated, survivors, updated, fired, pruned
+    uint32_t excl;                     // candidates of all lower workgroups (capped)
+    uint32_t done;                     // waves through their refractory stage
+    uint32_t total;                    // candidates of the pass (capped; workgroup 0)
+    uint32_t sg2;                      // sharded pass: the workgroup's refractory survivors
+};
+
+// Fused pass: range r's wave after its refractory stage (g1 pre-gated, S
+// survivors -- contiguous from g2x[region] -- and C spike candidates; its
+// stream took `stream_cost` 40-ns units, the next pass's partition cost): the
+// next partition (first wave of the workgroup), its share of the next bitmap
+// build, the workgroup look-back, the walk of its own survivors, statistics,
+// the stamps of the workgroup's spikes once every refractory stage of the
+// pass is done, and (workgroup 0) the pass's end.  Pass-start scalars (C1) as
+// read at kernel entry.
+template <int BLOCK, int NW>
+__device__ __forceinline__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region, uint32_t g1,
+                          uint32_t S, uint32_t C, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
+                          float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L, uint64_t t_stream)
+{
+    constexpr uint32_t RW = 4;  // rounds of survivors per walk batch (two batches in flight)
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
+    const uint32_t tag = epoch + 1u;
+    const uint64_t t_tail = __builtin_amdgcn_s_memrealtime();
+    uint32_t order = 0;
+    if (lane == 0) {
+        L.cand[wid] = C < budget ? C : budget;
+        if (d.shard_mode) atomicAdd(&L.sg2, S);
+        const uint32_t cost = stream_cost;
+        d.cost_out[r] = empty ? 0u : (cost < 1 ? 1u : (cost > 0xFFFFu ? 0xFFFFu : cost));
+        order = atomicAdd(&L.done, 1u);
+    }
+    if (wave_uniform(order) == 0) fused_next_bounds<NW>(d, L.cc);
+    // this wave's share of the next pass's bitmap build that does not depend
+    // on this pass (the spike lists of passes p+1-W..p-1, the stimulus): it
+    // fills the wait for the workgroup's other ranges
+    if (d.build_next) {
+        const uint64_t nitems = next_items(d, kp), step = (uint64_t)d.n_ranges * 64;
+        for (uint64_t x0 = (uint64_t)r * 64; x0 < nitems; x0 += step) {  // wave-uniform
+            const uint64_t x = x0 + lane;
+            const NextItem it = x < nitems ? next_item_load(d, kp, pass, x) : NextItem{0u, 0u, 0u};
+            wave_set_next_dedup(d, it.i < it.lim, it.n, L.setc);
+        }
+    }
+    lds_barrier();  // every range of the workgroup through its refractory stage
+    uint32_t vals[kLbMaxWords];
+    if (wid == 0) {
+        uint32_t c = lane < (uint32_t)NW ? L.cand[lane] : 0u;
+        c = wave_sum(c);
+        if (lane == 0 && d.shard_mode) {
+            // the pass's refractory survivors for the exchange summary: added
+            // before this workgroup's word is published (workgroup 0 sums
+            // them once every word is)
+            __hip_atomic_fetch_add(&d.work->shard_g2, (unsigned long long)L.sg2, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (lane == 0)
+            __hip_atomic_store((gu64*)(d.lb_status + blockIdx.x),
+                               (uint64_t)tag << 32 | (uint64_t)kLbAggregate << 30 | (c < budget ? c : budget),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t e = wg_poll(d, blockIdx.x, tag, budget, true, vals);
+        if (lane == 0) L.excl = e;
+    }
+    lds_barrier();
+    const uint32_t excl_wg = L.excl;
+    uint64_t P = excl_wg;
+    uint64_t c_wg = 0;  // the workgroup's candidates
+    for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
+        if (w < wid) P += L.cand[w];
+        c_wg += L.cand[w];
+    }
+    const uint64_t t_lb = __builtin_amdgcn_s_memrealtime();
+    // the budget walk of k_apply over this range alone, in event order
+    ApplyCtx ac{R, rb, now, pass, false, false, true, false, kp.w_prune > 0.0f, d.grown != nullptr && kp.p_new > 0.0f,
+                true, 0u, 0u, 0u};
+    uint32_t upd_rest = 0;
+    if (!d.shard_mode) {
+        upd_rest = range_walk(d, kp, ac, r, region, S, C, P, spec, d.build_next != 0, L.setc);
+    } else {
+        // sharded pass (the first of its two launches): the global budget
+        // offset is unknown until the exchange, so this range's local budget
+        // position, survivors and candidates go to range_info for
+        // k_shard_walk, and its candidates below the budget (local order)
+        // into the exchange record's spike list (abnn.h)
+        if (lane == 0)
+            d.range_info[r] = make_uint4((uint32_t)(P < budget ? P : budget), S, C, (spec ? 1u : 0u) | (empty ? 2u : 0u));
+        range_spikes_local(d, kp, r, region, S, C, P, d.xchg + 2 * ABNN_SUMMARY_WORDS);
     }
     const uint64_t t_walk = __builtin_amdgcn_s_memrealtime();
     const uint32_t wu = wave_sum(ac.upd) + upd_rest, wf = wave_sum(ac.nf), wp = wave_sum(ac.npr);
@@ -919,6 +993,23 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
             atomicAdd((ull*)&st->passes, 1ull);
             atomicAdd((ull*)&st->events, (ull)d.events);
         }
+    }
+    if (d.shard_mode) {
+        // sharded pass: no stamps, no pass end here (k_shard_walk, after the
+        // exchange); workgroup 0 writes the exchange summary (abnn.h) once
+        // every word is published
+        if (!first || wid != 0) return;
+        const uint32_t tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
+        if (lane == 0) {
+            int64_t* sm = reinterpret_cast<int64_t*>(d.xchg);
+            sm[0] = (int64_t)tot;  // candidates, capped at the budget
+            sm[1] = (int64_t)__hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sm[2] = (int64_t)d.events;
+            sm[3] = (int64_t)__hip_atomic_load(&d.work->shard_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            d.work->shard_g2 = 0;
+            d.work->epoch = epoch + 1u;
+        }
+        return;
     }
     if (s1 <= s0 && !first) return;  // workgroup-uniform: nothing to stamp
     // every workgroup's word published = every refractory stage of the pass
@@ -1120,6 +1211,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         if constexpr (kFused) {
             if (tid < 5) s_fz.stat[tid] = 0u;
             if (tid == 0) s_fz.done = 0u;
+            if (tid == 0) s_fz.sg2 = 0u;
             if (tid < kSetCache) s_fz.setc[tid] = ~0ull;
         }
     }
@@ -1843,6 +1935,81 @@ __global__ __launch_bounds__(kApplyThreads) void k_apply(DeviceState d, KernelPa
 }
 
 // ---------------------------------------------------------------------------
+// k_shard_walk: the second launch of a sharded pass on the fused path (the
+// first is k_gate<..., kFused> in shard mode, then the all-gather).  One wave
+// per range, as in the gate: the range's global budget position = the lower
+// ranks' capped candidates (rank_offset) + its local position (range_info,
+// written by the first launch); the walk of its survivors (range_walk: weight
+// updates below the budget or the restore of mispredicted speculative stores,
+// synaptogenesis at the global slot); every rank's spikes stamped from the
+// gathered records in global budget order (stamp_gathered: no lastFired read
+// is left in the pass) and set into the next pass's bitmap; the last
+// workgroup ends the pass (finalize_pass) and predicts the next pass's
+// speculative workgroups from the global cut.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_shard_walk(DeviceState d, KernelParams kp, const int32_t* gathered,
+                                                        uint32_t world, uint32_t rank)
+{
+    __shared__ uint64_t s_setc[1];
+    __shared__ uint32_t s_stat[3];
+    __shared__ uint64_t s_now, s_pass;
+    __shared__ float s_R, s_rb;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
+    if (threadIdx.x == 0) {  // pass-start scalars (C1): the last workgroup rewrites them
+        s_R = *d.reward;
+        s_rb = *d.rbar;
+        s_now = *d.clock;
+        s_pass = *d.pass_index;
+    }
+    if (threadIdx.x < 3) s_stat[threadIdx.x] = 0u;
+    __syncthreads();
+    const float R = s_R, rb = s_rb;
+    const uint64_t now = s_now, pass = s_pass;
+    const uint64_t off = rank_offset(kp, gathered, rank);
+    const uint32_t r = blockIdx.x * NW + wid;
+    const uint4 ri = d.range_info[r];  // {local budget position (capped), survivors, candidates, spec | empty << 1}
+    const uint64_t P = off + ri.x, region = (uint64_t)d.range_bounds[r] * d.iter_events;
+    const bool spec = ri.w & 1u;
+    ApplyCtx ac{R, rb, now, pass, false, false, false, false, kp.w_prune > 0.0f, d.grown != nullptr && kp.p_new > 0.0f,
+                true, 0u, 0u, 0u};
+    const uint32_t upd_rest = range_walk(d, kp, ac, r, region, ri.y, ri.z, P, spec, false, s_setc);
+    // the next pass's spec prediction: the workgroup holding the global cut
+    // (its first range's position below the budget, its last range's end at
+    // or past it) names the ones below it, less one, as the fused pass does
+    if (wid == NW - 1 && lane == 0) {
+        const uint4 r0 = d.range_info[blockIdx.x * NW];
+        if (off + r0.x < budget && P + ri.z >= budget)
+            d.work->spec_wgs = blockIdx.x > 0 ? blockIdx.x - 1 : 0u;
+    }
+    const uint32_t wu = wave_sum(ac.upd) + upd_rest, wf = wave_sum(ac.nf), wp = wave_sum(ac.npr);
+    if (lane == 0) {
+        atomicAdd(&s_stat[0], wu);
+        atomicAdd(&s_stat[1], wf);
+        atomicAdd(&s_stat[2], wp);
+    }
+    // every rank's spikes (global budget order) and, in steady state, into
+    // the next pass's bitmap
+    const uint64_t nsp = stamp_gathered(d, kp, gathered, world, now, pass);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        typedef unsigned long long ull;
+        abnn_stats* st = d.wg_stats + blockIdx.x % kWalkBlocks;
+        if (s_stat[0]) atomicAdd((ull*)&st->updated, (ull)s_stat[0]);
+        if (s_stat[1]) atomicAdd((ull*)&st->fired, (ull)s_stat[1]);
+        if (s_stat[2]) atomicAdd((ull*)&st->pruned, (ull)s_stat[2]);
+        if (blockIdx.x == 0) d.n_fired_ring[pass & (kFiredRing - 1)] = (uint32_t)nsp;
+        const uint32_t ticket = __hip_atomic_fetch_add((gu32*)(&d.work->ticket), 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        if (ticket == gridDim.x - 1) {
+            const int64_t mine = *reinterpret_cast<const int64_t*>(gathered + rank * xchg_words(kp.max_spikes));
+            if (off >= budget) d.work->spec_wgs = 0u;                        // the whole shard past the cut
+            else if (off + (uint64_t)mine < budget) d.work->spec_wgs = gridDim.x;  // ... below it
+            finalize_pass(d, kp, gathered, world, now, R, rb, pass);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_renorm: brain.metal:135-145; base (= the ticked clock) passed by the host.
 __global__ __launch_bounds__(256) void k_renorm(DeviceState d, uint64_t base)
 {
@@ -2110,6 +2277,14 @@ hipError_t launch_fused_pass(const DeviceState& d, const KernelParams& kp, hipSt
 #undef X
     }
     return hipErrorInvalidValue;
+}
+
+hipError_t launch_shard_walk(const DeviceState& d, const KernelParams& kp, const int32_t* gathered, uint32_t world,
+                             uint32_t rank, hipStream_t s)
+{
+    if (d.gate_block != 1024) return hipErrorInvalidValue;  // one wave per range of the 1024-thread fused gate
+    hipLaunchKernelGGL(k_shard_walk<16>, dim3(d.gate_blocks), dim3(1024), 0, s, d, kp, gathered, world, rank);
+    return hipGetLastError();
 }
 
 hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xchg_out, hipStream_t s)

@@ -111,12 +111,57 @@ class _GpuEngine:
         self.brain.shard_commit(gathered.data_ptr(), world, self._stream())
 
 
+class NativeComm:
+    """The library's own RCCL communicator (abnn_comm, include/abnn/abnn.h):
+    rank 0's unique id is broadcast over ``torch.distributed`` once, then
+    every pass's all-gather is enqueued by the C-ABI itself
+    (abnn_shard_traverse) -- no Python, no torch collective per pass."""
+
+    def __init__(self, device: int, group=None):
+        import ctypes as C
+
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib
+
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        uid = np.zeros(_lib.COMM_ID_BYTES, dtype=np.uint8)
+        if self.rank == 0:
+            _lib.call("abnn_comm_unique_id", uid.ctypes.data)
+        on_gpu = dist.get_backend(group) == "nccl"
+        t = torch.from_numpy(uid).to(torch.device("cuda", device) if on_gpu else "cpu")
+        dist.broadcast(t, 0, group=group)
+        uid = np.ascontiguousarray(t.cpu().numpy())
+        h = C.c_void_p()
+        _lib.call("abnn_comm_create", uid.ctypes.data, self.world, self.rank, int(device), C.byref(h))
+        self.handle = h
+
+    def close(self) -> None:
+        from . import _lib
+
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            _lib.call("abnn_comm_destroy", self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ShardedBrain:
-    """The rank-local shard of a graph of ``n_syn_global`` synapses on GPU ``device``."""
+    """The rank-local shard of a graph of ``n_syn_global`` synapses on GPU ``device``.
+
+    native=True (one GPU per rank, RCCL): passes are driven by the C-ABI over
+    the library's RCCL communicator (NativeComm, abnn_shard_traverse); False:
+    phase by phase from Python around ``comm.all_gather`` (any backend; the
+    gloo rehearsal of ranks that share a GPU)."""
 
     def __init__(self, comm, n_input: int, n_output: int, n_hidden: int, n_syn_global: int,
                  events_per_pass: int, *, device: int = 0, capacity_factor: float = 1.0,
-                 **param_overrides):
+                 native: bool = False, **param_overrides):
         import torch
 
         self.comm = comm
@@ -138,8 +183,15 @@ class ShardedBrain:
         self.engine = _GpuEngine(self.brain, lambda: torch.cuda.current_stream(dev))
         self.compact_every = int(self.brain.params.compact_every)
         self._updates = self.brain.structural_updates()
+        self.native = NativeComm(device) if native else None
 
     def step(self, passes: int = 1) -> None:
+        if self.native is not None:
+            from ._lib import call
+
+            call("abnn_shard_traverse", self.brain._h, self.native.handle, int(passes),
+                 int(self._torch.cuda.current_stream(self.xchg.device).cuda_stream))
+            return
         for _ in range(passes):
             sharded_pass(self.engine, self.comm, self.xchg, self.gathered)
             # every rank runs its structural update after the same pass (the
@@ -162,6 +214,11 @@ class ShardedBrain:
 
     def sync_visits(self) -> None:
         """Lazy all-reduce(MAX) of lastVisited (never read by a decision)."""
+        if self.native is not None:
+            from ._lib import call
+
+            call("abnn_comm_sync_visits", self.brain._h, self.native.handle, None)
+            return
         torch = self._torch
         lv = self.brain.last_visited().view(np.int64)
         t = torch.from_numpy(lv.copy()).to(self.xchg.device)

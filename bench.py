@@ -85,11 +85,12 @@ def algorithmic_bytes(stats: dict, track_visits: bool, random_mode: bool = False
     and the pre-spike gate reads nothing else (+4 B dst read and 8 B
     lastVisited write per event with track_visits).  The pre-spike lookup of
     lastFired[src] is served by the per-pass LDS filter / L2 bitmap, built by
-    k_apply from the last passes' spike lists (k_bitmap, after host writes,
-    reads lastFired once: 8 B per neuron).  Random mode: one u32 src per pick
-    (the src32 mirror)."""
+    the pass from the last passes' spike lists (k_bitmap, after host writes,
+    reads lastFired once: 8 B per neuron).  Random mode: every pick is one
+    random access to the 4-GB src32 mirror, and HBM moves a whole 64-B line
+    for it: 64 B per pick (the 4 useful bytes are 1/16 of that)."""
     e = stats["events"]
-    return (4 if random_mode else 3) * e + (12 * e if track_visits else 0)
+    return (64 if random_mode else 3) * e + (12 * e if track_visits else 0)
 
 
 def survey_bytes(stats: dict, track_visits: bool) -> int:
@@ -100,14 +101,23 @@ def survey_bytes(stats: dict, track_visits: bool) -> int:
 
 
 def load_traffic(config: str):
+    """The committed PMC traffic record (tools/profile.sh -> tools/pmc_summary.py)
+    if it was measured on these kernel sources; else (None, why)."""
+    from abnn_amd.build import kernel_source_sha
+
     p = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
     if not os.path.exists(p):
-        return None
+        return None, "no profiles/traffic_%s.json" % config
     try:
         with open(p) as f:
-            return json.load(f)
-    except Exception:
-        return None
+            t = json.load(f)
+    except (OSError, ValueError) as e:
+        return None, f"unreadable traffic record: {e}"
+    sha = kernel_source_sha()
+    if t.get("source_sha") != sha:
+        return None, (f"stale: traffic_{config}.json was measured on kernel sources {t.get('source_sha')}, "
+                      f"this tree is {sha} (re-run tools/profile.sh)")
+    return t, None
 
 
 def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, extra: dict,
@@ -142,7 +152,8 @@ def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, ex
     t0 = time.perf_counter()
     ob.pass_threaded(timed_passes, nthreads=threads)
     dt = time.perf_counter() - t0
-    return {"value": timed_passes * E / dt, "unit": "events/s", "cores": threads, "kind": "port",
+    return {"value": timed_passes * E / dt, "unit": "events/s", "cores": threads, "threads": threads,
+            "host_cpus": os.cpu_count(), "kind": "port",
             "n_syn": n_syn, "graph": ("reduced: %d of %d synapses, picks hit a smaller working set than "
                                       "the GPU's (likely overstates the CPU rate)" % (n_syn, wl.n_syn))
             if reduced else "same records as the GPU run",
@@ -181,9 +192,12 @@ def main():
             dist.init_process_group(backend)
 
     if world > 1:
+        # one GPU per rank (RCCL): the passes are driven by the C-ABI over the
+        # library's RCCL communicator (abnn_shard_traverse); the gloo
+        # rehearsal (ranks sharing a GPU) drives them phase by phase from Python
         sb = ShardedBrain(TorchComm(), wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, events,
                           device=device, mode=mode, capacity_factor=1.01 if args.plasticity else 1.0,
-                          **extra)
+                          native=backend == "nccl", **extra)
         brain = sb.brain
         step = sb.step
     else:
@@ -246,7 +260,7 @@ def main():
         achieved = bytes_per_launch / (avg_gate_ms * 1e-3) / 1e9
         survey_per_launch = survey_bytes(stats, track) / passes
         default_run = mode == 0 and events == wl.events
-        traffic = load_traffic(args.config) if world == 1 and default_run else None
+        traffic, traffic_note = load_traffic(args.config) if world == 1 and default_run else (None, "not the default run")
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -262,14 +276,16 @@ def main():
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "bytes_formula": ("3*E (24-bit src stream: 2-B lo + 1-B hi per event; E visited events) -- "
                               "DESIGN.md §5" if mode == 0 else
-                              "4*E (one random u32 src per pick, the src32 mirror; HBM moves >= 64 B "
-                              "per random access) -- DESIGN.md §5"),
+                              "64*E (one random 64-B HBM line per pick of the src32 mirror; 4 B of it "
+                              "used) -- DESIGN.md §5"),
+            "random_picks_per_s": (round(stats["events"] / passes / (avg_gate_ms * 1e-3), 1) if mode == 1 else None),
             "survey_formula_bytes_per_launch": int(survey_per_launch),
             "survey_formula_achieved": round(survey_per_launch / (avg_gate_ms * 1e-3) / 1e9, 1),
             "survey_formula": "24*E + 8*G1 (SURVEY §8d; G1 pre-gated) -- counts an 8-B lastFired[src] "
                               "gather per event that this design answers from LDS/L2",
-            "traffic_source": "profiles/traffic_%s.json (rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE)"
-                              % args.config if traffic else None,
+            "traffic_source": ("profiles/traffic_%s.json (rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE; tag %s, "
+                               "kernel sources %s)" % (args.config, traffic.get("tag"), traffic.get("source_sha"))
+                               if traffic else traffic_note),
             "pass_ms": round(dt / args.steps * 1e3, 4),
         }
         cpu = None

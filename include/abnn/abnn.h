@@ -386,6 +386,27 @@ abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream);
 abnn_status abnn_launch_renormalise(uint32_t* last_fired, uint32_t* last_visited, uint32_t* clock,
                                     uint32_t n_nrn, void* stream);
 
+/* ---- sharded passes driven from C over RCCL ---------------------------------
+ * One process per GPU (xGMI), one communicator per shard handle.  The
+ * library's own RCCL communicator (RCCL = NCCL on ROCm; the one already
+ * loaded in the process, e.g. by torch, else librccl.so.1): one rank calls
+ * abnn_comm_unique_id, every rank gets those ABNN_COMM_ID_BYTES bytes (any
+ * channel: torch.distributed broadcast, a file, MPI) and calls
+ * abnn_comm_create.  abnn_shard_traverse then enqueues `passes` whole sharded
+ * passes on `stream` -- per pass: abnn_shard_gate, ONE ncclAllGather of the
+ * exchange records (in place, on the stream), abnn_shard_apply,
+ * abnn_shard_commit -- with no host round trip except after a structural
+ * update (an all-reduce of the shards' visited events for the clock-tick
+ * rule, then abnn_set_global_events).  abnn_comm_sync_visits is the lazy
+ * all-reduce(MAX) of lastVisited (never read by a decision, brain.metal:44). */
+#define ABNN_COMM_ID_BYTES 128
+typedef struct abnn_comm abnn_comm;
+abnn_status abnn_comm_unique_id(void* id_out);
+abnn_status abnn_comm_create(const void* id, uint32_t world, uint32_t rank, int device, abnn_comm** out);
+abnn_status abnn_comm_destroy(abnn_comm* c);
+abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, void* stream);
+abnn_status abnn_comm_sync_visits(abnn_brain* b, abnn_comm* c, void* stream);
+
 /* ---- statistics / timing ---------------------------------------------------- */
 abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out);   /* synchronises */
 abnn_status abnn_reset_stats(abnn_brain* b);

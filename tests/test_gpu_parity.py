@@ -205,8 +205,13 @@ def _virtual_shard_run(world, n_syn, events, passes, n_hidden=30_000, seed=4):
     return shards
 
 
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["fused-shard-pass", "two-kernel-shard-pass"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_virtual_shards_equal_unsharded_gpu(gpu, world):
+def test_virtual_shards_equal_unsharded_gpu(gpu, monkeypatch, world, fused):
+    """A sharded pass is k_gate (shard mode) + all-gather + k_shard_walk on the
+    fused path, four kernels + all-gather on the two-kernel one: both equal
+    the unsharded fused pass bit for bit."""
+    monkeypatch.setenv("ABNN_FUSED", fused)
     n_syn, passes = 2_000_000, 10
     shards = _virtual_shard_run(world, n_syn, n_syn, passes)
     g, o = _pair(30_000, n_syn, n_syn, seed=4)

@@ -29,3 +29,44 @@ def test_two_rank_sharded_brain_equals_unsharded(gpu):
                        env={**os.environ, "OMP_NUM_THREADS": "4"})
     assert r.returncode == 0, r.stderr[-3000:]
     assert "SHARDED_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_native_rccl_shard_traverse_world1(gpu, monkeypatch):
+    """The C-driven sharded pass (abnn_comm over RCCL, abnn_shard_traverse: gate,
+    in-place ncclAllGather and apply/commit enqueued by the library, no Python
+    per pass) at world 1 on the box's one GPU, with plasticity so the
+    structural update's all-reduce of visited events runs: equal to the
+    unsharded brain bit for bit."""
+    import numpy as np
+    import torch.distributed as dist
+
+    import abnn_amd
+    from abnn_amd.shard import ShardedBrain, TorchComm
+
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        extra = dict(w_prune=0.105, p_new=0.35, w_init=0.5, compact_every=4, track_visits=1)
+        n_syn, events, passes = 1_000_000, 1_000_000, 13
+        sb = ShardedBrain(TorchComm(), 256, 256, 30_000, n_syn, events, device=0, capacity_factor=1.05,
+                          native=True, **extra)
+        ref = abnn_amd.Brain(256, 256, 30_000, n_syn, events, syn_capacity=int(n_syn * 1.05), **extra)
+        for b in (sb.brain, ref):
+            b.build_random_graph(4)
+            b.set_auto_stimulus(0, 256)
+            b.set_reward(0.25)
+        sb.step(passes)
+        ref.encode_traversal(passes)
+        sb.sync_visits()
+        ref.synchronize()
+        assert sb.brain.structural_updates() == ref.structural_updates() == 3
+        assert np.array_equal(sb.brain.download_synapses().view(np.uint32), ref.download_synapses().view(np.uint32))
+        assert np.array_equal(sb.brain.last_fired(), ref.last_fired())
+        assert np.array_equal(sb.brain.last_visited(), ref.last_visited())
+        assert sb.brain.scalars() == ref.scalars()
+        assert sb.brain.stats() == ref.stats()
+        sb.native.close()
+    finally:
+        dist.destroy_process_group()

@@ -85,7 +85,12 @@ def main():
     # last 10 timed k_gate launches of each PMC pass are steady state
     fetch = pmc_values(os.path.join(out, "fetch"), "FETCH_SIZE")[-10:]
     write = pmc_values(os.path.join(out, "write"), "WRITE_SIZE")[-10:]
-    res = {"config": cfg, "tag": tag, "kernel": "k_gate"}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from abnn_amd.build import kernel_source_sha
+
+    # bench.py uses this record only while the kernel sources are these
+    res = {"config": cfg, "tag": tag, "kernel": "k_gate", "source_sha": kernel_source_sha(),
+           "commit": os.environ.get("ABNN_COMMIT", "")}
     if fetch and write:
         f_kib, w_kib = statistics.median(fetch), statistics.median(write)
         res.update({
