@@ -866,6 +866,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = dalloc(&d.cand_list, (uint64_t)kFusedMaxRanges * kCandCap)) != ABNN_OK) return fail(s);
     if (const char* env = std::getenv("ABNN_FUSED")) b->use_fused = std::atoi(env) != 0;
     d.spec_mode = 1;
+    d.spec_margin = -1;
+    if (const char* env = std::getenv("ABNN_SPEC_MARGIN")) d.spec_margin = std::atoi(env);
     d.cost_tail = 1;
     if (const char* env = std::getenv("ABNN_COST_TAIL")) d.cost_tail = std::atoi(env) ? 1u : 0u;
     d.flush_at = kChunk;

@@ -63,6 +63,19 @@ __device__ __forceinline__ uint32_t wave_uniform(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
+// A wave-uniform READ through the scalar data cache (s_load, counted by
+// lgkmcnt): the gate's prologue reads its range bounds and the pass-start
+// scalars this way, so they do not queue behind the filter's LDS-DMA and the
+// first record loads, which vmcnt counts in issue order.  Only for values no
+// wave of the launch writes before every wave has read them (the previous
+// launch or the host wrote them).  Never a write: nothing stores through the
+// scalar cache.
+template <typename T>
+__device__ __forceinline__ T sload(const T* p)
+{
+    return *(const __attribute__((address_space(4))) T*)p;
+}
+
 // Inclusive wave scan on DPP (row_shr within 16-lane rows, then the gfx9
 // row broadcasts): six VALU ops, no LDS crossbar round trips.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)

@@ -14,6 +14,15 @@ namespace abnn {
 // recent-spike bitmap, each folded onto filter_words 32-bit words with its own
 // word hash (kernels.hip; 8192 words = 32 KiB each by default).
 constexpr int kMaxFilterWords = 16384;  // per image
+// Second-level filter of the refractory stage (kernels.hip refrac_chunk): a
+// 2-probe Bloom filter of the same recent set over kF2Words words (64 Ki bits),
+// stored after the blocked filter in each filter buffer and copied to LDS by
+// the gate's prologue.  Staged events it rejects gather nothing; the ones it
+// passes gather {dst, w} beside the exact bitmap word (one dependent round
+// trip less).  Its hashes are independent of the blocked filter's.
+constexpr uint32_t kF2Words = 2048;
+__host__ __device__ inline uint32_t f2_hash1(uint32_t n) { return (n * 0x9E3779B1u) >> 16; }
+__host__ __device__ inline uint32_t f2_hash2(uint32_t n) { return (n * 0x85EBCA77u + 0x165667B1u) >> 16; }
 constexpr int kScanThreads = 1024; // k_scan is one workgroup
 constexpr int kMaxGateBlocks = 1024;
 constexpr int kMaxRanges = 16384;  // kMaxGateBlocks x up to 16 waves (one range per gate wave)
@@ -28,7 +37,7 @@ constexpr int kDummyRecords = 64 * 32;  // >= 64 lanes x max events per lane; al
                                          // (the dummy block itself holds 2x as many words: {dst, w} loads)
 constexpr uint32_t kFiredRing = 8;     // spike lists kept (the bitmap build needs window_pre < kFiredRing)
 constexpr uint32_t kChunk = 384;        // pre-gated events per chunk (staged in LDS by a gate wave)
-constexpr uint32_t kWaveClock = 12;     // diagnostics: u64 words per gate wave (wave_clock)
+constexpr uint32_t kWaveClock = 16;     // diagnostics: u64 words per gate wave (wave_clock)
 constexpr uint32_t kChunkSlotDiv = 128; // chunk_cnt index = (region + c * kChunk) / 128 (unique per chunk)
 
 // Per-pass bookkeeping in device memory (one per handle).
@@ -163,6 +172,7 @@ struct DeviceState {
     uint32_t cost_tail;       // fused: a range's partition cost includes its tail (default; ABNN_COST_TAIL=0: off)
     uint32_t flush_at;        // fused: staged events that send a wave's stage through the refractory stage
                               // (<= kChunk; ABNN_FLUSH_AT)
+    int32_t spec_margin;      // fused: workgroups predicted below the cut = last cut + spec_margin (ABNN_SPEC_MARGIN, -1)
     uint32_t spec_mode;       // fused: speculative weight stores 0 off, 1 below the predicted cut (default),
                               // 2 everywhere (ABNN_SPEC; 2 exercises the restore path)
     uint32_t shard_mode;      // fused pass = the first launch of a sharded pass (k_gate: no stamps, exchange record)

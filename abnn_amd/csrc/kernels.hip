@@ -275,6 +275,21 @@ __device__ __forceinline__ void filter_set(uint32_t* f, uint32_t j, uint32_t bit
     const uint32_t t = filter_t(j, lg), g = (j ^ t) & (FB - 1), r = t & 31u;
     atomicOr(f + 2 * g, bits);
     atomicOr(f + 2 * g + 1, (bits << r) | (bits >> ((32u - r) & 31u)));
+    // the second-level filter (engine.h kF2Words), after the blocks: per neuron
+    uint32_t* f2 = f + 2 * FB;
+    for (uint32_t m = bits; m; m &= m - 1u) {
+        const uint32_t n = 32u * j + (uint32_t)__builtin_ctz(m), h1 = f2_hash1(n), h2 = f2_hash2(n);
+        atomicOr(f2 + (h1 >> 5), 1u << (h1 & 31u));
+        atomicOr(f2 + (h2 >> 5), 1u << (h2 & 31u));
+    }
+}
+
+// The second-level filter test on an LDS copy: false for no recent neuron
+// (no false negatives), true for ~a tenth of the others.
+__device__ __forceinline__ bool f2_test(const uint32_t* s_f2, uint32_t n)
+{
+    const uint32_t h1 = f2_hash1(n), h2 = f2_hash2(n);
+    return ((s_f2[h1 >> 5] >> (h1 & 31u)) & (s_f2[h2 >> 5] >> (h2 & 31u)) & 1u) != 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -468,10 +483,11 @@ __device__ __forceinline__ uint4 range_totals(const DeviceState& d, uint32_t r) 
 // (the workgroup is predicted to lie below the pass's budget cut) the updated
 // weight is stored here already; the walk restores w where the prediction was
 // wrong.
-template <int R, bool kRandom, bool kFused, class At>
+template <int R, bool kRandom, bool kFused, bool kTail, class At>
 __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const KernelParams& kp, uint64_t region,
                                               uint64_t base, uint32_t n, uint64_t now, uint64_t pass, float Rw,
-                                              float rbw, bool spec, uint32_t crange, uint32_t c0, At&& at)
+                                              float rbw, bool spec, uint32_t crange, uint32_t c0,
+                                              const uint32_t* s_f2, At&& at)
 {
     const uint32_t lane = threadIdx.x & 63, nn = (uint32_t)d.n_nrn;
     uint32_t n_g1 = 0, n_g2 = 0, n_cand = 0;
@@ -483,29 +499,76 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
         uint32_t rel[R], src[R], bw[R], dst[R];
         float w[R];
         uint64_t ld[R];
+        uint2 dw[R];
+        bool f2[R];
+        // one dependent round trip for both: the exact bitmap word of src
+        // and, for the events the second-level filter passes (LDS: the
+        // recent ones and ~a tenth of the blocked filter's false positives),
+        // the record's {dst, w}
+        if constexpr (!kTail) {
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const uint32_t q = b0 + j * 64 + lane;
-            const uint2 e = q < n ? at(q) : make_uint2(0u, 0xFFFFFFFFu);
-            rel[j] = e.x;
-            // the sweep stages the record's code (engine.h, src_code), random mode its src
-            src[j] = kRandom || q >= n ? e.y : code_src(e.y & 0xFFFFu, e.y >> 16);
-            bw[j] = src[j] < nn ? d.bitmap[src[j] >> 5] : 0u;
+            for (int j = 0; j < R; ++j) {
+                const uint32_t q = b0 + j * 64 + lane;
+                const uint2 e = q < n ? at(q) : make_uint2(0u, 0xFFFFFFFFu);
+                rel[j] = e.x;
+                // the sweep stages the record's code (engine.h, src_code), random mode its src
+                src[j] = kRandom || q >= n ? e.y : code_src(e.y & 0xFFFFu, e.y >> 16);
+                bw[j] = src[j] < nn ? d.bitmap[src[j] >> 5] : 0u;
+                f2[j] = src[j] < nn && f2_test(s_f2, src[j]);
+                dw[j] = f2[j] ? d.syn.dw[record_of(rel[j])] : make_uint2(0xFFFFFFFFu, 0u);  // one access for both
+            }
+        } else {
+            // the range's tail (after its stream: no stream registers live):
+            // straight-line (no per-round branches, so every access of a phase is
+            // in flight at once): lanes past n and rejected events read a safe
+            // address (the stage's spare slots, word 0, record 0) and discard it.
+            // (n <= kChunk <= R * 64 entries of a stage of kChunk + 128)
+            uint2 e[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) e[j] = at(b0 + j * 64 + lane);
+            uint32_t fa[R], fb[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const bool v = b0 + j * 64 + lane < n;
+                rel[j] = e[j].x;
+                // the sweep stages the record's code (engine.h, src_code), random mode its src
+                src[j] = !v ? 0xFFFFFFFFu : (kRandom ? e[j].y : code_src(e[j].y & 0xFFFFu, e[j].y >> 16));
+                const uint32_t sn = src[j] < nn ? src[j] : 0u;
+                fa[j] = s_f2[f2_hash1(sn) >> 5];
+                fb[j] = s_f2[f2_hash2(sn) >> 5];
+            }
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const uint32_t sn = src[j] < nn ? src[j] : 0u;
+                f2[j] = src[j] < nn && ((fa[j] >> (f2_hash1(sn) & 31u)) & (fb[j] >> (f2_hash2(sn) & 31u)) & 1u);
+                bw[j] = d.bitmap[sn >> 5];
+                dw[j] = d.syn.dw[f2[j] ? record_of(rel[j]) : 0];
+            }
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const bool g1 = (bw[j] >> (src[j] & 31u)) & 1u;  // brain.metal:73-77, exact
+            const bool g1 = src[j] < nn && ((bw[j] >> (src[j] & 31u)) & 1u);  // brain.metal:73-77, exact
             bw[j] = g1;
-            const uint64_t ri = g1 ? record_of(rel[j]) : 0;
-            const uint2 dw = g1 ? d.syn.dw[ri] : make_uint2(0xFFFFFFFFu, 0u);  // one access for both
-            dst[j] = dw.x;  // tombstones (dst = 0xFFFFFFFF) never pass
-            w[j] = __uint_as_float(dw.y);
+            // never taken while the second-level filter holds every recent
+            // neuron (it is built beside the bitmap: filter_set)
+            if (__ballot(g1 && !f2[j]) != 0 && g1 && !f2[j]) dw[j] = d.syn.dw[record_of(rel[j])];
+            if (!g1) dw[j] = make_uint2(0xFFFFFFFFu, 0u);
+            dst[j] = dw[j].x;  // tombstones (dst = 0xFFFFFFFF) never pass
+            w[j] = __uint_as_float(dw[j].y);
         }
-#pragma unroll
         // the stimulus of this pass is stamped `now` (brain.cpp:82) by k_bitmap
         // or, in steady state, by the gate itself at some point of the pass
-        for (int j = 0; j < R; ++j)
-            ld[j] = dst[j] - d.stim_first < d.stim_count ? now : (dst[j] < nn ? d.last_fired[dst[j]] : 0ull);
+        if constexpr (!kTail) {
+#pragma unroll
+            for (int j = 0; j < R; ++j)
+                ld[j] = dst[j] - d.stim_first < d.stim_count ? now : (dst[j] < nn ? d.last_fired[dst[j]] : 0ull);
+        } else {
+#pragma unroll
+            for (int j = 0; j < R; ++j) ld[j] = d.last_fired[dst[j] < nn ? dst[j] : 0u];
+#pragma unroll
+            for (int j = 0; j < R; ++j)
+                ld[j] = dst[j] - d.stim_first < d.stim_count ? now : (dst[j] < nn ? ld[j] : 0ull);
+        }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             if (b0 + (uint32_t)j * 64 >= n) break;  // wave-uniform
@@ -861,6 +924,16 @@ __device__ __forceinline__ void range_spikes_local(const DeviceState& d, const K
     }
 }
 
+// The next pass's speculative workgroups (refrac_chunk's spec) from the
+// workgroup `cut` where this pass's budget ran out: the ones below it, moved
+// by spec_margin (default -1: the cut's own workgroup and one below it walk).
+__device__ __forceinline__ uint32_t spec_prediction(const DeviceState& d, uint32_t cut, uint32_t G)
+{
+    if (cut >= G) return G;
+    const int64_t v = (int64_t)cut + d.spec_margin;
+    return v < 0 ? 0u : (v > (int64_t)G ? G : (uint32_t)v);
+}
+
 // LDS of the fused pass's end (per workgroup).
 template <int NW>
 struct FusedLds {
@@ -901,19 +974,21 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         order = atomicAdd(&L.done, 1u);
     }
     if (wave_uniform(order) == 0) fused_next_bounds<NW>(d, L.cc);
-    // this wave's share of the next pass's bitmap build that does not depend
-    // on this pass (the spike lists of passes p+1-W..p-1, the stimulus): it
-    // fills the wait for the workgroup's other ranges
-    if (d.build_next) {
-        const uint64_t nitems = next_items(d, kp), step = (uint64_t)d.n_ranges * 64;
-        for (uint64_t x0 = (uint64_t)r * 64; x0 < nitems; x0 += step) {  // wave-uniform
-            const uint64_t x = x0 + lane;
+    lds_barrier();  // every range of the workgroup through its refractory stage
+    uint32_t vals[kLbMaxWords];
+    if (wid != 0 && d.build_next) {
+        // while wave 0 publishes and polls: the workgroup's share of the next
+        // pass's bitmap build that does not depend on this pass (the spike
+        // lists of passes p+1-W..p-1, the stimulus), item x to workgroup
+        // x % G -- after the publication, so that it never delays a look-back
+        // word (the bitmap is read by the next pass only)
+        const uint64_t nitems = next_items(d, kp), G = gridDim.x;
+        for (uint64_t s0 = (uint64_t)(wid - 1) * 64; s0 * G + blockIdx.x < nitems; s0 += (uint64_t)(NW - 1) * 64) {
+            const uint64_t x = (s0 + lane) * G + blockIdx.x;  // wave-uniform trip count (lane 0's item)
             const NextItem it = x < nitems ? next_item_load(d, kp, pass, x) : NextItem{0u, 0u, 0u};
             wave_set_next_dedup(d, it.i < it.lim, it.n, L.setc);
         }
     }
-    lds_barrier();  // every range of the workgroup through its refractory stage
-    uint32_t vals[kLbMaxWords];
     if (wid == 0) {
         uint32_t c = lane < (uint32_t)NW ? L.cand[lane] : 0u;
         c = wave_sum(c);
@@ -1011,7 +1086,14 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         }
         return;
     }
-    if (s1 <= s0 && !first) return;  // workgroup-uniform: nothing to stamp
+    uint64_t* wc0 = d.wave_clock + (uint64_t)kWaveClock * r;  // diagnostics, wave 0: all words seen, exit
+    if (s1 <= s0 && !first) {  // workgroup-uniform: nothing to stamp
+        if (threadIdx.x == 0) {
+            wc0[12] = 0;
+            wc0[13] = __builtin_amdgcn_s_memrealtime();
+        }
+        return;
+    }
     // every workgroup's word published = every refractory stage of the pass
     // done: no lastFired read is left, the stamps may land
     if (wid == 0) {
@@ -1029,10 +1111,11 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
             }
             if (lane == 0) {
                 L.total = tot;
-                d.work->spec_wgs = cut >= gridDim.x ? gridDim.x : (cut > 0 ? cut - 1 : 0u);
+                d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
             }
         }
     }
+    if (threadIdx.x == 0) wc0[12] = __builtin_amdgcn_s_memrealtime();
     lds_barrier();
     const uint32_t* ring = d.fired_ring + (pass & (kFiredRing - 1)) * (uint64_t)budget;
     for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
@@ -1048,6 +1131,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         __hip_atomic_store((gu32*)&d.work->t0_g2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         d.work->epoch = epoch + 1u;
     }
+    if (threadIdx.x == 0) wc0[13] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------------------
@@ -1095,6 +1179,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
     static_assert(!(kFused && kRandom), "the fused pass is sweep-mode only");
     __shared__ uint2 s_fb[FW];  // the filter's FW 64-bit blocks
+    __shared__ uint32_t s_f2[kF2Words];  // the second-level filter (refrac_chunk)
     __shared__ uint32_t s_off[NW][SE], s_src[NW][SE];
     __shared__ FusedLds<NW> s_fz;            // fused: the pass end's workgroup state
 
@@ -1110,6 +1195,12 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     for (int c = 0; c < FW / 2 / BLOCK; ++c)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(d.filter) + c * BLOCK + tid,
                                          reinterpret_cast<uint4*>(s_fb) + c * BLOCK + (tid & ~63u), 16, 0, 0);
+    // the second-level filter, stored after the blocks (engine.h kF2Words)
+    static_assert(kF2Words % 4 == 0 && kF2Words / 4 <= 2048, "second-level filter copy");
+    for (uint32_t i0 = 0; i0 < kF2Words / 4; i0 += BLOCK)  // workgroup-uniform
+        if (i0 + tid < kF2Words / 4)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(d.filter + 2 * FW) + i0 + tid,
+                                             reinterpret_cast<uint4*>(s_f2) + i0 + (tid & ~63u), 16, 0, 0);
     // fused: the previous pass's range costs (the next partition's input,
     // fused_next_bounds) go to LDS the same way
     if constexpr (kFused) {
@@ -1126,24 +1217,24 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // a dense stretch of the graph does not land on one CU)
     const uint32_t r = (!kFused && d.range_map) ? wid * gridDim.x + blockIdx.x : blockIdx.x * NW + wid;
     // (iteration counts < 2^31, checked at create; wave-uniform, held in SGPRs)
-    const uint32_t it_begin = wave_uniform(d.range_bounds[r]), it_end = wave_uniform(d.range_bounds[r + 1]);
+    const uint32_t it_begin = sload(d.range_bounds + r), it_end = sload(d.range_bounds + r + 1);
     const uint64_t region = (uint64_t)it_begin * IE;
-    const uint64_t now = *d.clock;  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
+    const uint64_t now = sload(d.clock);  // per-TG clock cache, brain.metal:63-68 (C1: pass start)
     // fused: the pass-start reward and rBar (brain.metal:105-106; C1) for the
     // updated weights of the refractory stage
     // (pass-start scalars are moved to SGPRs: held through the stream in
     // VGPRs they would spill)
-    const float Rw = kFused ? __uint_as_float(wave_uniform(__float_as_uint(*d.reward))) : 0.0f;
-    const float rbw = kFused ? __uint_as_float(wave_uniform(__float_as_uint(*d.rbar))) : 0.0f;
+    const float Rw = kFused ? sload(d.reward) : 0.0f;
+    const float rbw = kFused ? sload(d.rbar) : 0.0f;
     // fused: the pass index and epoch (workgroup 0 advances both at the end,
     // once every workgroup has read them), and whether this workgroup is
     // predicted below the budget cut (the previous pass's cut, less one); never
     // with pruning (a pruned record's src and dst change, which a restore would
     // have to undo too)
-    const uint64_t pass_f = kFused ? *d.pass_index : 0;
-    const uint32_t epoch = kFused ? wave_uniform(d.work->epoch) : 0u;
+    const uint64_t pass_f = kFused ? sload(d.pass_index) : 0;
+    const uint32_t epoch = kFused ? sload(&d.work->epoch) : 0u;
     const bool spec = kFused && !(kp.w_prune > 0.0f) &&
-                      (d.spec_mode == 2 || (d.spec_mode == 1 && blockIdx.x < wave_uniform(d.work->spec_wgs)));
+                      (d.spec_mode == 2 || (d.spec_mode == 1 && blockIdx.x < sload(&d.work->spec_wgs)));
     uint32_t* st_off = s_off[wid];
     uint32_t* st_src = s_src[wid];
     // Records in flight.  Sweep: the packed src stream (engine.h, SynArrays):
@@ -1158,7 +1249,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         uint32_t s[kRandom ? K : 2 * NG], h[NG], dd[KD];
     };
     Recs A, B;
-    const uint64_t pass = kRandom ? *d.pass_index : 0;
+    const uint64_t pass = kRandom ? sload(d.pass_index) : 0;
     auto issue = [&](Recs& x, uint64_t it, bool live) __attribute__((always_inline)) {
         if constexpr (kRandom) {  // random-edge mode: a per-lane random record per event
 #pragma unroll
@@ -1201,7 +1292,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // next pass builds them: k_apply, the fused pass, or k_bitmap), a
         // slice per workgroup; this pass's stimulus is stamped by workgroup 0
         // (the refractory stage reads it as now)
-        const uint32_t nz = d.n_bitmap_words + 2 * FW, per = (nz + gridDim.x - 1) / gridDim.x;
+        const uint32_t nz = d.n_bitmap_words + 2 * FW + kF2Words, per = (nz + gridDim.x - 1) / gridDim.x;
         for (uint32_t i = blockIdx.x * per + tid; i < min(nz, (blockIdx.x + 1) * per); i += BLOCK) {
             if (i < d.n_bitmap_words) d.bitmap_clear[i] = 0u;
             else d.filter_clear[i - d.n_bitmap_words] = 0u;
@@ -1237,8 +1328,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     auto chunk_out = [&]() {
         const uint64_t tc = __builtin_amdgcn_s_memrealtime();
         const uint64_t at = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
-        const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused>(d, kp, region, at, kChunk, now, pass, Rw, rbw,
-                                                                   spec, r, tot.z, stage_at);
+        const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, false>(d, kp, region, at, kChunk, now, pass, Rw, rbw,
+                                                                   spec, r, tot.z, s_f2, stage_at);
         if (!kFused && lane == 0) d.chunk_cnt[chunk_slot(region, nch)] = c;
         tot.x += c.x;
         tot.y += c.y;
@@ -1261,8 +1352,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // are staged (survivors go right after the range's earlier ones)
     auto flush_all = [&]() {
         const uint64_t tc = __builtin_amdgcn_s_memrealtime();
-        const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused>(d, kp, region, region + tot.y, pend, now, pass, Rw,
-                                                                   rbw, spec, r, tot.z, stage_at);
+        const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, false>(d, kp, region, region + tot.y, pend, now, pass, Rw,
+                                                                   rbw, spec, r, tot.z, s_f2, stage_at);
         tot.x += c.x;
         tot.y += c.y;
         tot.z += c.z;
@@ -1418,8 +1509,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     if (d.tail_prio < 4) set_priority(d.tail_prio);
     // the range's last chunk: refractory stage by this wave
     const uint64_t tb = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
-    const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
-                                                               r, tot.z, stage_at);
+    const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, true>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
+                                                               r, tot.z, s_f2, stage_at);
     const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
     const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
     if constexpr (kFused) {
@@ -1978,8 +2069,7 @@ __global__ __launch_bounds__(NW * 64) void k_shard_walk(DeviceState d, KernelPar
     // or past it) names the ones below it, less one, as the fused pass does
     if (wid == NW - 1 && lane == 0) {
         const uint4 r0 = d.range_info[blockIdx.x * NW];
-        if (off + r0.x < budget && P + ri.z >= budget)
-            d.work->spec_wgs = blockIdx.x > 0 ? blockIdx.x - 1 : 0u;
+        if (off + r0.x < budget && P + ri.z >= budget) d.work->spec_wgs = spec_prediction(d, blockIdx.x, gridDim.x);
     }
     const uint32_t wu = wave_sum(ac.upd) + upd_rest, wf = wave_sum(ac.nf), wp = wave_sum(ac.npr);
     if (lane == 0) {

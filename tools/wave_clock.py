@@ -29,7 +29,7 @@ for p in range(passes - 1 if b2b else 0, passes):
     b.synchronize()
     if p < first:
         continue
-    nr, KW = 16384, 12  # kWaveClock u64 per range (engine.h)
+    nr, KW = 16384, 16  # kWaveClock u64 per range (engine.h)
     buf = np.zeros(KW * nr + 32, dtype=np.uint64)
     f = b._lib.abnn_debug_wave_clock
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
@@ -59,6 +59,13 @@ for p in range(passes - 1 if b2b else 0, passes):
         print(f"  walk done   {q(wk)}")
         print(f"  lb wait     {q(lb - en)}")
         print(f"  walk dur    {q(wk - lb)}")
+        w0 = w[::16]  # wave 0 of each workgroup: all words seen (stampers), exit
+        if (w0[:, 13] > 0).all():
+            seen, ex = (w0[:, 12] - t0) * 10e-3, (w0[:, 13] - t0) * 10e-3
+            stampers = w0[:, 12] > 0
+            print(f"  wg exit     {q(ex)}")
+            if stampers.any():
+                print(f"  all words seen (stamping wgs: {int(stampers.sum())}) {q(seen[stampers])}")
     np.save(os.path.join(os.environ.get("OUT", "gpurun_out"), f"wave_clock_p{p}.npy"), w)
     rb = np.zeros(len(w) + 1, dtype=np.uint32)
     g = b._lib.abnn_debug_range_bounds
