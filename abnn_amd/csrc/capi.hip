@@ -873,6 +873,12 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.flush_at = kChunk;
     if (const char* env = std::getenv("ABNN_FLUSH_AT"))
         d.flush_at = (uint32_t)std::min<int>((int)kChunk, std::max(64, std::atoi(env)));
+    d.wt_sc1 = 0;
+    if (const char* env = std::getenv("ABNN_WT_SC1")) d.wt_sc1 = std::atoi(env) != 0;
+    d.lds_tail = 1;
+    if (const char* env = std::getenv("ABNN_LDS_TAIL")) d.lds_tail = std::atoi(env) != 0;
+    d.next_helpers = 1;
+    if (const char* env = std::getenv("ABNN_NEXT_HELPERS")) d.next_helpers = std::atoi(env) != 0;
     if (const char* env = std::getenv("ABNN_SPEC")) d.spec_mode = (uint32_t)std::min(2, std::max(0, std::atoi(env)));
     d.bitmap = b->bitmap_buf[0];
     d.filter = b->filter_buf[0];
@@ -905,7 +911,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     }
     *b->err_host = 0;
     if ((s = dalloc(&b->u64_scratch, 4)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.wave_clock, (uint64_t)kWaveClock * kMaxRanges + 32)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.wave_clock, (uint64_t)kWaveClockPasses * kWaveClock * kMaxRanges + 32)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.apply_clock, 8 * (uint64_t)kWalkBlocks)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.fired_ring, (uint64_t)kFiredRing * std::max(1u, p.max_spikes))) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.n_fired_ring, kFiredRing)) != ABNN_OK) return fail(s);
@@ -1370,13 +1376,22 @@ abnn_status abnn_comm_sync_visits(abnn_brain* b, abnn_comm* c, void* stream)
 
 // Diagnostics (not part of abnn.h): the last pass's per-wave gate times,
 // kWaveClock u64 per range (engine.h, DeviceState::wave_clock), 100 MHz ticks.
-abnn_status abnn_debug_wave_clock(abnn_brain* b, uint64_t* out, uint64_t n)
+abnn_status abnn_debug_wave_clock_slot(abnn_brain* b, uint32_t slot, uint64_t* out, uint64_t n)
 {
     REQUIRE(b && out, "null argument");
+    REQUIRE(slot < kWaveClockPasses, "slot out of range");
     ST_TRY(sync_all(b));
-    HIP_TRY(hipMemcpy(out, b->d.wave_clock, std::min<uint64_t>(n, (uint64_t)kWaveClock * kMaxRanges + 32) * 8,
-                      hipMemcpyDeviceToHost));
+    const uint64_t per = (uint64_t)kWaveClock * kMaxRanges;
+    HIP_TRY(hipMemcpy(out, b->d.wave_clock + slot * per, std::min<uint64_t>(n, per) * 8, hipMemcpyDeviceToHost));
     return ABNN_OK;
+}
+
+abnn_status abnn_debug_wave_clock(abnn_brain* b, uint64_t* out, uint64_t n)
+{
+    REQUIRE(b, "null argument");
+    // a fused pass p writes slot p % kWaveClockPasses, the two-kernel gate slot 0
+    const uint32_t slot = b->last_pass_fused && b->pass_host ? (uint32_t)((b->pass_host - 1) % kWaveClockPasses) : 0u;
+    return abnn_debug_wave_clock_slot(b, slot, out, n);
 }
 
 // Diagnostics (not part of abnn.h): the last k_apply's per-workgroup timeline,

@@ -38,6 +38,7 @@ constexpr int kDummyRecords = 64 * 32;  // >= 64 lanes x max events per lane; al
 constexpr uint32_t kFiredRing = 8;     // spike lists kept (the bitmap build needs window_pre < kFiredRing)
 constexpr uint32_t kChunk = 384;        // pre-gated events per chunk (staged in LDS by a gate wave)
 constexpr uint32_t kWaveClock = 16;     // diagnostics: u64 words per gate wave (wave_clock)
+constexpr uint32_t kWaveClockPasses = 8; // ... per pass slot; the fused pass keeps the last 8 passes' (pass % 8)
 constexpr uint32_t kChunkSlotDiv = 128; // chunk_cnt index = (region + c * kChunk) / 128 (unique per chunk)
 
 // Per-pass bookkeeping in device memory (one per handle).
@@ -146,7 +147,7 @@ struct DeviceState {
     uint32_t* claim;          // random mode: [n_syn] highest updating event + 1 (0 = none)
     PassWork* work;
     uint32_t* err_word;       // host-mapped: a fused pass's look-back wait gave up (capi.hip pass_error)
-    uint64_t* wave_clock;     // [kWaveClock * n_ranges] per-wave gate times {start, stream done, refractory
+    uint64_t* wave_clock;     // [kWaveClockPasses][kWaveClock * kMaxRanges] per-wave gate times {start, stream done, refractory
                               // tail done, entry, (fused) look-back done, walk done} (100 MHz, diagnostics)
     uint32_t* fired_ring;     // [kFiredRing * max_spikes] spike list of pass q at (q % kFiredRing), budget order
     uint32_t* n_fired_ring;   // [kFiredRing] their lengths (k_apply workgroup 0)
@@ -175,6 +176,12 @@ struct DeviceState {
     int32_t spec_margin;      // fused: workgroups predicted below the cut = last cut + spec_margin (ABNN_SPEC_MARGIN, -1)
     uint32_t spec_mode;       // fused: speculative weight stores 0 off, 1 below the predicted cut (default),
                               // 2 everywhere (ABNN_SPEC; 2 exercises the restore path)
+    uint32_t next_helpers;    // fused: the next bitmap's pass-independent items go to the workgroups past the
+                              // predicted cut, after their look-back (1, default), or to every workgroup
+                              // while it publishes (0; ABNN_NEXT_HELPERS)
+    uint32_t lds_tail;        // fused: a range's last refractory stage keeps its survivors in LDS for the
+                              // walk (1, default; ABNN_LDS_TAIL=0: in g2x like the others)
+    uint32_t wt_sc1;          // weight stores write-through (sc1) instead of non-temporal (ABNN_WT_SC1)
     uint32_t shard_mode;      // fused pass = the first launch of a sharded pass (k_gate: no stamps, exchange record)
     int32_t* xchg;            // ... its exchange record (abnn.h: summary + local spike list)
     uint32_t prologue_adapt;  // the previous pass was fused over the same ranges: its costs move the next

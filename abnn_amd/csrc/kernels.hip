@@ -130,6 +130,17 @@ __device__ __forceinline__ void set_src(const SynArrays& a, uint64_t i, uint32_t
     if (a.src32) a.src32[i] = v;
 }
 
+// A weight store (brain.metal:122).  Non-temporal by default: a plain 4-B
+// store leaves scattered dirty partial lines whose write-back lands in the
+// middle of the next pass's record stream.  wt_sc1: write-through (sc1) --
+// the line leaves the XCD's L2 at once instead of at the kernel's end.
+__device__ __forceinline__ void store_w(const DeviceState& d, uint64_t i, float w)
+{
+    float* p = w_ptr(d.syn, i);
+    if (d.wt_sc1) __hip_atomic_store((gu32*)p, __float_as_uint(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __builtin_nontemporal_store(w, p);
+}
+
 // Record visited by local event t: itself (sweep, brain.metal:70) or its pick.
 __device__ __forceinline__ uint64_t rec_index(const DeviceState& d, uint64_t t, uint64_t pass)
 {
@@ -487,7 +498,7 @@ template <int R, bool kRandom, bool kFused, bool kTail, class At>
 __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const KernelParams& kp, uint64_t region,
                                               uint64_t base, uint32_t n, uint64_t now, uint64_t pass, float Rw,
                                               float rbw, bool spec, uint32_t crange, uint32_t c0,
-                                              const uint32_t* s_f2, At&& at)
+                                              const uint32_t* s_f2, At&& at, uint4* lds_out = nullptr)
 {
     const uint32_t lane = threadIdx.x & 63, nn = (uint32_t)d.n_nrn;
     uint32_t n_g1 = 0, n_g2 = 0, n_cand = 0;
@@ -581,12 +592,20 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
                 const uint64_t o = base + n_g2 + mbcnt64(bg);
                 if constexpr (kFused) {
                     const float wn = updated_weight(kp, w[j], cand, Rw, rbw, (float)age32(now, ld[j]));
-                    d.g2x[o] = make_uint4(rel[j] | (cand ? 0x80000000u : 0u), __float_as_uint(w[j]),
-                                          __float_as_uint(wn), dst[j]);
-                    if (spec) __builtin_nontemporal_store(wn, w_ptr(d.syn, region + rel[j]));  // brain.metal:122
-                    const uint32_t ci = c0 + n_cand + mbcnt64(bcd);  // the range's candidate index
-                    if (cand && ci < kCandCap)
-                        d.cand_list[crange * kCandCap + ci] = make_uint2((uint32_t)(base - region) + n_g2 + mbcnt64(bg), dst[j]);
+                    const uint4 ent = make_uint4(rel[j] | (cand ? 0x80000000u : 0u), __float_as_uint(w[j]),
+                                                 __float_as_uint(wn), dst[j]);
+                    if (kTail && lds_out) {
+                        // the fused tail keeps its survivors in LDS (fused_end's
+                        // walk reads them there, and stores the weights)
+                        lds_out[n_g2 + mbcnt64(bg)] = ent;
+                    } else {
+                        d.g2x[o] = ent;
+                        if (spec) store_w(d, region + rel[j], wn);  // brain.metal:122
+                        const uint32_t ci = c0 + n_cand + mbcnt64(bcd);  // the range's candidate index
+                        if (cand && ci < kCandCap)
+                            d.cand_list[crange * kCandCap + ci] =
+                                make_uint2((uint32_t)(base - region) + n_g2 + mbcnt64(bg), dst[j]);
+                    }
                 } else {
                     const uint32_t isi = __float_as_uint((float)age32(now, ld[j])) | (cand ? 0x80000000u : 0u);
                     d.g2x[o] = make_uint4(rel[j], isi, __float_as_uint(w[j]), dst[j]);
@@ -621,6 +640,8 @@ struct ApplyCtx {
     bool prune, genesis;
     bool precomputed;  // the entry holds the updated weight (fused pass: refrac_chunk<..., kFused>)
     uint32_t upd, nf, npr;
+    uint32_t* lds_spk = nullptr;  // fused pass: the workgroup's spikes also go to LDS (fused_end stamps
+    uint32_t lds_s0 = 0;          // them from there), budget position pre at lds_spk[pre - lds_s0]
 };
 
 // A spike of the pass (brain.metal:125-126): stamp (k_apply), the spike list
@@ -629,6 +650,7 @@ __device__ __forceinline__ void record_spike(const DeviceState& d, const KernelP
                                              const uint4& e, uint64_t pre, uint64_t slot)
 {
     if (c.stamp) d.last_fired[e.w] = c.now;  // brain.metal:125-126
+    if (c.lds_spk) c.lds_spk[pre - c.lds_s0] = e.w;
     if (c.ring) {
         uint32_t* q = d.fired_ring + (c.pass & (kFiredRing - 1)) * kp.max_spikes + pre;
         if (c.ring_sc1) __hip_atomic_store((gu32*)q, e.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -667,7 +689,7 @@ __device__ __forceinline__ void apply_event(const DeviceState& d, const KernelPa
         if (d.dead) atomicAdd(d.dead + ri / kCompactChunk, 1u);  // tally for the structural update
         ++c.npr;
     } else if (store) {
-        __builtin_nontemporal_store(w, w_ptr(d.syn, ri));
+        store_w(d, ri, w);
     }
     ++c.upd;
     if (f) record_spike(d, kp, c, e, pre, slot);
@@ -723,22 +745,37 @@ constexpr uint32_t kLbMaxWords = 8;  // look-back words per lane: gate_blocks <=
 // One wave sweeps the words of workgroups [0, n): their values (capped sum)
 // once all carry `tag`, or as soon as the published ones reach the budget
 // (stop_at_budget).  vals: this lane's words (q = 64 i + lane), for the caller.
+// pub != 0: this workgroup's own word, published by lane 0 right after the
+// first sweep's loads are issued (a load issued after a store waits for it:
+// vmcnt counts both, in order).
 __device__ uint32_t wg_poll(const DeviceState& d, uint32_t n, uint32_t tag, uint32_t budget, bool stop_at_budget,
-                            uint32_t (&vals)[kLbMaxWords])
+                            uint32_t (&vals)[kLbMaxWords], uint64_t pub = 0)
 {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t spins = 0;; ++spins) {  // wave-uniform
         uint64_t sum = 0;
         bool ok = true;
+        uint64_t raw[kLbMaxWords];
+#pragma unroll
+        for (uint32_t i = 0; i < kLbMaxWords; ++i) {
+            const uint32_t q = i * 64 + lane;
+            raw[i] = 0;
+            if (i * 64 < n && q < n)
+                raw[i] = __hip_atomic_load((gu64*)(d.lb_status + q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (pub && spins == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (lane == 0)
+                __hip_atomic_store((gu64*)(d.lb_status + blockIdx.x), pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (uint32_t i = 0; i < kLbMaxWords; ++i) {
             const uint32_t q = i * 64 + lane;
             vals[i] = 0u;
             if (i * 64 < n && q < n) {
-                const uint64_t s = __hip_atomic_load((gu64*)(d.lb_status + q), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                const bool mine = (uint32_t)(s >> 32) == tag;
-                vals[i] = mine ? (uint32_t)s & 0x3FFFFFFFu : 0u;
+                const bool mine = (uint32_t)(raw[i] >> 32) == tag;
+                vals[i] = mine ? (uint32_t)raw[i] & 0x3FFFFFFFu : 0u;
                 sum += vals[i];
                 ok = ok && mine;
             }
@@ -848,13 +885,18 @@ __device__ __forceinline__ uint32_t range_walk(const DeviceState& d, const Kerne
         upd_rest = C < k ? S : wave_uniform(cl[k - 1].x) + 1u;
         for (uint32_t q = upd_rest + lane; q < S; q += 64) {  // mispredicted tail: w stays (brain.metal:85-88)
             const uint2 x = *reinterpret_cast<const uint2*>(d.g2x + region + q);  // {offset | cand, w}
-            __builtin_nontemporal_store(__uint_as_float(x.y), w_ptr(d.syn, region + (x.x & 0x7FFFFFFFu)));
+            store_w(d, region + (x.x & 0x7FFFFFFFu), __uint_as_float(x.y));
         }
     }
-    const bool walk = !listed && (spec ? !(C == 0 && P < budget) : P < budget);
-    if (walk) load_batch(0, e);
-    else if (spec && !listed) upd_rest = S;
-    for (uint32_t b0 = 0; walk && b0 < S; b0 += RW * 64) {  // wave-uniform
+    const bool walk = !listed && (spec ? !(C == 0 && P < budget) : P < budget) && S > 0;
+    if (!walk && spec && !listed) upd_rest = S;
+    if (!walk) return upd_rest;
+    // (every load issued here is consumed before the function returns: a
+    // load left pending would make the compiler wait for it -- and, vmcnt
+    // being in order, for every store before it -- where the walk paths
+    // merge, on every path, the LDS-only ones included)
+    load_batch(0, e);
+    for (uint32_t b0 = 0; b0 < S; b0 += RW * 64) {  // wave-uniform
         if (!spec && P >= budget) break;
         if (spec && P < budget && seen == C) {
             upd_rest = S - b0;
@@ -877,7 +919,7 @@ __device__ __forceinline__ uint32_t range_walk(const DeviceState& d, const Kerne
                 ++ac.upd;
                 if (cand) record_spike(d, kp, ac, x, pre, region + q);
             } else if (v) {  // mispredicted: past the budget, w stays (brain.metal:85-88)
-                __builtin_nontemporal_store(__uint_as_float(x.y), w_ptr(d.syn, region + x.x));
+                store_w(d, region + x.x, __uint_as_float(x.y));
             }
             if (set_next) wave_set_next_dedup(d, cand && pre < budget, x.w, setc);  // this pass's spikes
             P += (uint64_t)__popcll(bc);
@@ -886,7 +928,31 @@ __device__ __forceinline__ uint32_t range_walk(const DeviceState& d, const Kerne
 #pragma unroll
         for (uint32_t j = 0; j < RW; ++j) e[j] = en[j];
     }
+#pragma unroll
+    for (uint32_t j = 0; j < RW; ++j) asm volatile("" ::"v"(e[j].x), "v"(e[j].y), "v"(e[j].z), "v"(e[j].w));
     return upd_rest;
+}
+
+// The fused tail's survivors (refrac_chunk lds_out: S entries {offset |
+// candidate << 31, w, updated w, dst} in LDS, event order) from budget
+// position P: the ordered budget (brain.metal:85-98), the weight stores of the
+// ones below it (brain.metal:122; nothing was stored speculatively for them)
+// and their spikes.  LDS only: no load waits behind the wave's stores.
+__device__ __forceinline__ void lds_walk(const DeviceState& d, const KernelParams& kp, ApplyCtx& ac, uint64_t region,
+                                         const uint4* e, uint32_t S, uint64_t P, bool set_next, uint64_t* setc)
+{
+    const uint32_t lane = threadIdx.x & 63, budget = kp.max_spikes;
+    for (uint32_t q0 = 0; q0 < S && P < budget; q0 += 64) {  // wave-uniform
+        const uint32_t q = q0 + lane;
+        const bool v = q < S;
+        const uint4 x = v ? e[q] : make_uint4(0u, 0u, 0u, 0u);
+        const bool cand = v && (x.x >> 31);
+        const uint64_t bc = __ballot(cand);
+        const uint64_t pre = P + mbcnt64(bc);
+        if (v && pre < budget) apply_event(d, kp, ac, region, make_uint4(x.x & 0x7FFFFFFFu, x.y, x.z, x.w), cand, pre, 0);
+        if (set_next) wave_set_next_dedup(d, cand && pre < budget, x.w, setc);  // this pass's spikes
+        P += (uint64_t)__popcll(bc);
+    }
 }
 
 // Sharded pass, first launch: the dst of this range's spike candidates whose
@@ -948,63 +1014,77 @@ struct FusedLds {
     uint32_t sg2;                      // sharded pass: the workgroup's refractory survivors
 };
 
-// Fused pass: range r's wave after its refractory stage (g1 pre-gated, S
-// survivors -- contiguous from g2x[region] -- and C spike candidates; its
-// stream took `stream_cost` 40-ns units, the next pass's partition cost): the
-// next partition (first wave of the workgroup), its share of the next bitmap
-// build, the workgroup look-back, the walk of its own survivors, statistics,
-// the stamps of the workgroup's spikes once every refractory stage of the
-// pass is done, and (workgroup 0) the pass's end.  Pass-start scalars (C1) as
-// read at kernel entry.
+// Fused pass: range r's wave after its refractory stage (g1 pre-gated; Sg
+// survivors contiguous from g2x[region] with Cg spike candidates among them,
+// then -- when the tail kept them in LDS, tl -- St more at tl with Ct
+// candidates; its stream took `stream_cost` 40-ns units, the next pass's
+// partition cost): the next partition (first wave of the workgroup), its share
+// of the next bitmap build, the workgroup look-back, the walk of its own
+// survivors, statistics, the stamps of the workgroup's spikes once every
+// refractory stage of the pass is done, and (workgroup 0) the pass's end.
+// Pass-start scalars (C1) as read at kernel entry.
+//
+// gfx9's vmcnt counts loads and stores in issue order, so a load waits for
+// every store the wave issued before it.  The path from the last refractory
+// stage to the pass's end therefore issues no load behind a store where it
+// can: the look-back's first sweep is issued before the publishing store, the
+// tail's survivors and the workgroup's spikes stay in LDS, LDS-only barriers,
+// and wave 0 sees every word published before it walks (and stores).
 template <int BLOCK, int NW>
-__device__ __forceinline__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region, uint32_t g1,
-                          uint32_t S, uint32_t C, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
-                          float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L, uint64_t t_stream)
+__device__ __forceinline__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region,
+                                          uint32_t g1, uint32_t Sg, uint32_t Cg, uint32_t St, uint32_t Ct,
+                                          const uint4* tl, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
+                                          float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L,
+                                          uint64_t t_stream, uint32_t h0, uint32_t chunk_t, uint32_t nch,
+                                          uint64_t* wcb)
 {
-    constexpr uint32_t RW = 4;  // rounds of survivors per walk batch (two batches in flight)
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
     const uint32_t tag = epoch + 1u;
     const uint64_t t_tail = __builtin_amdgcn_s_memrealtime();
+    const uint32_t S = Sg + St, C = Cg + Ct;  // the range's survivors and spike candidates
     uint32_t order = 0;
     if (lane == 0) {
         L.cand[wid] = C < budget ? C : budget;
         if (d.shard_mode) atomicAdd(&L.sg2, S);
-        const uint32_t cost = stream_cost;
-        d.cost_out[r] = empty ? 0u : (cost < 1 ? 1u : (cost > 0xFFFFu ? 0xFFFFu : cost));
         order = atomicAdd(&L.done, 1u);
     }
     if (wave_uniform(order) == 0) fused_next_bounds<NW>(d, L.cc);
     lds_barrier();  // every range of the workgroup through its refractory stage
     uint32_t vals[kLbMaxWords];
-    if (wid != 0 && d.build_next) {
-        // while wave 0 publishes and polls: the workgroup's share of the next
-        // pass's bitmap build that does not depend on this pass (the spike
-        // lists of passes p+1-W..p-1, the stimulus), item x to workgroup
-        // x % G -- after the publication, so that it never delays a look-back
-        // word (the bitmap is read by the next pass only)
-        const uint64_t nitems = next_items(d, kp), G = gridDim.x;
-        for (uint64_t s0 = (uint64_t)(wid - 1) * 64; s0 * G + blockIdx.x < nitems; s0 += (uint64_t)(NW - 1) * 64) {
-            const uint64_t x = (s0 + lane) * G + blockIdx.x;  // wave-uniform trip count (lane 0's item)
+    // The next pass's bitmap build items that do not depend on this pass (the
+    // spike lists of passes p+1-W..p-1, the stimulus): item x to workgroup
+    // h0 + x % (G - h0), by waves [w0, NW) of it.  With h0 > 0 only the
+    // workgroups past the predicted budget cut take them, after their
+    // look-back (they have no walk); with h0 = 0 every workgroup's waves 1..
+    // take them while wave 0 publishes and polls.
+    auto next_share = [&](uint32_t w0) {
+        const uint64_t nitems = next_items(d, kp), HG = gridDim.x - h0, hb = blockIdx.x - h0;
+        for (uint64_t s0 = (uint64_t)(wid - w0) * 64; s0 * HG + hb < nitems; s0 += (uint64_t)(NW - w0) * 64) {
+            const uint64_t x = (s0 + lane) * HG + hb;  // wave-uniform trip count (lane 0's item)
             const NextItem it = x < nitems ? next_item_load(d, kp, pass, x) : NextItem{0u, 0u, 0u};
             wave_set_next_dedup(d, it.i < it.lim, it.n, L.setc);
         }
-    }
+    };
+    if (h0 == 0 && wid != 0 && d.build_next) next_share(1);
     if (wid == 0) {
         uint32_t c = lane < (uint32_t)NW ? L.cand[lane] : 0u;
         c = wave_sum(c);
-        if (lane == 0 && d.shard_mode) {
+        const uint64_t word = (uint64_t)tag << 32 | (uint64_t)kLbAggregate << 30 | (c < budget ? c : budget);
+        uint32_t e;
+        if (d.shard_mode) {
             // the pass's refractory survivors for the exchange summary: added
             // before this workgroup's word is published (workgroup 0 sums
             // them once every word is)
-            __hip_atomic_fetch_add(&d.work->shard_g2, (unsigned long long)L.sg2, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                __hip_atomic_fetch_add(&d.work->shard_g2, (unsigned long long)L.sg2, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store((gu64*)(d.lb_status + blockIdx.x), word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            e = wg_poll(d, blockIdx.x, tag, budget, true, vals);
+        } else {
+            e = wg_poll(d, blockIdx.x, tag, budget, true, vals, word);
         }
-        if (lane == 0)
-            __hip_atomic_store((gu64*)(d.lb_status + blockIdx.x),
-                               (uint64_t)tag << 32 | (uint64_t)kLbAggregate << 30 | (c < budget ? c : budget),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t e = wg_poll(d, blockIdx.x, tag, budget, true, vals);
         if (lane == 0) L.excl = e;
     }
     lds_barrier();
@@ -1016,12 +1096,52 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         c_wg += L.cand[w];
     }
     const uint64_t t_lb = __builtin_amdgcn_s_memrealtime();
+    // the workgroup's spikes: budget positions [s0, s1) of the spike list
+    const uint32_t s0 = excl_wg, s1 = (uint32_t)(excl_wg + c_wg < budget ? excl_wg + c_wg : budget);
+    const bool first = blockIdx.x == 0;
+    const bool stamping = !d.shard_mode && (s1 > s0 || first);
+    // the spikes go to LDS too (L.cc: the partition's cost prefix is done)
+    // unless the budget is larger than it
+    const bool spk_lds = !d.shard_mode && budget <= kFusedMaxRanges;
+    // every workgroup's word published = every refractory stage of the pass
+    // done: no lastFired read is left, the stamps may land.  Wave 0 waits for
+    // that before its walk (its loads then wait for no store of the walk).
+    uint32_t tot = 0, t0 = 0;
+    if (wid == 0 && stamping) {
+        tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
+        if (first) {
+            // the next pass's prediction (refrac_chunk's spec): the workgroups
+            // below the one where the budget ran out, less one
+            uint32_t run = 0, cut = gridDim.x;
+#pragma unroll
+            for (uint32_t i = 0; i < kLbMaxWords; ++i) {
+                const uint32_t inc = wave_incl_scan(vals[i]) + run;  // prefix through word 64 i + lane
+                const uint64_t hit = __ballot(inc >= budget && inc - vals[i] < budget);
+                if (hit && cut == gridDim.x) cut = i * 64 + (uint32_t)__builtin_ctzll(hit);
+                run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            }
+            // the event-0 flag (refrac_chunk): stored and drained before its
+            // workgroup's word was published
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            t0 = __hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("" ::"v"(t0));  // consumed here, before any store of the walk (see range_walk)
+            if (lane == 0) d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
+        }
+    }
+    const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
     // the budget walk of k_apply over this range alone, in event order
     ApplyCtx ac{R, rb, now, pass, false, false, true, false, kp.w_prune > 0.0f, d.grown != nullptr && kp.p_new > 0.0f,
                 true, 0u, 0u, 0u};
+    if (spk_lds) {
+        ac.lds_spk = L.cc;
+        ac.lds_s0 = s0;
+    }
     uint32_t upd_rest = 0;
+    uint64_t t_rw = 0;
     if (!d.shard_mode) {
-        upd_rest = range_walk(d, kp, ac, r, region, S, C, P, spec, d.build_next != 0, L.setc);
+        upd_rest = range_walk(d, kp, ac, r, region, Sg, Cg, P, spec, d.build_next != 0, L.setc);
+        t_rw = __builtin_amdgcn_s_memrealtime();
+        if (tl) lds_walk(d, kp, ac, region, tl, St, P + Cg, d.build_next != 0, L.setc);
     } else {
         // sharded pass (the first of its two launches): the global budget
         // offset is unknown until the exchange, so this range's local budget
@@ -1032,6 +1152,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
             d.range_info[r] = make_uint4((uint32_t)(P < budget ? P : budget), S, C, (spec ? 1u : 0u) | (empty ? 2u : 0u));
         range_spikes_local(d, kp, r, region, S, C, P, d.xchg + 2 * ABNN_SUMMARY_WORDS);
     }
+    if (h0 > 0 && blockIdx.x >= h0 && d.build_next) next_share(0);
     const uint64_t t_walk = __builtin_amdgcn_s_memrealtime();
     const uint32_t wu = wave_sum(ac.upd) + upd_rest, wf = wave_sum(ac.nf), wp = wave_sum(ac.npr);
     if (lane == 0) {
@@ -1040,22 +1161,24 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         atomicAdd(&L.stat[2], wu);
         atomicAdd(&L.stat[3], wf);
         atomicAdd(&L.stat[4], wp);
-        uint64_t* wc = d.wave_clock + (uint64_t)kWaveClock * r;  // diagnostics (tools/wave_clock.py)
+        d.cost_out[r] = empty ? 0u : (stream_cost < 1 ? 1u : (stream_cost > 0xFFFFu ? 0xFFFFu : stream_cost));
+        uint64_t* wc = wcb + (uint64_t)kWaveClock * r;  // diagnostics (tools/wave_clock.py)
         wc[1] = t_stream;  // wc[0], wc[3]: stored by k_gate at the stream's start
         wc[2] = t_tail;
         wc[4] = t_lb;
         wc[5] = t_walk;
+        wc[6] = chunk_t;
+        wc[7] = nch;
         wc[8] = S;
         wc[9] = C;
         wc[10] = excl_wg;
         wc[11] = wu;
+        if (wid == 0) wc[12] = stamping ? t_seen : 0;
+        wc[14] = t_rw;  // range_walk done (then the LDS tail's walk, the helpers' items: t_walk)
     }
-    // the workgroup's spikes: budget positions [s0, s1) of the spike list,
-    // written by its waves (plain stores: this workgroup reads them, behind
-    // the barrier's workgroup-scope fence)
-    const uint32_t s0 = excl_wg, s1 = (uint32_t)(excl_wg + c_wg < budget ? excl_wg + c_wg : budget);
-    const bool first = blockIdx.x == 0;
-    __syncthreads();
+    // LDS only (the statistics, the LDS spike list): the walks' stores stay in flight
+    if (d.shard_mode || (stamping && !spk_lds)) __syncthreads();
+    else lds_barrier();
     if (threadIdx.x == 0) {
         typedef unsigned long long ull;
         abnn_stats* st = d.wg_stats + blockIdx.x % kWalkBlocks;
@@ -1074,10 +1197,10 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         // exchange); workgroup 0 writes the exchange summary (abnn.h) once
         // every word is published
         if (!first || wid != 0) return;
-        const uint32_t tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
+        const uint32_t tt = wg_poll(d, gridDim.x, tag, budget, false, vals);
         if (lane == 0) {
             int64_t* sm = reinterpret_cast<int64_t*>(d.xchg);
-            sm[0] = (int64_t)tot;  // candidates, capped at the budget
+            sm[0] = (int64_t)tt;  // candidates, capped at the budget
             sm[1] = (int64_t)__hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             sm[2] = (int64_t)d.events;
             sm[3] = (int64_t)__hip_atomic_load(&d.work->shard_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1086,45 +1209,23 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         }
         return;
     }
-    uint64_t* wc0 = d.wave_clock + (uint64_t)kWaveClock * r;  // diagnostics, wave 0: all words seen, exit
-    if (s1 <= s0 && !first) {  // workgroup-uniform: nothing to stamp
-        if (threadIdx.x == 0) {
-            wc0[12] = 0;
-            wc0[13] = __builtin_amdgcn_s_memrealtime();
-        }
-        return;
-    }
-    // every workgroup's word published = every refractory stage of the pass
-    // done: no lastFired read is left, the stamps may land
-    if (wid == 0) {
-        const uint32_t tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
-        if (first) {
-            // the next pass's prediction (refrac_chunk's spec): the workgroups
-            // below the one where the budget ran out, less one
-            uint32_t run = 0, cut = gridDim.x;
-#pragma unroll
-            for (uint32_t i = 0; i < kLbMaxWords; ++i) {
-                const uint32_t inc = wave_incl_scan(vals[i]) + run;  // prefix through word 64 i + lane
-                const uint64_t hit = __ballot(inc >= budget && inc - vals[i] < budget);
-                if (hit && cut == gridDim.x) cut = i * 64 + (uint32_t)__builtin_ctzll(hit);
-                run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    uint64_t* wc0 = wcb + (uint64_t)kWaveClock * r;  // diagnostics, wave 0: exit
+    if (stamping) {
+        if (spk_lds) {
+            for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
+                const uint32_t nrn = L.cc[i - s0];
+                if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
             }
-            if (lane == 0) {
-                L.total = tot;
-                d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
+        } else {
+            const uint32_t* ring = d.fired_ring + (pass & (kFiredRing - 1)) * (uint64_t)budget;
+            for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
+                const uint32_t nrn = ring[i];
+                if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
             }
         }
-    }
-    if (threadIdx.x == 0) wc0[12] = __builtin_amdgcn_s_memrealtime();
-    lds_barrier();
-    const uint32_t* ring = d.fired_ring + (pass & (kFiredRing - 1)) * (uint64_t)budget;
-    for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
-        const uint32_t nrn = ring[i];
-        if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
     }
     if (first && threadIdx.x == 0) {  // the pass's end: every workgroup has read the pass-start scalars
-        d.n_fired_ring[pass & (kFiredRing - 1)] = L.total;
-        const uint32_t t0 = __hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        d.n_fired_ring[pass & (kFiredRing - 1)] = tot;
         if (t0 != 0u && budget > 0) *d.rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
         *d.clock = now + kp.clock_inc;                                        // brain.metal:129
         *d.pass_index = pass + 1;
@@ -1180,7 +1281,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     static_assert(!(kFused && kRandom), "the fused pass is sweep-mode only");
     __shared__ uint2 s_fb[FW];  // the filter's FW 64-bit blocks
     __shared__ uint32_t s_f2[kF2Words];  // the second-level filter (refrac_chunk)
-    __shared__ uint32_t s_off[NW][SE], s_src[NW][SE];
+    // a wave's stage: SE offsets, then SE codes (one 8-SE-byte block, so the
+    // fused tail can reuse it for its survivors, refrac_chunk lds_out)
+    __shared__ uint32_t s_stage[NW][2 * SE];
     __shared__ FusedLds<NW> s_fz;            // fused: the pass end's workgroup state
 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1233,10 +1336,15 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // have to undo too)
     const uint64_t pass_f = kFused ? sload(d.pass_index) : 0;
     const uint32_t epoch = kFused ? sload(&d.work->epoch) : 0u;
-    const bool spec = kFused && !(kp.w_prune > 0.0f) &&
-                      (d.spec_mode == 2 || (d.spec_mode == 1 && blockIdx.x < sload(&d.work->spec_wgs)));
-    uint32_t* st_off = s_off[wid];
-    uint32_t* st_src = s_src[wid];
+    const uint32_t spec_wgs = kFused ? sload(&d.work->spec_wgs) : 0u;
+    const bool spec = kFused && !(kp.w_prune > 0.0f) && (d.spec_mode == 2 || (d.spec_mode == 1 && blockIdx.x < spec_wgs));
+    // fused: the first workgroup past the predicted cut (spec_wgs = cut - 1)
+    // and a margin -- the ones from it on take the next bitmap's
+    // pass-independent items (fused_end); 0: every workgroup does
+    uint32_t hw0 = 0;
+    if (kFused && d.next_helpers && !d.shard_mode && spec_wgs + 3u + gridDim.x / 4u <= gridDim.x) hw0 = spec_wgs + 3u;
+    uint32_t* st_off = s_stage[wid];
+    uint32_t* st_src = s_stage[wid] + SE;
     // Records in flight.  Sweep: the packed src stream (engine.h, SynArrays):
     // per 256-event group g a lane holds two lo words (events 128 kh + 2 lane
     // + {0, 1}, kh = 0, 1) and one hi word (the same four events' bits
@@ -1310,9 +1418,12 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // (zeroing, stimulus) and the first records stay in flight
     lds_barrier();
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) {  // diagnostics (tools/wave_clock.py): stored now, not held through the stream
-        d.wave_clock[kWaveClock * r] = t_start;
-        d.wave_clock[kWaveClock * r + 3] = t_entry;
+    // diagnostics (tools/wave_clock.py): the fused pass keeps the last
+    // kWaveClockPasses passes' clocks (slot pass % kWaveClockPasses)
+    uint64_t* wcb = d.wave_clock + (kFused ? (pass_f % kWaveClockPasses) * (uint64_t)kWaveClock * kMaxRanges : 0);
+    if (lane == 0) {  // stored now, not held through the stream
+        wcb[kWaveClock * r] = t_start;
+        wcb[kWaveClock * r + 3] = t_entry;
     }
     const uint64_t len = it_end - it_begin;
 
@@ -1500,7 +1611,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             if (it + 1 < it_end) step(B, it + 1);
     }
     const uint64_t t_stream = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) {  // diagnostics (tools/wave_clock.py)
+    if (!kFused && lane == 0) {  // diagnostics (tools/wave_clock.py; the fused pass stores them in fused_end)
         d.wave_clock[kWaveClock * r + 6] = chunk_t;
         d.wave_clock[kWaveClock * r + 7] = nch;
     }
@@ -1509,8 +1620,16 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     if (d.tail_prio < 4) set_priority(d.tail_prio);
     // the range's last chunk: refractory stage by this wave
     const uint64_t tb = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
+    // fused, single GPU, no synaptogenesis (its src list is global): the
+    // tail's survivors stay in the stage's LDS (its entries are all read
+    // before the first survivor is written: pend <= 256 <= one batch)
+    uint4* tail_lds = nullptr;
+    if constexpr (kFused) {
+        static_assert(2 * SE * 4 >= 256 * sizeof(uint4), "the stage holds 256 tail survivors");
+        if (d.lds_tail && !d.shard_mode && !d.g2src && pend <= 256u) tail_lds = reinterpret_cast<uint4*>(s_stage[wid]);
+    }
     const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, true>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
-                                                               r, tot.z, s_f2, stage_at);
+                                                               r, tot.z, s_f2, stage_at, tail_lds);
     const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
     const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
     if constexpr (kFused) {
@@ -1518,8 +1637,10 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // partition balances that (the tail's length follows the range's
         // staged events)
         const uint64_t gf = d.cost_tail ? ((__builtin_amdgcn_s_memrealtime() - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty : gt;
-        fused_end<BLOCK, NW>(d, kp, r, region, tot.x + c.x, tot.y + c.y, tot.z + c.z, (uint32_t)gf, len == 0, spec,
-                             now, Rw, rbw, pass_f, epoch, s_fz, t_stream);
+        const bool tl = tail_lds != nullptr;
+        fused_end<BLOCK, NW>(d, kp, r, region, tot.x + c.x, tl ? tot.y : tot.y + c.y, tl ? tot.z : tot.z + c.z,
+                             tl ? c.y : 0u, tl ? c.z : 0u, tail_lds, (uint32_t)gf, len == 0, spec, now, Rw, rbw, pass_f,
+                             epoch, s_fz, t_stream, hw0, chunk_t, nch, wcb);
         return;
     }
     if (lane == 0) {

@@ -17,6 +17,9 @@ extern "C" {
 /* The last pass's per-wave gate timeline: 12 u64 per range (100-MHz ticks:
  * start, stream done, tail done, entry, look-back done, walk done, ...). */
 abnn_status abnn_debug_wave_clock(abnn_brain* b, uint64_t* out, uint64_t n);
+/* The same for pass p of the fused single-GPU pass, slot = p % 8 (the last
+ * eight fused passes are kept). */
+abnn_status abnn_debug_wave_clock_slot(abnn_brain* b, uint32_t slot, uint64_t* out, uint64_t n);
 /* The last two-kernel pass's per-workgroup k_apply timeline, 8 u64 each. */
 abnn_status abnn_debug_apply_clock(abnn_brain* b, uint64_t* out, uint64_t n);
 /* The recent-spike bitmap the last pass read (bit i: neuron i recent at its
