@@ -873,6 +873,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.flush_at = kChunk;
     if (const char* env = std::getenv("ABNN_FLUSH_AT"))
         d.flush_at = (uint32_t)std::min<int>((int)kChunk, std::max(64, std::atoi(env)));
+    d.lean = 1;
+    if (const char* env = std::getenv("ABNN_LEAN")) d.lean = std::atoi(env) != 0;
     d.wt_sc1 = 0;
     if (const char* env = std::getenv("ABNN_WT_SC1")) d.wt_sc1 = std::atoi(env) != 0;
     d.lds_tail = 1;

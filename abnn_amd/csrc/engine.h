@@ -181,6 +181,7 @@ struct DeviceState {
                               // while it publishes (0; ABNN_NEXT_HELPERS)
     uint32_t lds_tail;        // fused: a range's last refractory stage keeps its survivors in LDS for the
                               // walk (1, default; ABNN_LDS_TAIL=0: in g2x like the others)
+    uint32_t lean;            // fused single-GPU pass without plasticity: the lean kernel (ABNN_LEAN, default 1)
     uint32_t wt_sc1;          // weight stores write-through (sc1) instead of non-temporal (ABNN_WT_SC1)
     uint32_t shard_mode;      // fused pass = the first launch of a sharded pass (k_gate: no stamps, exchange record)
     int32_t* xchg;            // ... its exchange record (abnn.h: summary + local spike list)

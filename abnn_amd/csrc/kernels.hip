@@ -673,7 +673,7 @@ __device__ __forceinline__ void apply_event(const DeviceState& d, const KernelPa
 {
     const float w = c.precomputed ? __uint_as_float(e.z)
                                   : updated_weight(kp, __uint_as_float(e.z), f, c.R, c.rb, __uint_as_float(e.y & 0x7FFFFFFFu));
-    const uint64_t t = region + e.x, ri = rec_index(d, t, c.pass);
+    const uint64_t t = region + e.x, ri = c.random ? rec_index(d, t, c.pass) : t;
     // random mode: of the events that updated one synapse this pass, the
     // highest (k_claim) stores its weight; every one of them still counts
     const bool store = !c.random || d.claim[ri] == (uint32_t)(t + 1);
@@ -1030,7 +1030,7 @@ struct FusedLds {
 // can: the look-back's first sweep is issued before the publishing store, the
 // tail's survivors and the workgroup's spikes stay in LDS, LDS-only barriers,
 // and wave 0 sees every word published before it walks (and stores).
-template <int BLOCK, int NW>
+template <int BLOCK, int NW, bool kLean>
 __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region,
                                           uint32_t g1, uint32_t Sg, uint32_t Cg, uint32_t St, uint32_t Ct,
                                           const uint4* tl, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
@@ -1040,12 +1040,15 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
 {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
     const uint32_t tag = epoch + 1u;
+    // kLean: the single-GPU pass without plasticity (less code: the end of
+    // the pass runs from a cold instruction cache)
+    const bool shard = !kLean && d.shard_mode;
     const uint64_t t_tail = __builtin_amdgcn_s_memrealtime();
     const uint32_t S = Sg + St, C = Cg + Ct;  // the range's survivors and spike candidates
     uint32_t order = 0;
     if (lane == 0) {
         L.cand[wid] = C < budget ? C : budget;
-        if (d.shard_mode) atomicAdd(&L.sg2, S);
+        if (shard) atomicAdd(&L.sg2, S);
         order = atomicAdd(&L.done, 1u);
     }
     if (wave_uniform(order) == 0) fused_next_bounds<NW>(d, L.cc);
@@ -1071,7 +1074,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         c = wave_sum(c);
         const uint64_t word = (uint64_t)tag << 32 | (uint64_t)kLbAggregate << 30 | (c < budget ? c : budget);
         uint32_t e;
-        if (d.shard_mode) {
+        if (shard) {
             // the pass's refractory survivors for the exchange summary: added
             // before this workgroup's word is published (workgroup 0 sums
             // them once every word is)
@@ -1099,10 +1102,10 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     // the workgroup's spikes: budget positions [s0, s1) of the spike list
     const uint32_t s0 = excl_wg, s1 = (uint32_t)(excl_wg + c_wg < budget ? excl_wg + c_wg : budget);
     const bool first = blockIdx.x == 0;
-    const bool stamping = !d.shard_mode && (s1 > s0 || first);
+    const bool stamping = !shard && (s1 > s0 || first);
     // the spikes go to LDS too (L.cc: the partition's cost prefix is done)
     // unless the budget is larger than it
-    const bool spk_lds = !d.shard_mode && budget <= kFusedMaxRanges;
+    const bool spk_lds = !shard && budget <= kFusedMaxRanges;
     // every workgroup's word published = every refractory stage of the pass
     // done: no lastFired read is left, the stamps may land.  Wave 0 waits for
     // that before its walk (its loads then wait for no store of the walk).
@@ -1130,15 +1133,15 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     }
     const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
     // the budget walk of k_apply over this range alone, in event order
-    ApplyCtx ac{R, rb, now, pass, false, false, true, false, kp.w_prune > 0.0f, d.grown != nullptr && kp.p_new > 0.0f,
-                true, 0u, 0u, 0u};
+    ApplyCtx ac{R, rb, now, pass, false, false, true, false, !kLean && kp.w_prune > 0.0f,
+                !kLean && d.grown != nullptr && kp.p_new > 0.0f, true, 0u, 0u, 0u};
     if (spk_lds) {
         ac.lds_spk = L.cc;
         ac.lds_s0 = s0;
     }
     uint32_t upd_rest = 0;
     uint64_t t_rw = 0;
-    if (!d.shard_mode) {
+    if (!shard) {
         upd_rest = range_walk(d, kp, ac, r, region, Sg, Cg, P, spec, d.build_next != 0, L.setc);
         t_rw = __builtin_amdgcn_s_memrealtime();
         if (tl) lds_walk(d, kp, ac, region, tl, St, P + Cg, d.build_next != 0, L.setc);
@@ -1177,7 +1180,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         wc[14] = t_rw;  // range_walk done (then the LDS tail's walk, the helpers' items: t_walk)
     }
     // LDS only (the statistics, the LDS spike list): the walks' stores stay in flight
-    if (d.shard_mode || (stamping && !spk_lds)) __syncthreads();
+    if (shard || (stamping && !spk_lds)) __syncthreads();
     else lds_barrier();
     if (threadIdx.x == 0) {
         typedef unsigned long long ull;
@@ -1192,7 +1195,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
             atomicAdd((ull*)&st->events, (ull)d.events);
         }
     }
-    if (d.shard_mode) {
+    if (shard) {
         // sharded pass: no stamps, no pass end here (k_shard_walk, after the
         // exchange); workgroup 0 writes the exchange summary (abnn.h) once
         // every word is published
@@ -1266,7 +1269,7 @@ __device__ __forceinline__ void set_priority(uint32_t p)
 // weight update of k_apply: apply_event), and the last workgroup ends the pass
 // (fused_finalize).  Its survivors are written contiguously from the range's
 // region start (no per-chunk slots: the wave walks them itself).
-template <int BLOCK, int K, int FW, bool kTrack, bool kRandom, bool kFused>
+template <int BLOCK, int K, int FW, bool kTrack, bool kRandom, bool kFused, bool kLean = false>
 __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
     constexpr int NW = BLOCK / 64;
@@ -1638,7 +1641,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // staged events)
         const uint64_t gf = d.cost_tail ? ((__builtin_amdgcn_s_memrealtime() - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty : gt;
         const bool tl = tail_lds != nullptr;
-        fused_end<BLOCK, NW>(d, kp, r, region, tot.x + c.x, tl ? tot.y : tot.y + c.y, tl ? tot.z : tot.z + c.z,
+        fused_end<BLOCK, NW, kLean>(d, kp, r, region, tot.x + c.x, tl ? tot.y : tot.y + c.y, tl ? tot.z : tot.z + c.z,
                              tl ? c.y : 0u, tl ? c.z : 0u, tail_lds, (uint32_t)gf, len == 0, spec, now, Rw, rbw, pass_f,
                              epoch, s_fz, t_stream, hw0, chunk_t, nch, wcb);
         return;
@@ -2368,7 +2371,10 @@ template <int BLOCK, int K, int FW>
 hipError_t launch_fused_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
 {
     const dim3 g(d.gate_blocks), b(BLOCK);
+    // lean: the single-GPU pass without pruning or synaptogenesis
+    const bool lean = d.lean && !d.shard_mode && !(kp.w_prune > 0.0f) && !(d.grown != nullptr && kp.p_new > 0.0f);
     if (kp.track_visits) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true, false, true>), g, b, 0, s, d, kp);
+    else if (lean) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false, true, true>), g, b, 0, s, d, kp);
     else hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false, true>), g, b, 0, s, d, kp);
     return hipGetLastError();
 }
