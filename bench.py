@@ -69,6 +69,10 @@ def parse():
                          "README §4 random-edge picks (include/abnn/abnn.h)")
     ap.add_argument("--events", type=int, default=0,
                     help="override EVENTS_PER_PASS (e.g. = N_SYN for the config-3 full sweep)")
+    ap.add_argument("--shard-path", action="store_true",
+                    help="at one GPU, run the sharded pass (abnn_shard_traverse over the library's RCCL "
+                         "communicator, world 1) instead of the fused single-GPU pass: its per-pass "
+                         "overhead (DESIGN.md §7)")
     ap.add_argument("--plasticity", action="store_true",
                     help="config-5 dynamics: reward-modulated STDP (reward 0.25) with pruning "
                          "(w < 0.105) and synaptogenesis (p_new 0.25, w_init 0.5, +1%% capacity), "
@@ -182,6 +186,17 @@ def main():
     # ranks sharing the visible GPUs (exchange tensors staged through the host)
     backend = os.environ.get("ABNN_DIST_BACKEND", "nccl")
     device = local_rank if backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
+    if world == 1 and args.shard_path:  # a one-rank process group for the sharded path
+        import socket
+
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            with socket.socket() as so:
+                so.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(so.getsockname()[1])
+        dist.init_process_group("gloo", rank=0, world_size=1)
     if world > 1:
         import torch.distributed as dist
 
@@ -191,13 +206,13 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    if world > 1:
+    if world > 1 or args.shard_path:
         # one GPU per rank (RCCL): the passes are driven by the C-ABI over the
         # library's RCCL communicator (abnn_shard_traverse); the gloo
         # rehearsal (ranks sharing a GPU) drives them phase by phase from Python
         sb = ShardedBrain(TorchComm(), wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, events,
                           device=device, mode=mode, capacity_factor=1.01 if args.plasticity else 1.0,
-                          native=backend == "nccl", **extra)
+                          native=backend == "nccl" or world == 1, **extra)
         brain = sb.brain
         step = sb.step
     else:
@@ -225,19 +240,30 @@ def main():
     step(args.warmup)
     sync()
     brain.reset_stats()
-    # HIP events around a sample of the gate launches (an event pair costs
-    # stream time, so timing every pass would tax the measured rate); the
-    # sample starts at the second timed launch
-    every = timing_every(args.steps)
-    brain.enable_timing(every)
     sync()
+    # one HIP event pair around the K timed passes, on the stream they are
+    # enqueued on (the device's null stream = torch's default stream): the
+    # average launch duration is its span / K (one k_gate launch per pass in
+    # steady state; the ~1 us dispatch gap between launches included)
+    ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev_a.record()
     step(args.steps)
+    ev_b.record()
     sync()
     dt = time.perf_counter() - t0
-    launch_ms = brain.kernel_times()
-    gate_ms, launches = float(launch_ms.sum()), int(launch_ms.size)
+    region_ms = float(ev_a.elapsed_time(ev_b))
     stats = brain.stats()
+    # then, untimed: an event pair around a sample of single launches (every
+    # TIMING_EVERY-th; a pair adds a few us to the launch it brackets) for
+    # the min / median and the steady-state check
+    every = timing_every(args.steps)
+    brain.enable_timing(every)
+    step(args.steps)
+    sync()
+    brain.enable_timing(0)
+    launch_ms = brain.kernel_times()
+    launches = int(launch_ms.size)
     if dist is not None:
         tdev = f"cuda:{device}" if backend == "nccl" else "cpu"
         t = torch.tensor([dt], dtype=torch.float64, device=tdev)
@@ -251,7 +277,7 @@ def main():
 
     if rank == 0:
         value = total_events / dt
-        avg_gate_ms = gate_ms / max(1, launches)
+        avg_gate_ms = region_ms / args.steps
         track = bool(brain.params.track_visits)
         # one gate launch per pass; HIP events time a sample of them (every
         # TIMING_EVERY-th), so bytes per launch come from the pass count
@@ -259,15 +285,17 @@ def main():
         bytes_per_launch = algorithmic_bytes(stats, track, mode == 1) / passes
         achieved = bytes_per_launch / (avg_gate_ms * 1e-3) / 1e9
         survey_per_launch = survey_bytes(stats, track) / passes
-        default_run = mode == 0 and events == wl.events
+        default_run = mode == 0 and events == wl.events and not args.shard_path
         traffic, traffic_note = load_traffic(args.config) if world == 1 and default_run else (None, "not the default run")
         roofline = {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
-            "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": launches,
-            "min_launch_ms": round(float(launch_ms.min()), 4) if launches else None,
-            "median_launch_ms": round(float(np.median(launch_ms)), 4) if launches else None,
+            "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": args.steps,
+            "launch_ms_source": "HIP event pair around the timed passes / steps (launch + dispatch gap)",
+            "sampled_launches": launches,
+            "sampled_min_launch_ms": round(float(launch_ms.min()), 4) if launches else None,
+            "sampled_median_launch_ms": round(float(np.median(launch_ms)), 4) if launches else None,
             "timing_every": every,
             # a launch cannot take longer than the pass it is part of: if the
             # sample's median says so (beyond the few us an event pair adds to
@@ -308,7 +336,8 @@ def main():
                                     n_syn_after=brain.n_syn(), pruned=stats.get("pruned", 0),
                                     grown=stats.get("grown", 0)) if args.plasticity else None),
                 "parallelism": (f"synapse-shard dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)"))
-                               if world > 1 else "single GPU",
+                               if world > 1 else ("synapse-shard dp1 (the sharded pass at one GPU)" if args.shard_path
+                                                  else "single GPU"),
                 "settle_passes": args.settle, "settle_s": round(settle_s, 4),
                 "pre_gated_frac": stats["pre_gated"] / max(1, stats["events"]),
                 "spikes_per_pass": stats["fired"] / max(1, stats["passes"]),

@@ -70,16 +70,18 @@ def main():
             lines.append(f"{k:14s} {statistics.median(v):9.2f} {v[0]:9.2f} {v[-1]:9.2f}")
         if spans:
             lines.append(f"pass span median {statistics.median(spans):.2f} us")
-        # the bench's timed region = its last `steps` gate launches: their mean is
-        # what bench.py's HIP-event sample estimates (roofline.avg_launch_ms)
+        # the bench's timed region = the `steps` gate launches before its last
+        # `steps` (the untimed sampling passes): their mean is what bench.py's
+        # HIP event pair around the region measures (roofline.avg_launch_ms, which
+        # also holds the dispatch gaps)
         try:
             bj = [x for x in open(os.path.join(out, "bench_trace.json")) if x.startswith("{")][-1]
             steps = json.loads(bj)["steps"]
             rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
             g = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
-                 if "k_gate" in r["Kernel_Name"].split("(")[0]][-steps:]
+                 if "k_gate" in r["Kernel_Name"].split("(")[0]][-2 * steps:-steps]
             lines.append(f"k_gate mean over the {len(g)} timed launches {statistics.mean(g):.2f} us "
-                         f"(bench HIP-event sample: {json.loads(bj)['roofline']['avg_launch_ms'] * 1e3:.2f} us)")
+                         f"(bench HIP events, span / passes: {json.loads(bj)['roofline']['avg_launch_ms'] * 1e3:.2f} us)")
         except (OSError, IndexError, KeyError, ValueError):
             pass
     # last 10 timed k_gate launches of each PMC pass are steady state
