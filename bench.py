@@ -261,9 +261,9 @@ def main():
     brain.enable_timing(every)
     step(args.steps)
     sync()
-    brain.enable_timing(0)
     launch_ms = brain.kernel_times()
     launches = int(launch_ms.size)
+    brain.enable_timing(0)
     if dist is not None:
         tdev = f"cuda:{device}" if backend == "nccl" else "cpu"
         t = torch.tensor([dt], dtype=torch.float64, device=tdev)
