@@ -824,11 +824,11 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     b->per_cu = per_cu;
     // partition A-B knobs: wave -> range map, adaptation gain
     if (const char* env = std::getenv("ABNN_RANGE_MAP")) d.range_map = std::atoi(env) ? 1u : 0u;
-    d.adapt_gain = 2;
+    d.adapt_gain = 1;  // profiles/r03g_*: 1 with tail priority 0 is -1 us against 2 with the rank kept
     if (const char* env = std::getenv("ABNN_ADAPT_GAIN")) d.adapt_gain = (uint32_t)std::min(4, std::max(1, std::atoi(env)));
     d.chunk_penalty = 350;  // 14 us per full chunk: the dense input->output stretch spread over more
                             // ranges (tools/knob_sweep.sh ABNN_CHUNK_PENALTY: 25 -> 350 measured -6 us per pass)
-    d.tail_prio = 4;
+    d.tail_prio = 0;  // a range's tail at the lowest issue priority: the streams still running go first
     d.apply_blocks = kWalkBlocks;
     if (const char* env = std::getenv("ABNN_APPLY_BLOCKS"))
         d.apply_blocks = (uint32_t)std::min<int>(kWalkBlocks, std::max(1, std::atoi(env)));

@@ -157,10 +157,10 @@ struct DeviceState {
                                   // pass's prologue; the host rotates the three)
     uint32_t* range_bounds_prev;  // [n_ranges + 1] the previous pass's (the fused prologue's cost curve)
     uint32_t adapt_ranges;    // rebalance the partition after every pass (default on; ABNN_STATIC_RANGES=1: off)
-    uint32_t adapt_gain;      // a boundary moves adapt_gain / 4 of the way to its target (1..4, ABNN_ADAPT_GAIN; default 2)
+    uint32_t adapt_gain;      // a boundary moves adapt_gain / 4 of the way to its target (1..4, ABNN_ADAPT_GAIN; default 1)
     uint32_t chunk_penalty;   // partition cost added per full chunk, 40-ns units (ABNN_CHUNK_PENALTY)
     uint32_t apply_blocks;    // k_claim / k_apply grid (<= kWalkBlocks; ABNN_APPLY_BLOCKS)
-    uint32_t tail_prio;       // gate issue priority for a wave's tail, 0..3 (4: keep; ABNN_TAIL_PRIO)
+    uint32_t tail_prio;       // gate issue priority for a wave's tail, 0..3 (4: keep; ABNN_TAIL_PRIO, default 0)
     uint32_t prio_clock;      // gate priority rotation by wall clock (1) or by iteration (0; ABNN_PRIO_CLOCK)
     uint32_t range_map;       // gate wave -> range: 0 blocked (workgroup b: ranges b*NW..), 1 interleaved (ABNN_RANGE_MAP=1)
     // fused pass: look-back words [gate_blocks]; gate costs of the previous
