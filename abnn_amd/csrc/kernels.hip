@@ -1934,9 +1934,13 @@ __device__ uint64_t stamp_gathered(const DeviceState& d, const KernelParams& kp,
         const int64_t cnt = *reinterpret_cast<const int64_t*>(gathered + r * words);
         const int32_t* sp = gathered + r * words + 2 * ABNN_SUMMARY_WORDS;
         const uint64_t room = budget - off, n = (uint64_t)cnt < room ? (uint64_t)cnt : room;
-        // wave-uniform trip count (wave_set_next is wave-converged)
-        for (uint64_t i0 = (uint64_t)blockIdx.x * kApplyThreads + (threadIdx.x - lane); i0 < n;
-             i0 += (uint64_t)gridDim.x * kApplyThreads) {
+        // wave-uniform trip count (wave_set_next is wave-converged); the
+        // list's 64-entry slices go to the waves in workgroup-interleaved
+        // order, so that the stamps and the bitmap atomics of a few thousand
+        // spikes spread over as many CUs (in workgroup order three CUs took
+        // them all: their stores drained 5 us after every other workgroup's)
+        const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+        for (uint64_t i0 = ((uint64_t)(threadIdx.x >> 6) * gridDim.x + blockIdx.x) * 64; i0 < n; i0 += nw * 64) {
             const uint64_t i = i0 + lane;
             const uint32_t nrn = i < n ? (uint32_t)sp[i] : 0xFFFFFFFFu;
             if (nrn < d.n_nrn) {
@@ -2170,6 +2174,9 @@ __global__ __launch_bounds__(NW * 64) void k_shard_walk(DeviceState d, KernelPar
     __shared__ uint64_t s_now, s_pass;
     __shared__ float s_R, s_rb;
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
+    // diagnostics (tools/shard_clock.py): per workgroup, 100-MHz ticks
+    uint64_t* ck = d.apply_clock + 8ull * (blockIdx.x % kWalkBlocks);
+    if (threadIdx.x == 0) ck[0] = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {  // pass-start scalars (C1): the last workgroup rewrites them
         s_R = *d.reward;
         s_rb = *d.rbar;
@@ -2187,7 +2194,9 @@ __global__ __launch_bounds__(NW * 64) void k_shard_walk(DeviceState d, KernelPar
     const bool spec = ri.w & 1u;
     ApplyCtx ac{R, rb, now, pass, false, false, false, false, kp.w_prune > 0.0f, d.grown != nullptr && kp.p_new > 0.0f,
                 true, 0u, 0u, 0u};
+    if (threadIdx.x == 0) ck[1] = __builtin_amdgcn_s_memrealtime();
     const uint32_t upd_rest = range_walk(d, kp, ac, r, region, ri.y, ri.z, P, spec, false, s_setc);
+    if (threadIdx.x == 0) ck[2] = __builtin_amdgcn_s_memrealtime();
     // the next pass's spec prediction: the workgroup holding the global cut
     // (its first range's position below the budget, its last range's end at
     // or past it) names the ones below it, less one, as the fused pass does
@@ -2204,7 +2213,9 @@ __global__ __launch_bounds__(NW * 64) void k_shard_walk(DeviceState d, KernelPar
     // every rank's spikes (global budget order) and, in steady state, into
     // the next pass's bitmap
     const uint64_t nsp = stamp_gathered(d, kp, gathered, world, now, pass);
+    if (threadIdx.x == 0) ck[3] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
+    if (threadIdx.x == 0) ck[4] = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {
         typedef unsigned long long ull;
         abnn_stats* st = d.wg_stats + blockIdx.x % kWalkBlocks;
@@ -2214,6 +2225,8 @@ __global__ __launch_bounds__(NW * 64) void k_shard_walk(DeviceState d, KernelPar
         if (blockIdx.x == 0) d.n_fired_ring[pass & (kFiredRing - 1)] = (uint32_t)nsp;
         const uint32_t ticket = __hip_atomic_fetch_add((gu32*)(&d.work->ticket), 1u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT);
+        ck[5] = __builtin_amdgcn_s_memrealtime();
+        ck[6] = ticket == gridDim.x - 1;
         if (ticket == gridDim.x - 1) {
             const int64_t mine = *reinterpret_cast<const int64_t*>(gathered + rank * xchg_words(kp.max_spikes));
             if (off >= budget) d.work->spec_wgs = 0u;                        // the whole shard past the cut
