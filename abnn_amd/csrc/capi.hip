@@ -759,7 +759,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     // Gate kernel shape: threads per workgroup x events per lane x KiB per LDS
     // filter image (ABNN_GATE="1024x16f32"; tuning knob, the default is the measured best:
     // profiles/r01s_shape_sweep.txt).
-    uint32_t gate_block = 1024, gate_k = 16, filter_kib = 32;
+    uint32_t gate_block = 1024, gate_k = 8, filter_kib = 32;  // profiles/r03l_ab_k8.txt: 1024x8 -1.7 us against 1024x16
     if (const char* env = std::getenv("ABNN_GATE")) {
         unsigned gb = 0, gk = 0, fk = 0;
         const int got = std::sscanf(env, "%ux%uf%u", &gb, &gk, &fk);
@@ -826,8 +826,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (const char* env = std::getenv("ABNN_RANGE_MAP")) d.range_map = std::atoi(env) ? 1u : 0u;
     d.adapt_gain = 1;  // profiles/r03g_*: 1 with tail priority 0 is -1 us against 2 with the rank kept
     if (const char* env = std::getenv("ABNN_ADAPT_GAIN")) d.adapt_gain = (uint32_t)std::min(4, std::max(1, std::atoi(env)));
-    d.chunk_penalty = 350;  // 14 us per full chunk: the dense input->output stretch spread over more
-                            // ranges (tools/knob_sweep.sh ABNN_CHUNK_PENALTY: 25 -> 350 measured -6 us per pass)
+    d.chunk_penalty = 600;  // 24 us per full chunk: the dense input->output stretch spread over more
+                            // ranges (ABNN_CHUNK_PENALTY: 25 -> 350 measured -6 us per pass in round 2;
+                            // 600 with the 1024x8 gate, profiles/r03l_ab_k8.txt)
     d.tail_prio = 0;  // a range's tail at the lowest issue priority: the streams still running go first
     d.apply_blocks = kWalkBlocks;
     if (const char* env = std::getenv("ABNN_APPLY_BLOCKS"))
