@@ -174,6 +174,8 @@ SIGNATURES = [
     ("abnn_get_budget", C.c_int, [_VP, _PU32]),
     ("abnn_structural_updates", C.c_uint64, [_VP]),
     ("abnn_traversal_workspace_bytes", C.c_uint64, [_U32, _U32]),
+    ("abnn_traversal_workspace_min_bytes", C.c_uint64, [_U32, _U32]),
+    ("abnn_traversal_workspace_error", C.c_int, [_VP, _PU32, _VP]),
     ("abnn_launch_traversal", C.c_int, [C.POINTER(TraversalArgs), _VP]),
     ("abnn_launch_renormalise", C.c_int, [_VP, _VP, _VP, _U32, _VP]),
     ("abnn_comm_unique_id", C.c_int, [_VP]),
@@ -212,6 +214,14 @@ def _share_hip_runtime_with_torch() -> None:
         C.CDLL(hip, mode=C.RTLD_GLOBAL)
 
 
+# diagnostics (include/abnn/abnn_debug.h, outside the stable boundary)
+DEBUG_SIGNATURES = [
+    ("abnn_debug_raw_stats", C.c_int, [_VP, C.POINTER(C.c_uint64), _VP]),
+    ("abnn_debug_raw_gate_timing", C.c_int, [C.c_int]),
+    ("abnn_debug_raw_gate_time", C.c_int, [C.POINTER(C.c_double), _PU32]),
+]
+
+
 def load() -> C.CDLL:
     """Load libabnn_hip.so (built in-tree); raise if it is missing."""
     global _lib
@@ -223,7 +233,7 @@ def load() -> C.CDLL:
             "(there is no CPU fallback for the traversal engine)")
     _share_hip_runtime_with_torch()
     lib = C.CDLL(LIB_PATH)
-    for name, res, args in SIGNATURES:
+    for name, res, args in SIGNATURES + DEBUG_SIGNATURES:
         fn = getattr(lib, name)  # AttributeError = the ABI is not exported
         fn.restype = res
         fn.argtypes = args

@@ -1271,6 +1271,7 @@ struct abnn_comm {
     char* gathered = nullptr;   // world exchange records, rank order
     uint64_t rec_bytes = 0;
     uint64_t* scratch = nullptr;  // visited-events all-reduce
+    bool broken = false;          // an earlier pass failed on this rank (abnn.h: abort on every rank)
 };
 
 abnn_status abnn_comm_unique_id(void* id_out)
@@ -1331,14 +1332,14 @@ abnn_status abnn_comm_destroy(abnn_comm* c)
     return ABNN_OK;
 }
 
-abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, void* stream)
+// One sharded pass per iteration.  An error part-way through a pass leaves
+// the other ranks inside (or about to enter) the pass's collectives, so the
+// communicator is marked broken: every later call on it fails at once, and
+// the caller must abort / destroy it on every rank (abnn.h).  The handle's
+// half-done pass is dropped (no walk of a gate whose exchange never came).
+static abnn_status shard_traverse_passes(abnn_brain* b, abnn_comm* c, uint32_t passes, hipStream_t s)
 {
-    REQUIRE(b && c, "null argument");
-    REQUIRE(c->device == b->device, "communicator and handle are on different devices");
-    ST_TRY(pass_error(b));
-    HIP_TRY(hipSetDevice(b->device));
     const RcclApi& r = rccl_api();
-    hipStream_t s = pick(b, stream);
     const uint64_t rec = abnn_exchange_bytes(b);
     if (rec != c->rec_bytes) {  // the records' size follows the budget: sized on first use
         if (c->gathered) HIP_TRY(hipFree(c->gathered));
@@ -1365,6 +1366,21 @@ abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, vo
         }
     }
     return ABNN_OK;
+}
+
+abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, void* stream)
+{
+    REQUIRE(b && c, "null argument");
+    REQUIRE(c->device == b->device, "communicator and handle are on different devices");
+    REQUIRE(!c->broken, "communicator unusable after an earlier error on this rank: abort / destroy it on every rank");
+    HIP_TRY(hipSetDevice(b->device));
+    abnn_status st = pass_error(b);
+    if (st == ABNN_OK) st = shard_traverse_passes(b, c, passes, pick(b, stream));
+    if (st != ABNN_OK) {
+        c->broken = true;
+        b->pending_walk = false;
+    }
+    return st;
 }
 
 abnn_status abnn_comm_sync_visits(abnn_brain* b, abnn_comm* c, void* stream)

@@ -2409,10 +2409,16 @@ int occupancy_shape(bool track, bool random)
 template <int BLOCK, int K, int FW>
 int occupancy_fused_shape(bool track)
 {
-    int n = 0;
-    const hipError_t e = track ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, false, true>, BLOCK, 0)
-                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, false, true>, BLOCK, 0);
-    return e == hipSuccess ? n : 0;
+    // every instance launch_fused_shape may select for these knobs: the
+    // look-back needs all gate workgroups resident, whichever one runs
+    int n = 0, m = 0;
+    if (track) {
+        const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, false, true>, BLOCK, 0);
+        return e == hipSuccess ? n : 0;
+    }
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, false, true>, BLOCK, 0);
+    const hipError_t f = hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, k_gate<BLOCK, K, FW, false, false, true, true>, BLOCK, 0);
+    return e == hipSuccess && f == hipSuccess ? std::min(n, m) : 0;
 }
 
 // Compiled gate shapes: threads per workgroup x events per lane x filter words.

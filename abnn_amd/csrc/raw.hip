@@ -6,30 +6,47 @@
 //
 // The handle API (capi.hip, kernels.hip) re-lays the records out for the gate
 // (3 B per event).  Here the caller owns the memory, so every visited event
-// streams its whole 16-B record and gathers lastF[src] as the reference does.
-// Three launches per pass, all on the caller's stream:
+// streams its whole 16-B record (brain.metal:70) -- the compulsory traffic.
+// What is not compulsory is the reference's 4-B lastF[src] gather per event
+// (brain.metal:73): the pass answers the pre-spike gate from an LDS filter of
+// the recent neurons and gathers lastF only for the ~1 % of events the filter
+// passes.  Launches per pass, all on the caller's stream:
 //
-//   k_raw_gate  : tiles of 2048 events (8 per thread, record loads coalesced):
-//                 pre-spike gate (brain.metal:73-77), refractory gate
-//                 (brain.metal:79-83), spike-candidate test (brain.metal:91-92)
-//                 and the u32 age (brain.metal:116); survivors compacted in
-//                 event order into the tile's workspace region.
-//   k_raw_scan  : one workgroup: the tiles' capped candidate prefix (the
-//                 ordered budget of C1, brain.metal:85-98 without its races),
-//                 then the pass end on the scalars, which nothing later in the
-//                 pass reads: *budget left, rBar (brain.metal:110-113), one
-//                 clock tick (brain.metal:129).  The pass-start values go to the
-//                 workspace header for k_raw_apply.
-//   k_raw_apply : one wave per tile with budget left: the weight update of its
-//                 survivors below the budget (brain.metal:101-122) and the
-//                 spikes' stamps (brain.metal:125-126) -- every lastF read of
-//                 the pass was in k_raw_gate, so the stamps land after them (C1).
+//   k_raw_filter : lastF (read once, 4 B per neuron) -> the blocked Bloom
+//                  filter of the neurons with age <= window_pre (the same
+//                  filter as the handle API's; each filter block
+//                  built by one workgroup from its ~20 bitmap words: no
+//                  atomics, no zeroing); resets the pass's workspace counters.
+//   k_raw_gate   : persistent, one 1024-thread workgroup per CU; every wave
+//                  sweeps groups of 1024 events (interleaved over the CUs):
+//                  16-B records four iterations ahead, the filter test per
+//                  event (one 8-B LDS read), hits staged in LDS in event
+//                  order; per group the staged hits' lastF[src] and lastF[dst]
+//                  in ONE round trip -> exact pre-spike gate (brain.metal:
+//                  73-77), refractory gate (brain.metal:79-83), spike
+//                  candidate (brain.metal:91-92), u32 age (brain.metal:116);
+//                  survivors appended to the wave's survivor sequence, held
+//                  in 4-KiB chunks of a BOUNDED pool (one atomic per chunk).
+//   k_raw_scan   : one workgroup: the groups' capped candidate prefix (the
+//                  ordered budget of C1, brain.metal:85-98 without its races),
+//                  the budget cut, then the pass end on the scalars: *budget
+//                  left, rBar (brain.metal:110-113), one clock tick
+//                  (brain.metal:129).
+//   k_raw_apply  : the groups below the cut: the weight update of their
+//                  survivors below the budget (brain.metal:101-122) and the
+//                  spike list in budget order.  A group whose survivors did
+//                  not fit the pool is recomputed from its records (the pass-
+//                  start lastF: the stamps are deferred).
+//   k_raw_stamp  : the spike list's stamps (brain.metal:125-126), after every
+//                  lastF read of the pass (C1).
 //
 // renormalise_clock_and_times (brain.metal:135-145): k_raw_renorm subtracts
 // the clock read by every thread, k_raw_zero_clock zeroes it afterwards (the
 // reference zeroes it inside the same kernel, racing with the readers).
 #include <algorithm>
 #include <cstring>
+#include <utility>
+#include <vector>
 
 #include "engine.h"
 #include "device.h"
@@ -39,44 +56,109 @@
 namespace abnn {
 namespace {
 
-constexpr uint32_t kRawThreads = 256, kRawK = 8, kRawTile = kRawThreads * kRawK;  // events per tile
-constexpr uint32_t kRawWaves = kRawThreads / 64;
+constexpr uint32_t kRawBlock = 1024;                 // gate threads per workgroup (16 waves)
+constexpr uint32_t kRawGateWGs = 256;                // gate workgroups (one per CU; no inter-WG dependency)
+constexpr uint32_t kRawWaves = kRawGateWGs * (kRawBlock / 64);  // 4096 gate waves
+constexpr uint32_t kRawK = 4;                        // records per lane per iteration (256 events)
+constexpr uint32_t kRawIt = 64 * kRawK;              // events per iteration
+constexpr uint32_t kRawD = 4;                        // iterations per group = buffers in flight
+constexpr uint32_t kRawGroup = kRawIt * kRawD;       // 1024 events: the scan / apply unit
+constexpr uint32_t kRawChunk = 256;                  // survivor entries (16 B) per pool chunk
+constexpr uint32_t kRawStage = 256;                  // staged hits per wave (flush above 192)
+constexpr uint32_t kRawFB = 8192;                    // filter blocks (64 KiB of LDS)
+constexpr uint32_t kRawFLg = 13;
+constexpr uint32_t kRawSpikeCap = 65536;             // spike list entries (deferred stamps)
 constexpr uint32_t kRawScanThreads = 1024;
-constexpr uint32_t kRawApplyBlocks = 4096;  // x 4 waves, each walks tiles w, w + 16384, ...
+constexpr uint32_t kRawApplyWGs = 1024;              // x 4 waves, grid-stride over the groups below the cut
+constexpr uint32_t kRawNone = 0xFFFFFFFFu;
 
-// Workspace: header | tile counts {survivors, candidates} | capped candidate
-// prefix per tile | survivors {event, age bits | candidate << 31, w, dst}.
+// Workspace (16-B aligned pieces):
+//   hdr | filter (FB uint2) | gcand[NG] | gpre[NG] | ginfo[NG] {S, seq} |
+//   wlim[W] | wstat[W] | ctab[W][maxc] | spikes[L] | pool[cap][kRawChunk] uint4
 struct RawHdr {
-    uint32_t now, budget0, t0, ncand;  // pass-start clock and budget; event 0 survived; candidates below the budget
+    uint32_t now, budget0, t0, ncand;  // pass-start clock and budget; event 0 survived; spikes (capped)
     float R, rb;                       // pass-start reward and rBar (brain.metal:105-106)
-    uint32_t pad[10];
+    uint32_t chunks;                   // pool chunks handed out this pass
+    uint32_t gcut;                     // groups below the budget's cut: [0, gcut)
+    uint32_t direct;                   // budget0 > the spike list: apply stamps itself
+    uint32_t err;                      // a recomputed group met direct stamps (abnn_traversal_workspace_error)
+    uint32_t pad[2];
+    uint64_t g1, g2;                   // the pass's pre-gated and refractory-surviving events (diagnostics)
 };
 static_assert(sizeof(RawHdr) == 64, "workspace header");
 
 struct RawWs {
     RawHdr* hdr;
-    uint2* cnt;
-    uint32_t* pre;
-    uint4* surv;
+    uint2* filter;
+    uint32_t* gcand;   // spike candidates per group
+    uint32_t* gpre;    // capped exclusive candidate prefix per group
+    uint2* ginfo;      // {survivors, first index in the owning wave's survivor sequence}
+    uint32_t* wlim;    // per wave: survivor-sequence entries stored (the rest overflowed the pool)
+    uint2* wstat;      // per wave: {pre-gated, survivors} of its groups (k_raw_scan sums them)
+    uint32_t* ctab;    // per wave: pool chunk of every 256 entries of its sequence
+    uint32_t* spikes;  // dst per budget position (deferred stamps)
+    uint4* pool;       // survivors {event, age bits | candidate << 31, w bits, dst}
+    uint32_t ng, maxc, spike_cap, pool_chunks;
 };
 
-__host__ __device__ inline uint64_t raw_tiles(uint64_t E) { return (E + kRawTile - 1) / kRawTile; }
-
-__host__ __device__ inline RawWs raw_ws(void* base, uint64_t tiles)
+__host__ __device__ inline uint64_t raw_groups(uint64_t E) { return (E + kRawGroup - 1) / kRawGroup; }
+__host__ __device__ inline uint32_t raw_maxc(uint64_t ng)
 {
-    char* p = static_cast<char*>(base);
-    RawWs w;
-    w.hdr = reinterpret_cast<RawHdr*>(p);
-    w.cnt = reinterpret_cast<uint2*>(p + 64);
-    w.pre = reinterpret_cast<uint32_t*>(p + 64 + 8 * tiles);
-    w.surv = reinterpret_cast<uint4*>(p + 64 + ((12 * tiles + 15) & ~15ull));
-    return w;
+    const uint64_t per_wave = (ng + kRawWaves - 1) / kRawWaves;  // groups of one wave
+    return (uint32_t)(per_wave * (kRawGroup / kRawChunk) + 1);
+}
+inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
+
+inline uint64_t raw_fixed_bytes(uint64_t E)
+{
+    const uint64_t ng = raw_groups(E);
+    const uint64_t L = std::min<uint64_t>(E, kRawSpikeCap);
+    return 64 + kRawFB * 8 + al16(4 * ng) * 2 + al16(8 * ng) + al16(4ull * kRawWaves) + al16(8ull * kRawWaves) +
+           al16(4ull * kRawWaves * raw_maxc(ng)) + al16(4 * L);
+}
+
+// Recommended pool: a partial chunk per wave plus 1/64 of the events (config
+// 3 keeps ~0.3 % of them); a larger workspace only makes overflow rarer.
+inline uint64_t raw_pool_chunks_recommended(uint64_t E)
+{
+    return E ? kRawWaves + (E / 64 + kRawChunk - 1) / kRawChunk + 64 : 0;
 }
 
 inline uint64_t raw_ws_bytes(uint64_t E)
 {
-    const uint64_t tiles = raw_tiles(E);
-    return 64 + ((12 * tiles + 15) & ~15ull) + 16 * tiles * kRawTile;
+    return raw_fixed_bytes(E) + raw_pool_chunks_recommended(E) * kRawChunk * 16;
+}
+
+inline RawWs raw_ws(void* base, uint64_t E, uint64_t bytes)
+{
+    char* p = static_cast<char*>(base);
+    const uint64_t ng = raw_groups(E);
+    RawWs w;
+    w.ng = (uint32_t)ng;
+    w.maxc = raw_maxc(ng);
+    w.spike_cap = (uint32_t)std::min<uint64_t>(E, kRawSpikeCap);
+    w.hdr = reinterpret_cast<RawHdr*>(p);
+    p += 64;
+    w.filter = reinterpret_cast<uint2*>(p);
+    p += kRawFB * 8;
+    w.gcand = reinterpret_cast<uint32_t*>(p);
+    p += al16(4 * ng);
+    w.gpre = reinterpret_cast<uint32_t*>(p);
+    p += al16(4 * ng);
+    w.ginfo = reinterpret_cast<uint2*>(p);
+    p += al16(8 * ng);
+    w.wlim = reinterpret_cast<uint32_t*>(p);
+    p += al16(4ull * kRawWaves);
+    w.wstat = reinterpret_cast<uint2*>(p);
+    p += al16(8ull * kRawWaves);
+    w.ctab = reinterpret_cast<uint32_t*>(p);
+    p += al16(4ull * kRawWaves * w.maxc);
+    w.spikes = reinterpret_cast<uint32_t*>(p);
+    p += al16(4ull * w.spike_cap);
+    w.pool = reinterpret_cast<uint4*>(p);
+    const uint64_t fixed = (uint64_t)(p - static_cast<char*>(base));
+    w.pool_chunks = (uint32_t)std::min<uint64_t>((bytes - fixed) / (kRawChunk * 16), 0xFFFFFFFEu);
+    return w;
 }
 
 // visited events: min(roundup(events, 256), n_syn) (brain.cpp:116-118, brain.metal:60-61)
@@ -86,81 +168,236 @@ inline uint64_t raw_events(uint32_t n_syn, uint32_t events)
     return grid < n_syn ? grid : n_syn;
 }
 
-__global__ __launch_bounds__(kRawThreads) void k_raw_gate(const uint4* __restrict__ syn, const uint32_t* lastF,
-                                                           const uint32_t* clock, uint32_t n_nrn, uint32_t E,
-                                                           KernelParams kp, RawWs ws)
+// The filter block of word j (neurons 32 j .. 32 j + 31): g(j) = (j ^ t) mod
+// FB, t = 0x9E5 (j >> 13); its high half holds the word rotated left by t mod
+// 32 (kernels.hip filter_set).
+__device__ __forceinline__ uint32_t raw_t(uint32_t j) { return __umul24(j >> kRawFLg, 0x9E5u); }
+
+// One 8-B LDS read per event; no false negatives.  Any src (tombstones
+// included) reads inside the filter.
+__device__ __forceinline__ bool raw_filter_pass(const uint2* s_fb, uint32_t src)
 {
-    __shared__ uint32_t s_cnt[kRawK * kRawWaves], s_cand[kRawK * kRawWaves];
+    const uint32_t j = src >> 5, t = raw_t(j);
+    const uint2 f = s_fb[(j ^ t) & (kRawFB - 1)];
+    return (__builtin_amdgcn_ubfe(f.x, src, 1) & __builtin_amdgcn_ubfe(f.y, src + t, 1)) != 0u;
+}
+
+// ---------------------------------------------------------------------------
+// k_raw_filter: workgroup b builds filter blocks [8 b, 8 b + 8).  The words
+// of block g are j = h << 13 | ((g ^ t(h)) & 8191), h = 0 .. H-1 (t depends on
+// h only); half a wave reads one word's 32 lastF values (128 B), so a wave
+// instruction covers two words and the ballot returns both.  Every lastF
+// value is read once by the whole grid.
+__global__ __launch_bounds__(256) void k_raw_filter(const uint32_t* lastF, const uint32_t* clock, uint32_t n_nrn,
+                                                    KernelParams kp, RawWs ws)
+{
+    __shared__ uint32_t s_lo[8], s_hi[8];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t now = *clock;  // per-TG clock cache (brain.metal:63-68); C1: the pass-start value
-    const uint64_t base = (uint64_t)blockIdx.x * kRawTile;
-    uint4 rec[kRawK];
-#pragma unroll
-    for (uint32_t k = 0; k < kRawK; ++k) {  // brain.metal:70, all loads in flight at once
-        const uint64_t t = base + k * kRawThreads + threadIdx.x;
-        rec[k] = t < E ? syn[t] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+    if (threadIdx.x < 8) {
+        s_lo[threadIdx.x] = 0u;
+        s_hi[threadIdx.x] = 0u;
     }
-    uint32_t lp[kRawK];
-#pragma unroll
-    for (uint32_t k = 0; k < kRawK; ++k) lp[k] = rec[k].x < n_nrn ? lastF[rec[k].x] : 0u;
-    uint32_t ld[kRawK];
-    bool g1[kRawK];
-#pragma unroll
-    for (uint32_t k = 0; k < kRawK; ++k) {
-        // a record naming a neuron >= n_nrn (the {0xFFFFFFFF, 0xFFFFFFFF} tombstone of a
-        // pruned synapse) never passes
-        g1[k] = rec[k].x < n_nrn && rec[k].y < n_nrn && now - lp[k] <= kp.window_pre;  // brain.metal:73-77
-        ld[k] = g1[k] ? lastF[rec[k].y] : now;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // this pass's counters (the gate and the scan set them)
+        ws.hdr->chunks = 0u;
+        ws.hdr->t0 = 0u;
+        ws.hdr->err = 0u;
     }
-    uint64_t m2[kRawK];  // wave-uniform: survivors of step k
+    __syncthreads();
+    const uint32_t now = *clock;
+    const uint32_t words = (n_nrn + 31u) / 32u, H = (words + kRawFB - 1) >> kRawFLg;
+    const uint32_t tasks = 8u * H;  // (block, h) pairs of this workgroup
+    constexpr uint32_t kU = 4;
+    for (uint32_t x0 = wv * 2u * kU; x0 < tasks; x0 += 4u * 2u * kU) {  // wave-uniform
+        uint32_t v[kU];
+        uint32_t jw[kU];
 #pragma unroll
-    for (uint32_t k = 0; k < kRawK; ++k) {
-        const bool g2 = g1[k] && now - ld[k] > kp.refractory;  // brain.metal:79-83
-        const uint64_t t = base + k * kRawThreads + threadIdx.x;
-        const float w = __uint_as_float(rec[k].z);
-        const bool cand = g2 && spike_candidate(kp, w, t, now);  // brain.metal:91-92
-        m2[k] = __ballot(g2);
-        const uint64_t mc = __ballot(cand);
-        rec[k] = make_uint4((uint32_t)t, __float_as_uint((float)(now - ld[k])) | (cand ? 0x80000000u : 0u),
-                            rec[k].z, rec[k].y);
-        if (lane == 0) {
-            s_cnt[k * kRawWaves + wv] = (uint32_t)__popcll(m2[k]);
-            s_cand[k * kRawWaves + wv] = (uint32_t)__popcll(mc);
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t x = x0 + 2u * u + (lane >> 5);  // this half-wave's task
+            const uint32_t gl = x & 7u, h = x >> 3, g = blockIdx.x * 8u + gl;
+            const uint32_t t = __umul24(h, 0x9E5u);
+            const uint32_t j = h << kRawFLg | ((g ^ t) & (kRawFB - 1));
+            jw[u] = x < tasks ? j : kRawNone;
+            const uint64_t n = (uint64_t)j * 32u + (lane & 31u);
+            v[u] = (x < tasks && n < n_nrn) ? lastF[n] : 0u;
+            const bool ok = x < tasks && n < n_nrn;
+            v[u] = ok ? ((now - v[u]) <= kp.window_pre ? 1u : 0u) : 0u;  // brain.metal:73-77 (u32 age)
         }
-        if (t == 0) ws.hdr->t0 = g2 ? 1u : 0u;  // event 0 reached the budget test (brain.metal:110)
-    }
-    __syncthreads();
-    // exclusive offsets in event order: (k, wave, lane)
-    uint32_t off = 0;
-    if (wv == 0) {
-        const uint32_t c = lane < kRawK * kRawWaves ? s_cnt[lane] : 0u;
-        const uint32_t inc = wave_incl_scan(c);
-        const uint32_t cc = wave_incl_scan(lane < kRawK * kRawWaves ? s_cand[lane] : 0u);
-        if (lane < kRawK * kRawWaves) s_cnt[lane] = inc - c;
-        if (lane == 63)
-            ws.cnt[blockIdx.x] = make_uint2(inc, cc);
-    }
-    __syncthreads();
 #pragma unroll
-    for (uint32_t k = 0; k < kRawK; ++k) {
-        off = s_cnt[k * kRawWaves + wv];
-        if ((m2[k] >> lane) & 1u) ws.surv[base + off + mbcnt64(m2[k])] = rec[k];
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint64_t m = __ballot(v[u] != 0u);
+            if ((lane & 31u) == 0 && jw[u] != kRawNone) {
+                const uint32_t bits = (uint32_t)(m >> (lane & 32u));
+                if (bits) {
+                    const uint32_t x = x0 + 2u * u + (lane >> 5), gl = x & 7u, r = raw_t(jw[u]) & 31u;
+                    atomicOr(&s_lo[gl], bits);
+                    atomicOr(&s_hi[gl], (bits << r) | (bits >> ((32u - r) & 31u)));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 8) ws.filter[blockIdx.x * 8u + threadIdx.x] = make_uint2(s_lo[threadIdx.x], s_hi[threadIdx.x]);
+}
+
+// ---------------------------------------------------------------------------
+// k_raw_gate (see the file header).  Wave v = wid * gridDim + blockIdx sweeps
+// groups v, v + W, v + 2W, ... (W = all gate waves): the dense stretches of a
+// graph spread over the CUs.  Its survivors form one sequence in group order,
+// stored 256 entries per pool chunk (ctab: the chunk of every 256 entries);
+// when the pool runs out the rest of the wave's sequence is not stored
+// (wlim), and k_raw_apply recomputes those groups.
+__global__ __launch_bounds__(kRawBlock) void k_raw_gate(const uint4* __restrict__ syn, const uint32_t* lastF,
+                                                         const uint32_t* clock, uint32_t n_nrn, uint32_t E,
+                                                         KernelParams kp, RawWs ws)
+{
+    constexpr uint32_t NW = kRawBlock / 64;
+    __shared__ uint2 s_fb[kRawFB];
+    __shared__ uint4 s_st[NW][kRawStage];  // staged hits {event, src, dst, w}
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = wave_uniform(tid >> 6);
+    // the filter global -> LDS (LDS-DMA) before the first records are requested
+#pragma unroll
+    for (uint32_t c = 0; c < kRawFB / 2 / kRawBlock; ++c)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(ws.filter) + c * kRawBlock + tid,
+                                         reinterpret_cast<uint4*>(s_fb) + c * kRawBlock + (tid & ~63u), 16, 0, 0);
+    const uint32_t now = sload(clock);  // per-TG clock cache (brain.metal:63-68); C1: the pass-start value
+    const uint32_t v = wid * gridDim.x + blockIdx.x, W = gridDim.x * NW;
+    const uint32_t NG = ws.ng;
+    uint4* st = s_st[wid];
+    uint4 R[kRawD][kRawK];
+    // iteration d of group g: events g * 1024 + d * 256 + k * 64 + lane;
+    // past E a tombstone-like record that never passes
+    auto issue = [&](uint32_t d, uint32_t g) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t k = 0; k < kRawK; ++k) {
+            const uint64_t t = (uint64_t)g * kRawGroup + d * kRawIt + k * 64 + lane;
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 x = {kRawNone, kRawNone, 0u, 0u};
+            if (t < E) x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(syn) + t);
+            R[d][k] = make_uint4(x.x, x.y, x.z, x.w);
+        }
+    };
+    if (v < NG) {
+#pragma unroll
+        for (uint32_t d = 0; d < kRawD; ++d) issue(d, v);
+    }
+    __syncthreads();  // the filter in LDS (every wave's LDS-DMA done: vmcnt is waited by the barrier's release)
+    uint32_t seq = 0;           // survivors of this wave so far (its sequence)
+    uint32_t have = 0;          // chunks held
+    uint32_t cur = kRawNone, prev = kRawNone;  // the last two chunks' pool ids
+    uint32_t lim = kRawNone;    // sequence entries stored (kRawNone: all so far)
+    uint32_t n_g1 = 0;          // pre-gated events of this wave (diagnostics)
+    const uint32_t window = kp.window_pre, refr = kp.refractory;
+    for (uint32_t g = v; g < NG; g += W) {  // wave-uniform
+        uint32_t pend = 0, S = 0, C = 0;
+        const uint32_t seq0 = seq;
+        // the staged hits through the gates; survivors appended to the sequence
+        auto flush = [&]() {
+            constexpr uint32_t RR = kRawStage / 64;
+            uint4 e[RR];
+            uint32_t a[RR], b[RR];
+#pragma unroll
+            for (uint32_t r = 0; r < RR; ++r) {
+                const uint32_t q = r * 64 + lane;
+                e[r] = q < pend ? st[q] : make_uint4(0u, kRawNone, kRawNone, 0u);
+                const bool ok = e[r].y < n_nrn && e[r].z < n_nrn;
+                a[r] = ok ? lastF[e[r].y] : now;  // brain.metal:73 (exact, for the filter's hits)
+                b[r] = ok ? lastF[e[r].z] : now;  // brain.metal:79, in the same round trip
+            }
+            uint64_t m2[RR], mc[RR];
+            uint32_t n = 0;
+#pragma unroll
+            for (uint32_t r = 0; r < RR; ++r) {
+                const bool ok = e[r].y < n_nrn && e[r].z < n_nrn;
+                const bool g1 = ok && now - a[r] <= window;          // brain.metal:73-77
+                const bool g2 = g1 && now - b[r] > refr;             // brain.metal:79-83
+                const bool cand = g2 && spike_candidate(kp, __uint_as_float(e[r].w), e[r].x, now);  // brain.metal:91-92
+                m2[r] = __ballot(g2);
+                mc[r] = __ballot(cand);
+                n_g1 += (uint32_t)__popcll(__ballot(g1));
+                if (g2 && e[r].x == 0u) ws.hdr->t0 = 1u;             // event 0 reached the budget test (brain.metal:110)
+                e[r] = make_uint4(e[r].x, __float_as_uint((float)(now - b[r])) | (cand ? 0x80000000u : 0u), e[r].w,
+                                  e[r].z);
+                n += (uint32_t)__popcll(m2[r]);
+                C += (uint32_t)__popcll(mc[r]);
+            }
+            if (n == 0) {
+                pend = 0;
+                return;
+            }
+            // chunks for entries [seq, seq + n): at most two new ones
+            if (lim == kRawNone) {
+                while (have * kRawChunk < seq + n) {  // wave-uniform
+                    uint32_t id = 0;
+                    if (lane == 0) id = atomicAdd(&ws.hdr->chunks, 1u);
+                    id = wave_uniform(id);
+                    if (id >= ws.pool_chunks) {  // the pool is spent: the rest of the sequence is not stored
+                        lim = have * kRawChunk;
+                        break;
+                    }
+                    if (lane == 0) ws.ctab[(uint64_t)v * ws.maxc + have] = id;
+                    prev = cur;
+                    cur = id;
+                    ++have;
+                }
+            }
+            uint32_t o = seq;
+#pragma unroll
+            for (uint32_t r = 0; r < RR; ++r) {
+                const uint32_t x = o + mbcnt64(m2[r]);
+                if (((m2[r] >> lane) & 1u) && (lim == kRawNone || x < lim)) {
+                    const uint32_t c = x / kRawChunk, id = c == have - 1 ? cur : prev;
+                    ws.pool[(uint64_t)id * kRawChunk + (x % kRawChunk)] = e[r];
+                }
+                o += (uint32_t)__popcll(m2[r]);
+            }
+            seq += n;
+            S += n;
+            pend = 0;
+        };
+#pragma unroll
+        for (uint32_t d = 0; d < kRawD; ++d) {
+            uint32_t src[kRawK];
+            uint4 rc[kRawK];
+#pragma unroll
+            for (uint32_t k = 0; k < kRawK; ++k) rc[k] = R[d][k];
+            // this buffer's next group in flight first
+            if (g + W < NG) issue(d, g + W);
+            const uint32_t rel = g * kRawGroup + d * kRawIt;
+#pragma unroll
+            for (uint32_t k = 0; k < kRawK; ++k) src[k] = rc[k].x;
+#pragma unroll
+            for (uint32_t k = 0; k < kRawK; ++k) {
+                const bool h = raw_filter_pass(s_fb, src[k]);
+                const uint64_t bm = __ballot(h);
+                if (bm == 0) continue;  // wave-uniform
+                if (h) st[pend + mbcnt64(bm)] = make_uint4(rel + k * 64 + lane, rc[k].x, rc[k].y, rc[k].z);
+                pend += (uint32_t)__popcll(bm);
+                if (pend > kRawStage - 64) flush();
+            }
+        }
+        if (pend) flush();
+        if (lane == 0) {
+            ws.gcand[g] = C;
+            ws.ginfo[g] = make_uint2(S, seq0);
+        }
+    }
+    if (lane == 0) {
+        ws.wlim[v] = lim;
+        ws.wstat[v] = make_uint2(n_g1, seq);
     }
 }
 
-__global__ __launch_bounds__(kRawScanThreads) void k_raw_scan(RawWs ws, uint32_t tiles, uint32_t E, uint32_t* clock,
-                                                              uint32_t* budget, const float* reward, float* rbar,
-                                                              KernelParams kp)
+__global__ __launch_bounds__(kRawScanThreads) void k_raw_scan(RawWs ws, uint32_t E, uint32_t* clock, uint32_t* budget,
+                                                              const float* reward, float* rbar, KernelParams kp)
 {
-    __shared__ uint32_t s_wave[kRawScanThreads / 64];
+    __shared__ uint32_t s_wave[kRawScanThreads / 64], s_cut[kRawScanThreads / 64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t b0 = *budget;
-    const uint32_t per = (tiles + kRawScanThreads - 1) / kRawScanThreads, q0 = threadIdx.x * per;
+    const uint32_t b0 = *budget, NG = ws.ng;
+    const uint32_t per = (NG + kRawScanThreads - 1) / kRawScanThreads, q0 = threadIdx.x * per;
     uint64_t sum = 0;
-    for (uint32_t q = q0; q < q0 + per && q < tiles; ++q) sum += ws.cnt[q].y;
-    // block exclusive scan of the per-thread sums (capped: budgets are u32)
+    for (uint32_t q = q0; q < q0 + per && q < NG; ++q) sum += ws.gcand[q];
     const uint32_t v = (uint32_t)(sum < 0xFFFFFFFFull ? sum : 0xFFFFFFFFull);
-    uint32_t inc = wave_incl_scan(v);  // tiles x 2048 < 2^32 events: no overflow
+    const uint32_t inc = wave_incl_scan(v);  // groups x 1024 < 2^32 events: no overflow
     if (lane == 63) s_wave[wv] = inc;
     __syncthreads();
     uint32_t before = 0, total = 0;
@@ -168,53 +405,115 @@ __global__ __launch_bounds__(kRawScanThreads) void k_raw_scan(RawWs ws, uint32_t
         before += w < wv ? s_wave[w] : 0u;
         total += s_wave[w];
     }
-    uint32_t run = before + inc - v;
-    for (uint32_t q = q0; q < q0 + per && q < tiles; ++q) {
-        ws.pre[q] = run < b0 ? run : b0;
-        run += ws.cnt[q].y;
+    uint32_t run = before + inc - v, below = 0;
+    for (uint32_t q = q0; q < q0 + per && q < NG; ++q) {
+        ws.gpre[q] = run < b0 ? run : b0;
+        below += run < b0 ? 1u : 0u;  // the prefix is monotone: the groups below the cut are [0, gcut)
+        run += ws.gcand[q];
     }
+    const uint32_t bw = wave_incl_scan(below);
+    if (lane == 63) s_cut[wv] = bw;
+    // the gate waves' statistics (a wave past the last group wrote zeros)
+    uint64_t a1 = 0, a2 = 0;
+    for (uint32_t w = threadIdx.x; w < kRawWaves; w += kRawScanThreads) {
+        const uint2 x = ws.wstat[w];
+        a1 += x.x;
+        a2 += x.y;
+    }
+    __shared__ unsigned long long s_g[2];
+    if (threadIdx.x == 0) s_g[0] = s_g[1] = 0ull;
+    __syncthreads();
+    if (a1) atomicAdd(&s_g[0], (unsigned long long)a1);
+    if (a2) atomicAdd(&s_g[1], (unsigned long long)a2);
+    __syncthreads();
     if (threadIdx.x == 0) {
+        uint32_t gcut = 0;
+        for (uint32_t w = 0; w < kRawScanThreads / 64; ++w) gcut += s_cut[w];
         const uint32_t now = *clock;
         const float R = *reward, rb = *rbar;
         const uint32_t t0 = E > 0 ? ws.hdr->t0 : 0u;
         const uint32_t nc = total < b0 ? total : b0;
-        ws.hdr->now = now;
-        ws.hdr->budget0 = b0;
-        ws.hdr->ncand = nc;
-        ws.hdr->R = R;
-        ws.hdr->rb = rb;
+        RawHdr* h = ws.hdr;
+        h->now = now;
+        h->budget0 = b0;
+        h->ncand = nc;
+        h->R = R;
+        h->rb = rb;
+        h->gcut = gcut;
+        h->direct = b0 > ws.spike_cap ? 1u : 0u;
+        h->g1 = ws.ng ? s_g[0] : 0ull;
+        h->g2 = ws.ng ? s_g[1] : 0ull;
         *budget = b0 - nc;                                               // brain.metal:95-98 (C1: no wrap)
         if (t0 && b0 > 0) *rbar = rb + kp.alpha_rbar * (R - rb);         // brain.metal:110-113
         if (E > 0) *clock = now + kp.clock_inc;                          // brain.metal:129
     }
 }
 
-__global__ __launch_bounds__(kRawThreads) void k_raw_apply(uint4* syn, uint32_t* lastF, uint32_t tiles, KernelParams kp,
-                                                            RawWs ws)
+// One survivor below the budget's cut at budget position pre (< budget0):
+// the weight update (brain.metal:101-122, the record's w only) and, for a
+// spike, its budget slot.
+__device__ __forceinline__ void raw_apply_one(uint4* syn, uint32_t* lastF, const RawWs& ws, const RawHdr& h,
+                                              const KernelParams& kp, const uint4& e, bool cand, uint32_t pre)
+{
+    const float w = updated_weight(kp, __uint_as_float(e.z), cand, h.R, h.rb, __uint_as_float(e.y & 0x7FFFFFFFu));
+    reinterpret_cast<float*>(syn + e.x)[2] = w;  // brain.metal:122 (src, dst, pad unchanged)
+    if (cand) {
+        if (h.direct) lastF[e.w] = h.now;  // brain.metal:125-126 (no group recomputed: raw_apply_group)
+        else ws.spikes[pre] = e.w;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_raw_apply(uint4* syn, uint32_t* lastF, uint32_t n_nrn, uint32_t E,
+                                                   KernelParams kp, RawWs ws)
 {
     const uint32_t lane = threadIdx.x & 63;
     const RawHdr h = *ws.hdr;  // pass-start scalars (k_raw_scan)
-    const uint32_t nw = gridDim.x * kRawWaves;
-    for (uint32_t tile = blockIdx.x * kRawWaves + (threadIdx.x >> 6); tile < tiles; tile += nw) {  // wave-uniform
-        uint32_t P = ws.pre[tile];
-        if (P >= h.budget0) continue;
-        const uint32_t n = ws.cnt[tile].x;
-        const uint4* sv = ws.surv + (uint64_t)tile * kRawTile;
-        for (uint32_t b0 = 0; b0 < n && P < h.budget0; b0 += 64) {
-            const bool v = b0 + lane < n;
-            const uint4 e = v ? sv[b0 + lane] : make_uint4(0u, 0u, 0u, 0u);
-            const bool cand = v && (e.y >> 31);
-            const uint64_t bc = __ballot(cand);
-            const uint32_t pre = P + mbcnt64(bc);  // spike candidates before this event
-            if (v && pre < h.budget0) {
-                const float w = updated_weight(kp, __uint_as_float(e.z), cand, h.R, h.rb,
-                                               __uint_as_float(e.y & 0x7FFFFFFFu));  // brain.metal:101-121
-                reinterpret_cast<float*>(syn + e.x)[2] = w;  // brain.metal:122 (src, dst, pad unchanged)
-                if (cand) lastF[e.w] = h.now;                // brain.metal:125-126
+    const uint32_t nw = gridDim.x * 4u;
+    for (uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6); g < h.gcut; g += nw) {  // wave-uniform
+        uint32_t P = ws.gpre[g];
+        const uint2 gi = ws.ginfo[g];
+        const uint32_t S = gi.x, s0 = gi.y, v = g % kRawWaves, lim = ws.wlim[v];
+        if (S == 0) continue;
+        if (lim == kRawNone || s0 + S <= lim) {  // stored: walk the wave's sequence [s0, s0 + S)
+            const uint32_t* ct = ws.ctab + (uint64_t)v * ws.maxc;
+            for (uint32_t b0 = 0; b0 < S && P < h.budget0; b0 += 64) {  // wave-uniform
+                const uint32_t q = b0 + lane, x = s0 + q;
+                const bool ok = q < S;
+                const uint4 e = ok ? ws.pool[(uint64_t)ct[x / kRawChunk] * kRawChunk + x % kRawChunk] : make_uint4(0u, 0u, 0u, 0u);
+                const bool cand = ok && (e.y >> 31);
+                const uint64_t bc = __ballot(cand);
+                const uint32_t pre = P + mbcnt64(bc);  // spike candidates before this event
+                if (ok && pre < h.budget0) raw_apply_one(syn, lastF, ws, h, kp, e, cand, pre);
+                P += (uint32_t)__popcll(bc);
             }
+            continue;
+        }
+        // not stored (the pool ran out): the group again from its records,
+        // with the pass-start lastF (the stamps wait for k_raw_stamp)
+        if (h.direct && lane == 0) ws.hdr->err = 1u;
+        for (uint32_t b0 = 0; b0 < kRawGroup && P < h.budget0; b0 += 64) {  // wave-uniform
+            const uint64_t t = (uint64_t)g * kRawGroup + b0 + lane;
+            const uint4 r = t < E ? syn[t] : make_uint4(kRawNone, kRawNone, 0u, 0u);
+            const bool ok = r.x < n_nrn && r.y < n_nrn;
+            const uint32_t a = ok ? lastF[r.x] : h.now, b = ok ? lastF[r.y] : h.now;
+            const bool g2 = ok && h.now - a <= kp.window_pre && h.now - b > kp.refractory;  // brain.metal:73-83
+            const bool cand = g2 && spike_candidate(kp, __uint_as_float(r.z), t, h.now);    // brain.metal:91-92
+            const uint64_t bc = __ballot(cand);
+            const uint32_t pre = P + mbcnt64(bc);
+            if (g2 && pre < h.budget0)
+                raw_apply_one(syn, lastF, ws, h, kp,
+                              make_uint4((uint32_t)t, __float_as_uint((float)(h.now - b)), r.z, r.y), cand, pre);
             P += (uint32_t)__popcll(bc);
         }
     }
+}
+
+__global__ __launch_bounds__(1024) void k_raw_stamp(uint32_t* lastF, RawWs ws)
+{
+    const RawHdr* h = ws.hdr;
+    if (h->direct) return;
+    const uint32_t now = h->now, n = h->ncand;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) lastF[ws.spikes[i]] = now;  // brain.metal:125-126
 }
 
 __global__ __launch_bounds__(256) void k_raw_renorm(uint32_t* lastF, const uint32_t* clock, uint32_t n)
@@ -225,6 +524,18 @@ __global__ __launch_bounds__(256) void k_raw_renorm(uint32_t* lastF, const uint3
 }
 
 __global__ void k_raw_zero_clock(uint32_t* clock) { *clock = 0u; }  // brain.metal:144
+
+// abnn_debug_raw_gate_timing: an event pair around every gate launch (host
+// state of the diagnostics only; the pass never reads it).
+struct RawTiming {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+};
+RawTiming& raw_timing()
+{
+    static RawTiming t;
+    return t;
+}
 
 KernelParams raw_params(const abnn_traversal_args& a)
 {
@@ -250,28 +561,91 @@ uint64_t abnn_traversal_workspace_bytes(uint32_t n_syn, uint32_t events)
     return raw_ws_bytes(raw_events(n_syn, events));
 }
 
+uint64_t abnn_traversal_workspace_min_bytes(uint32_t n_syn, uint32_t events)
+{
+    return raw_fixed_bytes(raw_events(n_syn, events));
+}
+
 abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream)
 {
     if (!a || !a->clock || !a->budget || !a->reward || !a->rbar || !a->workspace ||
         (a->n_syn && (!a->syn || !a->last_fired)))
         return ABNN_ERR_INVALID;
     const uint64_t E = raw_events(a->n_syn, a->events);
-    if (a->workspace_bytes < raw_ws_bytes(E) || ((uintptr_t)a->workspace & 15u)) return ABNN_ERR_INVALID;
+    if (a->workspace_bytes < raw_fixed_bytes(E) || ((uintptr_t)a->workspace & 15u)) return ABNN_ERR_INVALID;
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    const uint64_t tiles = raw_tiles(E);
-    const RawWs ws = raw_ws(a->workspace, tiles);
+    const RawWs ws = raw_ws(a->workspace, E, a->workspace_bytes);
     const KernelParams kp = raw_params(*a);
     uint4* syn = reinterpret_cast<uint4*>(a->syn);
-    if (tiles)
-        hipLaunchKernelGGL(k_raw_gate, dim3((uint32_t)tiles), dim3(kRawThreads), 0, s, syn, a->last_fired, a->clock,
-                           a->n_nrn, (uint32_t)E, kp, ws);
-    hipLaunchKernelGGL(k_raw_scan, dim3(1), dim3(kRawScanThreads), 0, s, ws, (uint32_t)tiles, (uint32_t)E, a->clock,
-                       a->budget, a->reward, a->rbar, kp);
-    if (tiles) {
-        const uint32_t g = (uint32_t)std::min<uint64_t>((tiles + kRawWaves - 1) / kRawWaves, kRawApplyBlocks);
-        hipLaunchKernelGGL(k_raw_apply, dim3(g), dim3(kRawThreads), 0, s, syn, a->last_fired, (uint32_t)tiles, kp, ws);
+    hipLaunchKernelGGL(k_raw_filter, dim3(kRawFB / 8), dim3(256), 0, s, a->last_fired, a->clock, a->n_nrn, kp, ws);
+    if (ws.ng) {
+        RawTiming& tm = raw_timing();
+        std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+        if (tm.on && hipEventCreate(&ev.first) == hipSuccess && hipEventCreate(&ev.second) == hipSuccess)
+            (void)hipEventRecord(ev.first, s);
+        hipLaunchKernelGGL(k_raw_gate, dim3(kRawGateWGs), dim3(kRawBlock), 0, s, syn, a->last_fired, a->clock, a->n_nrn,
+                           (uint32_t)E, kp, ws);
+        if (ev.second) {
+            (void)hipEventRecord(ev.second, s);
+            tm.ev.push_back(ev);
+        }
+    }
+    hipLaunchKernelGGL(k_raw_scan, dim3(1), dim3(kRawScanThreads), 0, s, ws, (uint32_t)E, a->clock, a->budget, a->reward,
+                       a->rbar, kp);
+    if (ws.ng) {
+        const uint32_t g = (uint32_t)std::min<uint64_t>((ws.ng + 3) / 4, kRawApplyWGs);
+        hipLaunchKernelGGL(k_raw_apply, dim3(g), dim3(256), 0, s, syn, a->last_fired, a->n_nrn, (uint32_t)E, kp, ws);
+        hipLaunchKernelGGL(k_raw_stamp, dim3(1), dim3(1024), 0, s, a->last_fired, ws);
     }
     return hipGetLastError() == hipSuccess ? ABNN_OK : ABNN_ERR_HIP;
+}
+
+abnn_status abnn_traversal_workspace_error(const void* workspace, uint32_t* err, void* stream)
+{
+    if (!workspace || !err) return ABNN_ERR_INVALID;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const RawHdr* h = static_cast<const RawHdr*>(workspace);
+    if (hipMemcpyAsync(err, &h->err, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return ABNN_ERR_HIP;
+    return hipStreamSynchronize(s) == hipSuccess ? ABNN_OK : ABNN_ERR_HIP;
+}
+
+// Diagnostics (abnn_debug.h): the last pass's pre-gated / surviving events
+// from the workspace header, and HIP events around every k_raw_gate launch.
+abnn_status abnn_debug_raw_stats(const void* workspace, uint64_t* out2, void* stream)
+{
+    if (!workspace || !out2) return ABNN_ERR_INVALID;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const RawHdr* h = static_cast<const RawHdr*>(workspace);
+    if (hipMemcpyAsync(out2, &h->g1, 16, hipMemcpyDeviceToHost, s) != hipSuccess) return ABNN_ERR_HIP;
+    return hipStreamSynchronize(s) == hipSuccess ? ABNN_OK : ABNN_ERR_HIP;
+}
+
+abnn_status abnn_debug_raw_gate_timing(int enable)
+{
+    RawTiming& t = raw_timing();
+    for (auto& e : t.ev) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    t.ev.clear();
+    t.on = enable != 0;
+    return ABNN_OK;
+}
+
+abnn_status abnn_debug_raw_gate_time(double* total_ms, uint32_t* launches)
+{
+    if (!total_ms || !launches) return ABNN_ERR_INVALID;
+    RawTiming& t = raw_timing();
+    double ms = 0.0;
+    for (auto& e : t.ev) {
+        if (hipEventSynchronize(e.second) != hipSuccess) return ABNN_ERR_HIP;
+        float x = 0.0f;
+        if (hipEventElapsedTime(&x, e.first, e.second) != hipSuccess) return ABNN_ERR_HIP;
+        ms += x;
+    }
+    *total_ms = ms;
+    *launches = (uint32_t)t.ev.size();
+    return ABNN_OK;
 }
 
 abnn_status abnn_launch_renormalise(uint32_t* last_fired, uint32_t* last_visited, uint32_t* clock, uint32_t n_nrn,

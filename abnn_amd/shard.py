@@ -131,7 +131,8 @@ class NativeComm:
             _lib.call("abnn_comm_unique_id", uid.ctypes.data)
         on_gpu = dist.get_backend(group) == "nccl"
         t = torch.from_numpy(uid).to(torch.device("cuda", device) if on_gpu else "cpu")
-        dist.broadcast(t, 0, group=group)
+        src = dist.get_global_rank(group, 0) if group is not None else 0  # the group's rank 0
+        dist.broadcast(t, src, group=group)
         uid = np.ascontiguousarray(t.cpu().numpy())
         h = C.c_void_p()
         _lib.call("abnn_comm_create", uid.ctypes.data, self.world, self.rank, int(device), C.byref(h))
@@ -183,7 +184,14 @@ class ShardedBrain:
         self.engine = _GpuEngine(self.brain, lambda: torch.cuda.current_stream(dev))
         self.compact_every = int(self.brain.params.compact_every)
         self._updates = self.brain.structural_updates()
-        self.native = NativeComm(device) if native else None
+        self.native = None
+        if native:
+            # the RCCL communicator spans the same process group as `comm`:
+            # rank_offset and the gathered records' order follow its ranks
+            self.native = NativeComm(device, group=getattr(comm, "group", None))
+            if (self.native.world, self.native.rank) != (self.world, self.rank):
+                raise ValueError(f"native communicator is rank {self.native.rank}/{self.native.world}, "
+                                 f"the shard layout rank {self.rank}/{self.world}")
 
     def step(self, passes: int = 1) -> None:
         if self.native is not None:

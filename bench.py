@@ -62,7 +62,8 @@ def parse():
                          "the warm-up (the start-up transient, DESIGN.md §6)")
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline (0: every CPU this process may run on)")
     ap.add_argument("--cpu-passes", type=int, default=3)
     ap.add_argument("--mode", choices=["sweep", "random"], default="sweep",
                     help="sweep: event t visits synapse t (the reference kernel); random: "
@@ -73,6 +74,10 @@ def parse():
                     help="at one GPU, run the sharded pass (abnn_shard_traverse over the library's RCCL "
                          "communicator, world 1) instead of the fused single-GPU pass: its per-pass "
                          "overhead (DESIGN.md §7)")
+    ap.add_argument("--raw", action="store_true",
+                    help="the reference-layout path: abnn_launch_traversal (brain.metal's 14-buffer ABI) over "
+                         "caller-owned 16-B SynapsePacked records and u32 lastF at the config's sweep "
+                         "(DESIGN.md §5, include/abnn/abnn.h)")
     ap.add_argument("--plasticity", action="store_true",
                     help="config-5 dynamics: reward-modulated STDP (reward 0.25) with pruning "
                          "(w < 0.105) and synaptogenesis (p_new 0.25, w_init 0.5, +1%% capacity), "
@@ -124,6 +129,22 @@ def load_traffic(config: str):
     return t, None
 
 
+def host_cpus() -> dict:
+    """The CPUs the CPU baseline may use: the affinity set (what a thread pool
+    can be scheduled on), the machine's count, and the cgroup CPU quota when
+    one is set (a quota below the affinity set caps the threads' real rate)."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"available": avail, "machine": os.cpu_count(), "cgroup_quota_cpus": quota}
+
+
 def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, extra: dict,
                  settle: int) -> dict:
     """The threaded C oracle ("port") on the host cores.  Sweep: the pass only
@@ -156,8 +177,9 @@ def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, ex
     t0 = time.perf_counter()
     ob.pass_threaded(timed_passes, nthreads=threads)
     dt = time.perf_counter() - t0
-    return {"value": timed_passes * E / dt, "unit": "events/s", "cores": threads, "threads": threads,
-            "host_cpus": os.cpu_count(), "kind": "port",
+    hc = host_cpus()
+    return {"value": timed_passes * E / dt, "unit": "events/s", "cores": hc["available"], "threads": threads,
+            "host_cpus": hc["machine"], "cgroup_quota_cpus": hc["cgroup_quota_cpus"], "kind": "port",
             "n_syn": n_syn, "graph": ("reduced: %d of %d synapses, picks hit a smaller working set than "
                                       "the GPU's (likely overstates the CPU rate)" % (n_syn, wl.n_syn))
             if reduced else "same records as the GPU run",
@@ -165,8 +187,122 @@ def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, ex
                       f"oracle_pass_threaded with {threads} threads"}
 
 
+def raw_main(args) -> None:
+    """--raw: one step = one pass of abnn_launch_traversal over caller-owned
+    buffers in the reference's layouts (brain.cpp:52-69): the host's two
+    writes of encode_traversal / inject_inputs (lastF[inputs] = clock,
+    budget = kMaxSpikes; brain.cpp:82,90) as two tiny torch kernels, then
+    the launcher's kernels.  The record buffer holds all N_SYN records (16 GB
+    at config 3); its first E (the only ones a sweep reads) are the
+    build_random_graph recipe generated on the GPU by the handle API."""
+    import ctypes as C
+
+    import torch
+
+    from abnn_amd import CONFIGS, Brain, _lib
+
+    wl = CONFIGS[args.config]
+    events = args.events or wl.events
+    E = min((events + 255) // 256 * 256, wl.n_syn)
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    gen = Brain(wl.n_input, wl.n_output, wl.n_hidden, E, events, device=0)
+    gen.build_random_graph(1)
+    head = gen.download_synapses(0, E)
+    del gen
+    recs = torch.zeros((wl.n_syn, 4), dtype=torch.int32, device=dev)
+    recs[:E].copy_(torch.from_numpy(head.view(np.int32).reshape(-1, 4)))
+    del head
+    n_nrn = wl.n_neuron
+    lastF = torch.zeros(n_nrn, dtype=torch.int32, device=dev)
+    lastV = torch.zeros(n_nrn, dtype=torch.int32, device=dev)
+    scal = torch.zeros(4, dtype=torch.int32, device=dev)  # clock, budget, reward, rBar
+    nb = int(lib.abnn_traversal_workspace_bytes(wl.n_syn, events))
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    kp = _lib.default_params()
+    a = _lib.TraversalArgs()
+    p = scal.data_ptr()
+    a.syn, a.last_fired, a.last_visited, a.clock = recs.data_ptr(), lastF.data_ptr(), lastV.data_ptr(), p
+    a.n_syn, a.tau_vis, a.tau_pre = wl.n_syn, 50_000, 50_000
+    a.a_ltp, a.a_ltd, a.w_min, a.w_max = kp.a_ltp, kp.a_ltd, kp.w_min, kp.w_max
+    a.budget, a.reward, a.rbar = p + 4, p + 8, p + 12
+    a.n_nrn, a.events, a.knobs = n_nrn, events, None
+    a.workspace, a.workspace_bytes = ws.data_ptr(), nb
+
+    def step(n: int) -> None:
+        for _ in range(n):
+            lastF[:wl.n_input] = scal[0]  # inject_inputs, every input firing (brain.cpp:82)
+            scal[1] = kp.max_spikes       # encode_traversal resets the budget (brain.cpp:90)
+            if lib.abnn_launch_traversal(C.byref(a), None) != 0:
+                raise RuntimeError("abnn_launch_traversal failed")
+
+    ts = time.perf_counter()
+    step(args.settle)
+    torch.cuda.synchronize()
+    settle_s = time.perf_counter() - ts
+    step(args.warmup)
+    torch.cuda.synchronize()
+    g = (C.c_uint64 * 2)()
+    lib.abnn_debug_raw_gate_timing(1)
+    ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g1 = g2 = 0
+    t0 = time.perf_counter()
+    ev_a.record()
+    step(args.steps)
+    ev_b.record()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    lib.abnn_debug_raw_stats(ws.data_ptr(), g, None)  # the last pass's
+    g1, g2 = int(g[0]), int(g[1])
+    gate_ms, n_gate = C.c_double(), C.c_uint32()
+    lib.abnn_debug_raw_gate_time(C.byref(gate_ms), C.byref(n_gate))
+    lib.abnn_debug_raw_gate_timing(0)
+    region_ms = float(ev_a.elapsed_time(ev_b))
+    avg_gate_ms = gate_ms.value / max(1, n_gate.value)
+    stream_bytes = 16 * E
+    achieved = stream_bytes / (avg_gate_ms * 1e-3) / 1e9
+    # SURVEY §8(d) for the reference's own accesses, u32 timestamps (VERDICT r3
+    # item 3): 16 B record + 4 B lastF[src] per event, 4 B lastF[dst] per
+    # pre-gated event (+ 16 B per update and 4 B per spike, not counted: the
+    # update/stamp kernels, < 0.1 % of the bytes at config 3)
+    survey = 20 * E + 4 * g1
+    out = {
+        "metric": "traversal events/sec at 1B synapses, 5M neurons; achieved HBM GB/s",
+        "value": E * args.steps / dt, "unit": "events/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (build_random_graph recipe, portable RNG, generated on GPU)",
+        "config": {"workload": f"{wl.name} reference layout: abnn_launch_traversal over caller-owned "
+                               f"16-B records ({wl.n_syn:,} x 16 B) and u32 lastF",
+                   "n_neuron": n_nrn, "n_syn": wl.n_syn, "visited_events_per_pass": E,
+                   "workspace_bytes": nb, "settle_passes": args.settle, "settle_s": round(settle_s, 3),
+                   "last_pass_pre_gated": g1, "last_pass_survivors": g2,
+                   "host_writes_per_pass": "lastF[inputs] = clock, budget = kMaxSpikes (2 torch kernels)"},
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "k_raw_gate", "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": n_gate.value,
+            "launch_ms_source": "HIP event pair around every k_raw_gate launch (abnn_debug_raw_gate_timing)",
+            "algorithmic_bytes_per_launch": stream_bytes,
+            "bytes_formula": "16*E (the caller's 16-B SynapsePacked record per visited event; DESIGN.md §5)",
+            "survey_formula_bytes_per_launch": survey,
+            "survey_formula_achieved": round(survey / (avg_gate_ms * 1e-3) / 1e9, 1),
+            "survey_formula": "20*E + 4*G1 (SURVEY §8d with u32 lastF: record + lastF[src] per event, "
+                              "lastF[dst] per pre-gated; G1 of the last pass)",
+            "pass_ms_events": round(region_ms / args.steps, 4),
+        },
+        "cpu_baseline": None,
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.raw:
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+            raise SystemExit("--raw runs on one GPU")
+        raw_main(args)
+        return
     import torch
 
     from abnn_amd import CONFIGS, Brain
@@ -318,7 +454,8 @@ def main():
         }
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+            avail = host_cpus()["available"]
+            threads = avail if args.cpu_threads <= 0 else max(1, min(args.cpu_threads, avail))
             # random mode on the CPU is ~100x slower per pass: 6 settle passes
             cpu = cpu_baseline(wl, events, mode, threads, args.cpu_passes, extra,
                                args.settle if mode == 0 else min(args.settle, 6))

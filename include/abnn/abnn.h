@@ -356,10 +356,21 @@ uint64_t abnn_structural_updates(const abnn_brain* b);
  * clock tick.  The knobs the reference compiles in (#define BASE_SCALE ...,
  * brain.metal:22-31) come from `knobs` (NULL = the reference defaults; only
  * the #define fields are read -- aLTP..wMax are the buffer arguments).
- * Scratch: `workspace` of at least abnn_traversal_workspace_bytes(n_syn,
- * events) bytes of device memory (any contents; reused every pass).  This is
- * the reference's memory layout, so it streams 16 B per visited event and
- * gathers lastF for every one (the handle API's layout moves 3).
+ * Scratch: `workspace` of device memory (any contents; reused every pass),
+ * 16-B aligned: abnn_traversal_workspace_bytes(n_syn, events) is the
+ * recommended size (~60 MB at config 3: a bounded pool of refractory
+ * survivors, 1/64 of the visited events, plus per-1024-event counters),
+ * abnn_traversal_workspace_min_bytes the least accepted (no pool).  Survivors
+ * that do not fit the pool are recomputed from the records (slower, same
+ * results).  The spikes are stamped after the pass's last lastF read from a
+ * list of min(events, 65536) entries; a *budget above that stamps them
+ * directly, which is exact unless survivors also overflowed the pool -- then
+ * abnn_traversal_workspace_error reports 1 (the host's kMaxSpikes = 2560,
+ * brain.cpp:90, never comes near it).  This is the reference's memory
+ * layout, so it streams 16 B per visited event; the pre-spike test is
+ * answered from an LDS filter of lastF, which is gathered only for the ~1 %
+ * of events the filter passes (the handle API's layout moves
+ * 3 B per event).
  * renormalise_clock_and_times (brain.metal:135-145) on the same buffers:
  * lastF[i] -= *clock for i < n_nrn, then *clock = 0 (the host decides when,
  * brain.cpp:127-128).                                                         */
@@ -382,6 +393,10 @@ typedef struct abnn_traversal_args {
     uint64_t workspace_bytes;
 } abnn_traversal_args;
 uint64_t abnn_traversal_workspace_bytes(uint32_t n_syn, uint32_t events);
+uint64_t abnn_traversal_workspace_min_bytes(uint32_t n_syn, uint32_t events);
+/* synchronises `stream`: 1 if a pass since the last launch's start stamped
+ * directly while recomputing overflowed survivors (see above), else 0 */
+abnn_status abnn_traversal_workspace_error(const void* workspace, uint32_t* err, void* stream);
 abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream);
 abnn_status abnn_launch_renormalise(uint32_t* last_fired, uint32_t* last_visited, uint32_t* clock,
                                     uint32_t n_nrn, void* stream);
@@ -398,7 +413,12 @@ abnn_status abnn_launch_renormalise(uint32_t* last_fired, uint32_t* last_visited
  * abnn_shard_commit -- with no host round trip except after a structural
  * update (an all-reduce of the shards' visited events for the clock-tick
  * rule, then abnn_set_global_events).  abnn_comm_sync_visits is the lazy
- * all-reduce(MAX) of lastVisited (never read by a decision, brain.metal:44). */
+ * all-reduce(MAX) of lastVisited (never read by a decision, brain.metal:44).
+ * An error on any rank (a failed launch or collective, a pass error flag)
+ * leaves the other ranks inside the pass's collectives: the communicator is
+ * then marked unusable (every later abnn_shard_traverse on it returns
+ * ABNN_ERR_INVALID) and the caller must abort / destroy it on every rank, as
+ * after any NCCL error. */
 #define ABNN_COMM_ID_BYTES 128
 typedef struct abnn_comm abnn_comm;
 abnn_status abnn_comm_unique_id(void* id_out);

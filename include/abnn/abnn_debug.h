@@ -29,6 +29,14 @@ abnn_status abnn_debug_bitmap(abnn_brain* b, uint32_t* out, uint64_t n, int* inc
 /* The current sweep partition: n_ranges + 1 iteration bounds. */
 abnn_status abnn_debug_range_bounds(abnn_brain* b, uint32_t* out, uint64_t n);
 
+/* Buffer-index launcher (abnn_launch_traversal): the last pass's pre-gated
+ * and refractory-surviving events {g1, g2} from its workspace (synchronises
+ * `stream`); HIP events around every k_raw_gate launch while enabled (enable
+ * also clears them), their summed milliseconds and count. */
+abnn_status abnn_debug_raw_stats(const void* workspace, uint64_t* out2, void* stream);
+abnn_status abnn_debug_raw_gate_timing(int enable);
+abnn_status abnn_debug_raw_gate_time(double* total_ms, uint32_t* launches);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -363,12 +363,20 @@ private:
     // Host writes into the current Shared views (lastFired, clock) go to the
     // device before any other operation of this Brain (brain.cpp:55-57 are
     // StorageModeShared: the reference's host writes are seen by the next pass).
+    // The dirty views are collected against the version seen on entry: an
+    // upload bumps the version, so checking inside the loop would skip (and a
+    // later contents() would overwrite) the second view's write.  After the
+    // uploads every flushed view equals the device again.
     void flush_shared() const
     {
+        Buffer* dirty[2];
+        int n = 0;
         for (int k : {(int)Buffer::kLastFired, (int)Buffer::kClock}) {
             Buffer* v = views_[k].get();
-            if (v && v->mapped_ && v->version_ == version_ && v->host_ != v->pristine_) v->upload(0, v->count());
+            if (v && v->mapped_ && v->version_ == version_ && v->host_ != v->pristine_) dirty[n++] = v;
         }
+        for (int i = 0; i < n; ++i) dirty[i]->upload(0, dirty[i]->count());
+        for (int i = 0; i < n; ++i) dirty[i]->version_ = version_;
     }
     void touch() const  // before an operation that changes device state
     {

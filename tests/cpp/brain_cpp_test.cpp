@@ -81,15 +81,41 @@ int main()
             }
             if (!threw) throw std::runtime_error("budget_buffer() accepted a write");
         }
+        // Both Shared views (lastFired and the clock) written before the next
+        // device operation: both writes reach the device (brain.cpp:55-57).
+        bool shared_both_ok = false;
+        {
+            abnn::Brain sb(256, 256, 488, 10'000, 100'000);
+            sb.build_random_graph(1);
+            uint32_t* lf = (uint32_t*)sb.last_fired_buffer()->contents();
+            uint32_t* clk = (uint32_t*)sb.clock_buffer()->contents();
+            lf[300] = 4242u;
+            *clk = 5000u;
+            const abnn_scalars s0 = sb.scalars();            // a device operation flushes both
+            const uint64_t lf300 = sb.last_fired(300, 1)[0];
+            const uint32_t seen_clk = *(uint32_t*)sb.clock_buffer()->contents();
+            const uint32_t seen_lf = ((uint32_t*)sb.last_fired_buffer()->contents())[300];
+            lf = (uint32_t*)sb.last_fired_buffer()->contents();
+            clk = (uint32_t*)sb.clock_buffer()->contents();
+            lf[301] = 4999u;
+            *clk = 6000u;
+            sb.encode_traversal();                           // ... and so does a pass
+            sb.synchronize();
+            const abnn_scalars s1 = sb.scalars();
+            const uint64_t lf301 = sb.last_fired(301, 1)[0];
+            shared_both_ok = s0.clock == 5000u && lf300 == 4242u && seen_clk == 5000u && seen_lf == 4242u &&
+                             s1.clock == 6001u && (lf301 == 4999u || lf301 == 6000u);
+        }
         const abnn_scalars sc = brain.scalars();
         uint64_t lf_sum = 0;
         for (uint64_t v : brain.last_fired()) lf_sum += v;
         std::printf("{\"clock\": %" PRIu64 ", \"rbar\": %.9g, \"checksum\": %" PRIu64
                     ", \"copy_checksum\": %" PRIu64 ", \"last_fired_sum\": %" PRIu64
                     ", \"outputs_fired\": %" PRIu64 ", \"mismatch_thrown\": %s, \"views_checksum\": %" PRIu64
-                    ", \"budget_sum\": %" PRIu64 ", \"views_outputs\": %" PRIu64 "}\n",
+                    ", \"budget_sum\": %" PRIu64 ", \"views_outputs\": %" PRIu64 ", \"shared_both_ok\": %s}\n",
                     sc.clock, (double)sc.rbar, brain.checksum(), copy.checksum(), lf_sum,
-                    outputs_fired, mismatch_thrown ? "true" : "false", views_checksum, budget_sum, views_outputs);
+                    outputs_fired, mismatch_thrown ? "true" : "false", views_checksum, budget_sum, views_outputs,
+                    shared_both_ok ? "true" : "false");
         return 0;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());

@@ -18,10 +18,15 @@ def main():
     from abnn_amd.shard import ShardedBrain, TorchComm
 
     n_syn, events, passes = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
-    dist.init_process_group("gloo")
+    # "native": one GPU per rank, passes driven by the C-ABI over the
+    # library's RCCL communicator (abnn_shard_traverse); else ranks share GPU 0
+    # and exchange over gloo from Python
+    native = len(sys.argv) > 4 and sys.argv[4] == "native"
+    dev = int(os.environ.get("LOCAL_RANK", "0")) if native else 0
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl" if native else "gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    torch.cuda.set_device(0)
-    sb = ShardedBrain(TorchComm(), 256, 256, 30_000, n_syn, events, device=0, track_visits=1)
+    sb = ShardedBrain(TorchComm(), 256, 256, 30_000, n_syn, events, device=dev, track_visits=1, native=native)
     sb.brain.build_random_graph(4)
     sb.brain.set_auto_stimulus(0, 256)
     for k in range(passes):
@@ -30,7 +35,7 @@ def main():
         sb.step(1)
     torch.cuda.synchronize()
     sb.sync_visits()
-    ref = abnn_amd.Brain(256, 256, 30_000, n_syn, events, track_visits=1)
+    ref = abnn_amd.Brain(256, 256, 30_000, n_syn, events, track_visits=1, device=dev)
     ref.build_random_graph(4)
     ref.set_auto_stimulus(0, 256)
     for k in range(passes):
@@ -43,8 +48,10 @@ def main():
     ok &= bool(np.array_equal(sb.brain.last_fired(), ref.last_fired()))
     ok &= bool(np.array_equal(sb.brain.last_visited(), ref.last_visited()))
     ok &= sb.brain.scalars() == ref.scalars()
-    flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=f"cuda:{dev}" if native else "cpu")
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if sb.native is not None:
+        sb.native.close()
     if rank == 0:
         print("SHARDED_OK" if flag.item() == 1 else "SHARDED_MISMATCH", flush=True)
     dist.destroy_process_group()

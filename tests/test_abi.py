@@ -157,17 +157,35 @@ def test_src_code_is_a_bijection_matching_the_filter():
     assert np.array_equal((lo & 7) | (hi >> 6) << 3, (b + t) & 31)
 
 
+def _raw_ws_bytes(n_syn: int, events: int) -> tuple[int, int]:
+    """raw.hip's workspace: header, filter (8192 x 8 B), per 1024-event group
+    {candidates, prefix, survivors + sequence start}, per gate wave (4096) its
+    stored limit, statistics and chunk table, the spike list (min(E, 65536)) -- and the
+    recommended pool of 4-KiB survivor chunks: one per wave + E/64 entries + 64."""
+    al = lambda x: (x + 15) & ~15
+    E = min((events + 255) // 256 * 256, n_syn)
+    g, W = (E + 1023) // 1024, 4096
+    maxc = (g + W - 1) // W * 4 + 1
+    fixed = 64 + 8192 * 8 + 2 * al(4 * g) + al(8 * g) + al(4 * W) + al(8 * W) + al(4 * W * maxc) + al(4 * min(E, 65536))
+    pool = (W + (E // 64 + 255) // 256 + 64) * 4096 if E else 0
+    return fixed, fixed + pool
+
+
 def test_workspace_bytes_of_the_buffer_index_launcher():
-    """abnn_traversal_workspace_bytes: header + per-tile counts + a 16-B survivor
-    slot per visited event (min(roundup(events, 256), n_syn)), tiles of 2048."""
+    """abnn_traversal_workspace_bytes / _min_bytes: a bounded survivor pool
+    (~60 MB at config 3, was 16 B per visited event = 2.4 GB) over fixed
+    per-group and per-wave counters."""
     from abnn_amd import _lib
 
     lib = _lib.load()
+    for n_syn, ev in ((0, 100), (10_000, 100_000), (150_000_128, 150_000_000), (1_000_000_000, 150_000_000),
+                      (3_000, 4_097), (4_000_000_000, 4_000_000_000)):
+        fixed, rec = _raw_ws_bytes(n_syn, ev)
+        assert lib.abnn_traversal_workspace_min_bytes(n_syn, ev) == fixed, (n_syn, ev)
+        assert lib.abnn_traversal_workspace_bytes(n_syn, ev) == rec, (n_syn, ev)
     ws = lib.abnn_traversal_workspace_bytes
-    assert ws(0, 100) == 64
-    tiles = (10_000 + 2047) // 2048
-    assert ws(10_000, 100_000) == 64 + ((12 * tiles + 15) & ~15) + 16 * 2048 * tiles
     assert ws(1_000_000_000, 150_000_000) == ws(150_000_128, 150_000_000)  # only visited events
+    assert ws(1_000_000_000, 150_000_000) < 70_000_000  # bounded: < 0.5 B per visited event
 
 
 def test_launcher_rejects_bad_arguments():

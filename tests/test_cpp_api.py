@@ -71,3 +71,6 @@ def test_cpp_brain_matches_oracle(gpu):
     assert got["views_checksum"] == vb.checksum()
     assert got["budget_sum"] == budget_sum
     assert got["views_outputs"] == outputs
+    # lastFired and clock both written through their Shared views before one
+    # device operation: both writes reached the device (brain.hpp)
+    assert got["shared_both_ok"] is True

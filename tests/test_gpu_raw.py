@@ -18,7 +18,8 @@ pytestmark = pytest.mark.gpu
 class RawBrain:
     """Caller-owned buffers, as Brain::build_buffers allocates them (brain.cpp:52-69)."""
 
-    def __init__(self, syn: np.ndarray, n_nrn: int, events: int, max_spikes: int = 2560, knobs=None):
+    def __init__(self, syn: np.ndarray, n_nrn: int, events: int, max_spikes: int = 2560, knobs=None,
+                 pool_chunks=None):
         import torch
 
         from abnn_amd import _lib
@@ -31,7 +32,10 @@ class RawBrain:
         self.lastV = torch.zeros(n_nrn, dtype=torch.int32, device=dev)
         self.scal = torch.zeros(4, dtype=torch.int32, device=dev)  # clock, budget, reward, rBar
         self.n_syn, self.n_nrn, self.events, self.max_spikes = syn.shape[0], n_nrn, events, max_spikes
-        nb = int(self.lib.abnn_traversal_workspace_bytes(self.n_syn, events))
+        # pool_chunks: None = the recommended workspace, else the least one plus
+        # that many 4-KiB survivor chunks (0: every survivor recomputed)
+        nb = int(self.lib.abnn_traversal_workspace_bytes(self.n_syn, events)) if pool_chunks is None else \
+            int(self.lib.abnn_traversal_workspace_min_bytes(self.n_syn, events)) + 4096 * pool_chunks
         self.ws = torch.zeros(max(16, nb), dtype=torch.uint8, device=dev)
         self.knobs = knobs
         a = _lib.TraversalArgs()
@@ -46,6 +50,17 @@ class RawBrain:
         a.knobs = C.cast(C.pointer(knobs), C.c_void_p) if knobs is not None else None
         a.workspace, a.workspace_bytes = self.ws.data_ptr(), nb
         self.args = a
+
+    def pass_stats(self) -> tuple[int, int]:
+        """The last pass's {pre-gated, refractory survivors} (abnn_debug_raw_stats)."""
+        g = (C.c_uint64 * 2)()
+        assert self.lib.abnn_debug_raw_stats(self.ws.data_ptr(), g, None) == 0
+        return int(g[0]), int(g[1])
+
+    def workspace_error(self) -> int:
+        e = C.c_uint32(7)
+        assert self.lib.abnn_traversal_workspace_error(self.ws.data_ptr(), C.byref(e), None) == 0
+        return int(e.value)
 
     def set_clock(self, v: int) -> None:
         self.scal[0] = np.int32(np.uint32(v).view(np.int32))
@@ -78,7 +93,7 @@ class RawBrain:
 
 
 def _run(n_hidden, n_syn, events, passes, seed=1, max_spikes=2560, reward_at=None, tombstones=0, renorm_at=None,
-         clock0=0, knobs=None):
+         clock0=0, knobs=None, pool_chunks=None, threads=0):
     from oracle import oracle as O
 
     n_nrn = 512 + n_hidden
@@ -86,7 +101,7 @@ def _run(n_hidden, n_syn, events, passes, seed=1, max_spikes=2560, reward_at=Non
     over["max_spikes"] = max_spikes
     over["renorm_thresh"] = 2**64 - 1  # the raw launcher's host decides renormalisation (renorm_at below)
     o = O.OracleBrain(256, 256, n_hidden, n_syn, events, **over)
-    o.build_random_graph(seed, nthreads=8)
+    o.build_random_graph(seed, nthreads=max(8, threads))
     if tombstones:  # pruned records {0xFFFFFFFF, 0xFFFFFFFF} (abnn.h): never pass
         idx = np.arange(0, n_syn, max(1, n_syn // tombstones))[:tombstones]
         s = o.syn.copy()
@@ -94,7 +109,7 @@ def _run(n_hidden, n_syn, events, passes, seed=1, max_spikes=2560, reward_at=Non
         s["dst"][idx] = 0xFFFFFFFF
         o.set_synapses(s)
     o.set_scalars(clock0, 0.0, 0.0)
-    r = RawBrain(o.syn.copy(), n_nrn, events, max_spikes, knobs)
+    r = RawBrain(o.syn.copy(), n_nrn, events, max_spikes, knobs, pool_chunks)
     r.set_clock(clock0)
     for k in range(passes):
         if reward_at is not None and k == reward_at:
@@ -102,7 +117,11 @@ def _run(n_hidden, n_syn, events, passes, seed=1, max_spikes=2560, reward_at=Non
             r.set_reward(0.5)
         o.set_timestamps(range(256), o.clock)
         before = o.stats()["fired"]
-        o.pass_serial()
+        st0 = o.stats()
+        if threads:
+            o.pass_threaded(1, nthreads=threads)
+        else:
+            o.pass_serial()
         r.one_pass()
         if renorm_at is not None and k == renorm_at:  # the host's decision (brain.cpp:127-128)
             base = o.clock
@@ -115,6 +134,9 @@ def _run(n_hidden, n_syn, events, passes, seed=1, max_spikes=2560, reward_at=Non
         assert np.float32(rbar) == np.float32(o.s.rbar), k
         assert np.array_equal(r.last_fired(), (o.last_fired & np.uint64(0xFFFFFFFF)).astype(np.uint32)), k
         assert np.array_equal(r.records(), o.syn.view(np.uint32)), k
+        assert r.workspace_error() == 0, k
+        st1 = o.stats()
+        assert r.pass_stats() == (st1["pre_gated"] - st0["pre_gated"], st1["post_gated"] - st0["post_gated"]), k
     return o
 
 
@@ -154,31 +176,36 @@ def test_raw_knobs(gpu):
     _run(9_488, 100_000, 100_000, 8, knobs=k, reward_at=2)
 
 
-def test_raw_full_size_c3_sample_is_fast_enough(gpu):
-    """The reference layout at config 3's visited events (150M of 1B records:
-    the sweep reads only those): a few passes bit-exact on the property side
-    (clock, budget left, stamps only at the clock) -- the full-state oracle
-    comparison runs at the smaller sizes above."""
-    import time
+@pytest.mark.parametrize("pool_chunks", [0, 3, 4200])
+def test_raw_survivor_pool_overflow_recomputes(gpu, pool_chunks):
+    """Survivors that do not fit the bounded pool (none, a few chunks, one
+    chunk per gate wave and some) are recomputed from the records by
+    k_raw_apply with the pass-start lastF: the same results, the all-gated
+    passes 3-5 of a fresh graph included."""
+    o = _run(99_488, 1_000_000, 1_000_000, 10, reward_at=5, pool_chunks=pool_chunks)
+    assert o.stats()["post_gated"] > 1_000_000  # the transient overflowed every pool tried
 
-    import torch
 
-    n_nrn, n_syn, events = 5_000_512, 150_000_128, 150_000_000
+def test_raw_direct_stamps_with_pool_overflow_are_reported(gpu):
+    """A budget above the spike list (min(E, 65536) entries) stamps directly;
+    with survivors recomputed as well, abnn_traversal_workspace_error says
+    so (abnn.h)."""
     from oracle import oracle as O
 
-    o = O.OracleBrain(256, 256, n_nrn - 512, n_syn, events)
-    o.build_random_graph(1, nthreads=16)
-    r = RawBrain(o.syn, n_nrn, events)
-    del o
-    for k in range(8):
+    o = O.OracleBrain(256, 256, 99_488, 1_000_000, 1_000_000)
+    o.build_random_graph(1, nthreads=8)
+    r = RawBrain(o.syn.copy(), 100_000, 1_000_000, 10**8, pool_chunks=0)
+    for _ in range(5):  # passes 3-5: every event gated, candidates far beyond the budget list
         r.one_pass()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(4):
-        r.one_pass()
-    dt = (time.perf_counter() - t0) / 4
-    clock, budget, _ = r.scalars()
-    assert clock == 12 and 0 <= budget <= 2560
-    lf = r.last_fired()
-    assert lf.max() <= 11
-    print(f"raw launcher at c3: {dt * 1e3:.2f} ms per pass, {events / dt / 1e9:.1f} G events/s")
+    assert r.workspace_error() == 1
+
+
+def test_raw_config3_bit_exact_vs_threaded_oracle(gpu):
+    """The reference layout at config 3 (5,000,512 neurons; 150,000,128
+    visited events: the first records of the 1B graph, the only ones a sweep
+    reads): 16 passes from the fresh graph through its all-gated transient
+    into the budget-saturated steady state, every pass bit-exact against the
+    threaded oracle -- records, u32 lastF, clock, budget left, rBar."""
+    o = _run(5_000_000, 150_000_128, 150_000_000, 16, reward_at=9, threads=32)
+    st = o.stats()
+    assert st["fired"] >= 2560 * 8 and st["updated"] > st["fired"]

@@ -32,6 +32,27 @@ def test_two_rank_sharded_brain_equals_unsharded(gpu):
 
 
 @pytest.mark.gpu
+def test_native_rccl_two_ranks_two_gpus(gpu):
+    """The C-driven RCCL pass at world 2 (one GPU per rank, the in-place
+    ncclAllGather with two records, rank_offset of rank 1): every rank's shard,
+    lastFired, lastVisited and scalars equal the unsharded brain.  Needs two
+    GPUs: skipped on a one-GPU box, so it runs wherever a node has them
+    (UNVERIFIED on hardware until then: DESIGN.md §7)."""
+    import abnn_amd
+
+    if abnn_amd.device_count() < 2:
+        pytest.skip("needs 2 GPUs (native RCCL at world 2)")
+    n_syn = 2_000_000
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "helpers", "shard_worker.py"), str(n_syn), str(n_syn), "10", "native"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600,
+                       env={**os.environ, "OMP_NUM_THREADS": "4"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "SHARDED_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
 def test_native_rccl_shard_traverse_world1(gpu, monkeypatch):
     """The C-driven sharded pass (abnn_comm over RCCL, abnn_shard_traverse: gate,
     in-place ncclAllGather and apply/commit enqueued by the library, no Python
