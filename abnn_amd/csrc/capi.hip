@@ -350,32 +350,61 @@ abnn_status reset_ranges(abnn_brain* b)
     return ABNN_OK;
 }
 
-// README §5 structural update (contract in abnn.h): stable removal of the
-// tombstones into a fresh buffer, then the grown records in (pass, slot)
-// order while capacity lasts.  Synchronous; runs between passes.
+// README §5 structural update (contract in abnn.h): the tombstones' span
+// [a, z) closes up in order and the hole at its end takes the array's last D
+// records (or the tail shifts down), then the grown records are appended in
+// (pass, slot) order while capacity lasts.  Synchronous; runs between passes.
+// Only the span and D records move: the tally's bounds give the span's blocks,
+// which are compacted into the spare buffer (syn_alt) at their final places
+// and copied back, so a sweep's update costs O(events), not O(n_syn).
 abnn_status structural_update(abnn_brain* b)
 {
     DeviceState& d = b->d;
     const uint64_t n = b->dims.n_syn, cap = b->dims.syn_capacity;
     ST_TRY(sync_all(b));
     const uint64_t nb = (n + kCompactChunk - 1) / kCompactChunk;
-    uint32_t* dead = d.dead;  // tombstones per block, tallied by k_apply (null: pruning off)
+    uint32_t* dead = d.dead;  // tombstones per block: the weight update's pruning tally + uploads
     uint64_t* offsets = b->compact_offsets;
-    // Double-buffered: records past n_syn are never read as events (the gate
-    // masks lanes beyond the sweep, picks stay below n_syn), so the spare
-    // buffer needs no clearing.
-    const SynArrays dst = b->syn_alt;
-    std::vector<uint32_t> hc(nb);
-    std::vector<uint64_t> ho(nb);
+    const SynArrays alt = b->syn_alt;
     hipError_t e = hipSuccess;
-    if (dead && nb) e = hipMemcpy(hc.data(), dead, nb * 4, hipMemcpyDeviceToHost);
-    uint64_t live = 0;
-    for (uint64_t i = 0; i < nb; ++i) {
-        ho[i] = live;
-        live += std::min<uint64_t>(kCompactChunk, n - i * kCompactChunk) - (dead ? hc[i] : 0u);
+    uint64_t live = n;
+    if (dead && nb) {
+        // {first block, last block + 1, tombstones}, in offsets[0..2] (scratch until the offsets)
+        unsigned long long bounds[3] = {~0ull, 0ull, 0ull};
+        auto* dev = reinterpret_cast<unsigned long long*>(offsets);
+        e = hipMemcpy(dev, bounds, sizeof(bounds), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = launch_dead_bounds(dead, nb, dev, nullptr);
+        if (e == hipSuccess) e = hipMemcpy(bounds, dev, sizeof(bounds), hipMemcpyDeviceToHost);
+        const uint64_t D = bounds[2];
+        if (e == hipSuccess && D) {
+            const uint64_t bf = bounds[0], bl = bounds[1];  // blocks [bf, bl) hold every tombstone
+            std::vector<uint32_t> hc(bl - bf);
+            std::vector<uint64_t> ho(bl - bf);
+            e = hipMemcpy(hc.data(), dead + bf, hc.size() * 4, hipMemcpyDeviceToHost);
+            uint64_t o = bf * kCompactChunk;  // the records before the first tombstone keep their places
+            for (uint64_t i = 0; i < hc.size(); ++i) {
+                ho[i] = o;
+                o += std::min<uint64_t>(kCompactChunk, n - (bf + i) * kCompactChunk) - hc[i];
+            }
+            unsigned long long z = 0;  // 1 + the last tombstone (in block bl - 1)
+            if (e == hipSuccess) e = hipMemcpy(dev, &z, 8, hipMemcpyHostToDevice);
+            const uint64_t lb = (bl - 1) * kCompactChunk;
+            if (e == hipSuccess) e = launch_last_tomb(d.syn, lb, std::min<uint64_t>(kCompactChunk, n - lb), dev, nullptr);
+            if (e == hipSuccess) e = hipMemcpy(&z, dev, 8, hipMemcpyDeviceToHost);
+            if (e == hipSuccess && (z <= lb || z > n || z < D)) e = hipErrorUnknown;  // the tally and the records disagree
+            if (e == hipSuccess) e = hipMemcpy(offsets, ho.data(), ho.size() * 8, hipMemcpyHostToDevice);
+            // the span's live records at their final places in alt, then back
+            if (e == hipSuccess) e = launch_compact(d.syn, n, offsets, alt, bf, bl - bf, nullptr);
+            const uint64_t s0 = bf * kCompactChunk;
+            if (e == hipSuccess) e = launch_copy_records(alt, s0, d.syn, s0, z - D - s0, nullptr);
+            // the hole [z - D, z): the last D records, or the tail shifted down
+            if (e == hipSuccess)
+                e = n - z >= D ? launch_copy_records(d.syn, n - D, d.syn, z - D, D, nullptr)
+                               : launch_copy_records(d.syn, z, d.syn, z - D, n - z, nullptr);
+            if (e == hipSuccess) e = hipMemset(dead + bf, 0, (bl - bf) * 4);
+            live = n - D;
+        }
     }
-    if (e == hipSuccess && nb) e = hipMemcpy(offsets, ho.data(), nb * 8, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = launch_compact(d.syn, n, offsets, dst, nullptr);
     uint64_t added = 0;
     if (e == hipSuccess && d.grown) {
         const uint64_t slots = (uint64_t)b->params.compact_every * b->params.max_spikes;
@@ -388,19 +417,16 @@ abnn_status structural_update(abnn_brain* b)
                 std::memcpy(&w, &g[j].z, 4);
                 app.push_back({g[j].x, g[j].y, w, 0.0f});
             }
-        if (e == hipSuccess && !app.empty() && records_h2d(dst, live, app.size(), app.data()) != ABNN_OK)
+        if (e == hipSuccess && !app.empty() && records_h2d(d.syn, live, app.size(), app.data()) != ABNN_OK)
             e = hipErrorUnknown;
         if (e == hipSuccess) e = hipMemset(d.grown, 0, slots * sizeof(uint4));
         added = app.size();
     }
-    if (e == hipSuccess && dead && nb) e = hipMemset(dead, 0, nb * 4);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
         set_err(std::string("structural update: ") + hipGetErrorString(e));
         return ABNN_ERR_HIP;
     }
-    b->syn_alt = d.syn;
-    d.syn = dst;
     b->dims.n_syn = live + added;
     b->structural_updates += 1;
     uint64_t grown = 0;
@@ -899,8 +925,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (p.compact_every > 0) {  // structural updates: the compaction's second buffer + scratch
         const uint64_t nb = (cap + kCompactChunk - 1) / kCompactChunk;
         if ((s = alloc_syn(&b->syn_alt, cap + kDummyRecords, p.mode == ABNN_MODE_RANDOM)) != ABNN_OK) return fail(s);
-        if ((s = dalloc(&b->compact_offsets, nb)) != ABNN_OK) return fail(s);
-        if (p.w_prune > 0.0f && (s = dalloc(&d.dead, nb)) != ABNN_OK) return fail(s);
+        if ((s = dalloc(&b->compact_offsets, nb + 4)) != ABNN_OK) return fail(s);  // + the span's 3 words
+        // the tombstone tally: pruning's, and an upload's (a saved pruned brain)
+        if ((s = dalloc(&d.dead, nb)) != ABNN_OK) return fail(s);
     }
     if (genesis) {
         if ((s = dalloc(&d.g2src, iters * iter_events)) != ABNN_OK) return fail(s);

@@ -257,12 +257,20 @@ hipError_t launch_scan(const DeviceState& d, const KernelParams& kp, int32_t* xc
 hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int32_t* gathered,
                         uint32_t world, uint32_t rank, hipStream_t s);
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);
-// Structural update: stable compaction into `dst`, block b of kCompactChunk
-// records starting at offsets[b] (live counts from the k_apply tombstone tally).
 hipError_t launch_pack_src(const SynArrays& a, const uint32_t* in_dev, uint64_t first, uint64_t n, hipStream_t s);
 hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t first, uint64_t n, hipStream_t s);
+// Structural update (abnn.h contract, capi.hip structural_update): blocks
+// [b0, b0 + nblocks) of kCompactChunk records stably compacted into `dst`,
+// block b0 + i from offsets[i] on (live counts from the tombstone tally);
+// the tally's span {first block, last block + 1, tombstones}; the last
+// tombstone of a record range (z = its index + 1, atomicMax); a record copy
+// between non-overlapping ranges.
 hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offsets, const SynArrays& dst,
-                          hipStream_t s);
+                          uint64_t b0, uint64_t nblocks, hipStream_t s);
+hipError_t launch_dead_bounds(const uint32_t* dead, uint64_t nb, unsigned long long* out, hipStream_t s);
+hipError_t launch_last_tomb(const SynArrays& a, uint64_t base, uint64_t count, unsigned long long* z, hipStream_t s);
+hipError_t launch_copy_records(const SynArrays& from, uint64_t f0, const SynArrays& to, uint64_t t0, uint64_t count,
+                               hipStream_t s);
 // dead[] (pruning tally) recounted for the blocks that hold records [first, first + count) of n
 hipError_t launch_tally_dead(const SynArrays& a, uint64_t n, uint32_t* dead, uint64_t first, uint64_t count,
                              hipStream_t s);

@@ -2251,11 +2251,11 @@ __global__ __launch_bounds__(256) void k_renorm(DeviceState d, uint64_t base)
 // offsets[b] on, in four coalesced rounds of kCompactThreads consecutive
 // records (one block scan of the live flags per round), streaming both ways.
 __global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint64_t n, const uint64_t* offsets,
-                                                             SynArrays dst)
+                                                             SynArrays dst, uint64_t b0)
 {
     static_assert(kCompactThreads == kScanThreads, "block_exclusive_scan is sized for kScanThreads");
     __shared__ uint64_t s_wave[kCompactThreads / 64];
-    const uint64_t base = (uint64_t)blockIdx.x * kCompactChunk;
+    const uint64_t base = (b0 + blockIdx.x) * kCompactChunk;  // offsets[blockIdx.x] is block b0 + blockIdx.x's
     uint32_t rs[4];
     uint64_t rdw[4];
 #pragma unroll
@@ -2276,6 +2276,49 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint
             __builtin_nontemporal_store(rdw[j], reinterpret_cast<uint64_t*>(dst.dw + o + pre));
         }
         o += tot;
+    }
+}
+
+// The structural update's span (abnn.h contract): out = {first block with a
+// tombstone, last such block + 1, tombstones} from the per-block tally.
+__global__ __launch_bounds__(256) void k_dead_bounds(const uint32_t* dead, uint64_t nb, unsigned long long* out)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    unsigned long long lo = ~0ull, hi = 0, sum = 0;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < nb; b += stride) {
+        const uint32_t c = dead[b];
+        if (c) {
+            lo = lo < b ? lo : b;
+            hi = b + 1;
+            sum += c;
+        }
+    }
+    if (sum) {
+        atomicMin(out, lo);
+        atomicMax(out + 1, hi);
+        atomicAdd(out + 2, sum);
+    }
+}
+
+// z = 1 + the index of the last tombstone among records [base, base + count)
+__global__ __launch_bounds__(256) void k_last_tomb(SynArrays a, uint64_t base, uint64_t count, unsigned long long* z)
+{
+    unsigned long long m = 0;
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < count; k += (uint64_t)gridDim.x * 256)
+        if (src_of(a, base + k) == kSrcNone) m = base + k + 1;
+    if (m) atomicMax(z, m);
+}
+
+// Records [f0, f0 + count) of `from` to [t0, t0 + count) of `to` (the
+// ranges never overlap within one array): src code (and the random-mode
+// mirror) and {dst, w}.
+__global__ __launch_bounds__(256) void k_copy_records(SynArrays from, uint64_t f0, SynArrays to, uint64_t t0,
+                                                      uint64_t count)
+{
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < count; k += (uint64_t)gridDim.x * 256) {
+        set_src(to, t0 + k, src_of(from, f0 + k));
+        __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(from.dw + f0 + k)),
+                                    reinterpret_cast<uint64_t*>(to.dw + t0 + k));
     }
 }
 
@@ -2587,11 +2630,35 @@ hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t fir
 }
 
 hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offsets, const SynArrays& dst,
-                          hipStream_t s)
+                          uint64_t b0, uint64_t nblocks, hipStream_t s)
 {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compact, dim3((uint32_t)((n + kCompactChunk - 1) / kCompactChunk)),
-                       dim3(kCompactThreads), 0, s, syn, n, offsets, dst);
+    if (n == 0 || nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_compact, dim3((uint32_t)nblocks), dim3(kCompactThreads), 0, s, syn, n, offsets, dst, b0);
+    return hipGetLastError();
+}
+
+hipError_t launch_dead_bounds(const uint32_t* dead, uint64_t nb, unsigned long long* out, hipStream_t s)
+{
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dead_bounds, dim3((uint32_t)std::min<uint64_t>((nb + 255) / 256, 1024)), dim3(256), 0, s,
+                       dead, nb, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_last_tomb(const SynArrays& a, uint64_t base, uint64_t count, unsigned long long* z, hipStream_t s)
+{
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_last_tomb, dim3((uint32_t)std::min<uint64_t>((count + 255) / 256, 64)), dim3(256), 0, s, a,
+                       base, count, z);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_records(const SynArrays& from, uint64_t f0, const SynArrays& to, uint64_t t0, uint64_t count,
+                               hipStream_t s)
+{
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_copy_records, dim3((uint32_t)std::min<uint64_t>((count + 255) / 256, 8192)), dim3(256), 0, s,
+                       from, f0, to, t0, count);
     return hipGetLastError();
 }
 

@@ -140,9 +140,14 @@ typedef struct abnn_params {
  *     record {src of the firing synapse, n_input + ((x & 0xFFFFFFFF) *
  *     (N_NRN - n_input) >> 32), w_init, 0};
  *   structural update, after every pass whose ticked pass_index is a multiple
- *     of compact_every: tombstones are removed by a stable compaction, then
- *     the synapses grown since the previous update are appended in (pass,
- *     slot) order while n_syn < syn_capacity.  n_syn, the visited events and
+ *     of compact_every: the tombstones are removed -- their span [a, z)
+ *     (first tombstone to last, D of them) closes up in order, and the D-
+ *     record hole left at its end, [z - D, z), takes the array's last D
+ *     records in order if the tail [z, n_syn) holds at least D records, else
+ *     the tail shifts down by D (O(z - a + D) records move; a sweep prunes
+ *     only inside its visited window, so the update costs O(events), not
+ *     O(n_syn)); then the synapses grown since the previous update are
+ *     appended in (pass, slot) order while n_syn < syn_capacity.  n_syn, the visited events and
  *     the borrowed synapse pointer (abnn_state_ptrs) change here.  Sweep-mode
  *     event ids stay syn_offset + local index (syn_offset is fixed). */
 #define ABNN_GENESIS_KEY 0xA24BAED4963EE407ull

@@ -289,9 +289,29 @@ static void structural_update(oracle_state* s)
 {
     const abnn_params* p = &s->p;
     if (p->compact_every == 0 || s->pass_index % p->compact_every != 0) return;
-    uint64_t n = 0;
-    for (uint64_t i = 0; i < s->dims.n_syn; ++i)
-        if (s->syn[i].src != kTomb) s->syn[n++] = s->syn[i];
+    /* Removal (abnn.h contract): the tombstones' span [a, z) closes up in
+     * order; the D-record hole left at its end [z - D, z) takes the array's
+     * last D records in order when the tail [z, n) holds at least D of them,
+     * else the tail shifts down by D.  Records outside the span and the moved
+     * ones keep their order; the work is O(z - a + D), not O(n) -- in a sweep
+     * the span lies in the visited window. */
+    uint64_t n = s->dims.n_syn, a = n, z = 0, D = 0;
+    for (uint64_t i = 0; i < n; ++i)
+        if (s->syn[i].src == kTomb) {
+            if (a == n) a = i;
+            z = i + 1;
+            D++;
+        }
+    if (D) {
+        uint64_t o = a;
+        for (uint64_t i = a; i < z; ++i)
+            if (s->syn[i].src != kTomb) s->syn[o++] = s->syn[i];  /* o ends at z - D */
+        if (n - z >= D)
+            memcpy(s->syn + (z - D), s->syn + (n - D), D * sizeof(abnn_synapse));  /* disjoint: n - D >= z */
+        else
+            memmove(s->syn + (z - D), s->syn + z, (n - z) * sizeof(abnn_synapse));
+        n -= D;
+    }
     const uint64_t slots = (uint64_t)p->compact_every * p->max_spikes;
     for (uint64_t j = 0; s->grown && j < slots; ++j) {
         uint32_t flag;

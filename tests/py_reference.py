@@ -197,11 +197,22 @@ class MetalEmu:
                     self.lastV[dv] = now_tg
         self.pass_index += 1
         ce = p.get("compact_every", 0)
-        if ce and self.pass_index % ce == 0:          # structural update
-            keep = [i for i in range(len(self.src)) if self.src[i] != TOMB]
-            self.src = [self.src[i] for i in keep]
-            self.dst = [self.dst[i] for i in keep]
-            self.w = [self.w[i] for i in keep]
+        if ce and self.pass_index % ce == 0:          # structural update (abnn.h contract)
+            # the tombstones' span [a, z): its live records close up in order,
+            # the D-record hole left at its end takes the array's last D
+            # records (or the whole tail shifts down when it is shorter)
+            tombs = [i for i in range(len(self.src)) if self.src[i] == TOMB]
+            if tombs:
+                a, z, n, D = tombs[0], tombs[-1] + 1, len(self.src), len(tombs)
+                recs = list(zip(self.src, self.dst, self.w))
+                mid = [r for r in recs[a:z] if r[0] != TOMB]
+                if n - z >= D:
+                    recs = recs[:a] + mid + recs[n - D:] + recs[z:n - D]
+                else:
+                    recs = recs[:a] + mid + recs[z:]
+                self.src = [r[0] for r in recs]
+                self.dst = [r[1] for r in recs]
+                self.w = [r[2] for r in recs]
             for slot in sorted(self.grown):
                 if len(self.src) < self.capacity:
                     s_, d_, w_ = self.grown[slot]

@@ -120,27 +120,37 @@ def test_c4_eight_virtual_shards_of_the_1b_graph(gpu):
 
 
 def test_c5_4b_records_plasticity(gpu):
-    """Config 5's size on one GPU: 4e9 records (44 GB of packed records, twice
-    for the structural update's second buffer), sweep mode, reward 0.25,
-    pruning and synaptogenesis with a structural update every 10 passes (two
-    inside the test).  Every pass: at most max_spikes spikes, one clock tick,
-    n_syn = n_syn(before) - pruned + grown across updates, no tombstone left
-    in the swept window after an update.  At the end the first E visited
-    records, every neuron's lastFired and the statistics are bit-exact against
-    the threaded oracle holding only the first E + 4M records (the sweep never
-    reaches past E; pruning only shifts the window by the removed records)."""
+    """Config 5's size on one GPU: 4e9 records (44 GB of packed records, plus
+    the structural update's spare buffer), sweep mode, reward 0.25, pruning
+    and synaptogenesis with a structural update every 10 passes (two inside
+    the test).  Every pass: at most max_spikes spikes, one clock tick, n_syn =
+    n_syn(before) - pruned + grown across updates, no tombstone left in the
+    swept window after an update.  The threaded oracle holds the graph's
+    first E + 4M records and its LAST 6M (the update's removal moves only
+    the tombstones' span, inside the window, and the array's last D records:
+    abnn.h), so at the end the GPU's whole array is pinned: the head and the
+    tail (grown records included) bit-exact, the untouched middle by the
+    whole-array checksum (the fresh graph's, less the head's and tail's)."""
     import abnn_amd
     from oracle import oracle as O
 
     n_in, n_out, n_hid, n_syn, events = 256, 256, 5_000_000, 4_000_000_000, 150_000_000
+    n_nrn = n_in + n_out + n_hid
     extra = dict(w_prune=0.105, p_new=0.25, w_init=0.5, compact_every=10)
     grow = 1_000_000
     g = abnn_amd.Brain(n_in, n_out, n_hid, n_syn, events, syn_capacity=n_syn + grow, **extra)
     E = g.visited_events()
-    slack = 4_000_000
-    o = O.OracleBrain(n_in, n_out, n_hid, E + slack, events, syn_capacity=E + slack + grow, **extra)
+    slack, K = 4_000_000, 6_000_000
+    H = E + slack
+    head = O.gen_synapses(0, H, n_in, n_out, n_nrn, 1, 16)
+    tail = O.gen_synapses(n_syn - K, K, n_in, n_out, n_nrn, 1, 16)
+    mid = n_syn - K - H
+    o = O.OracleBrain(n_in, n_out, n_hid, H + K, events, syn_capacity=H + K + grow, **extra)
+    o.set_synapses(np.concatenate([head, tail]))
     g.build_random_graph(1)
-    o.build_random_graph(1, nthreads=16)
+    M = (1 << 64) - 1
+    mid_ck = (g.checksum() - O.checksum(head, 0) - O.checksum(tail, n_syn - K)) & M  # the untouched middle
+    del head, tail
     for x in (g, o):
         x.set_auto_stimulus(0, n_in)
         x.set_reward(0.25)
@@ -164,14 +174,20 @@ def test_c5_4b_records_plasticity(gpu):
         prev = st
     assert g.structural_updates() == 2 and st["pruned"] > 0 and st["grown"] > 0
     o.pass_threaded(25, nthreads=16)
-    assert st["pruned"] <= slack
+    assert st["pruned"] <= slack and st["pruned"] <= K
     so = o.stats()
     assert so == st
     assert np.array_equal(g.last_fired(), o.last_fired)
     sg = g.scalars()
     assert sg["clock"] == o.clock and np.float32(sg["rbar"]) == np.float32(o.s.rbar)
+    # the whole array: GPU = head ++ middle (untouched) ++ rest, oracle = head ++ rest
+    osyn = o.syn
+    assert g.n_syn() == osyn.shape[0] + mid
     step = 10_000_000
-    for first in range(0, E, step):
-        n = min(step, E - first)
+    for first in range(0, H, step):
+        n = min(step, H - first)
         assert np.array_equal(g.download_synapses(first, n).view(np.uint32),
-                              o.syn[first:first + n].view(np.uint32)), f"records [{first}, {first + n})"
+                              osyn[first:first + n].view(np.uint32)), f"records [{first}, {first + n})"
+    rest = osyn[H:]
+    assert np.array_equal(g.download_synapses(H + mid, rest.shape[0]).view(np.uint32), rest.view(np.uint32))
+    assert g.checksum() == (O.checksum(osyn[:H], 0) + mid_ck + O.checksum(rest, H + mid)) & M

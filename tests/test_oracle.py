@@ -306,9 +306,11 @@ def _sp_brain(mode=0, cap_extra=20_000, n_hidden=3000, n_syn=120_000, events=120
     return ob
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_structural_plasticity_matches_python_restatement(mode):
-    ob = _sp_brain(mode, events=30_000 if mode else 120_000, track_visits=1)
+# sweep of the whole array (the tail shifts down), a sweep of its first third
+# (the hole takes the array's last records), random picks
+@pytest.mark.parametrize("mode,events", [(0, 120_000), (0, 90_000), (1, 30_000)])
+def test_structural_plasticity_matches_python_restatement(mode, events):
+    ob = _sp_brain(mode, events=events, track_visits=1)
     emu = _emu_from(ob, ob.s.dims.events_per_pass)
     emu.p.update(SP)
     emu.p["track_visits"] = 1
@@ -331,6 +333,36 @@ def test_structural_plasticity_matches_python_restatement(mode):
     st = ob.stats()
     assert st["pruned"] == emu.pruned > 0 and st["grown"] == emu.n_grown > 0
     assert len(set(sizes)) > 1  # the graph changed size
+
+
+@pytest.mark.parametrize("tombs,expect", [
+    # span [2, 5), D = 2: live 3 closes up; the hole [3, 5) takes 18, 19
+    ([2, 4], [0, 1, 3, 18, 19] + list(range(5, 18))),
+    # span [0, 1): the hole is the first record
+    ([0], [19] + list(range(1, 19))),
+    # span [15, 19), D = 3, tail [19, 20) shorter than D: it shifts down
+    ([15, 17, 18], list(range(15)) + [16, 19]),
+    # the last record: span [19, 20), tail empty
+    ([19], list(range(19))),
+    # every record
+    (list(range(20)), []),
+])
+def test_structural_update_removal_contract(tombs, expect):
+    """The removal of abnn.h's structural update on a hand-made array (no
+    pass work: 0 events, an update after every pass): the tombstones' span
+    closes up, its hole takes the array's last D records, or the tail shifts
+    down when it holds fewer than D."""
+    ob = O.OracleBrain(256, 256, 100, 20, 0, compact_every=1, w_prune=0.1, syn_capacity=20)
+    syn = np.zeros(20, dtype=O.SYN_DTYPE)
+    syn["src"] = 256 + np.arange(20)
+    syn["dst"] = np.arange(20)  # record identity
+    syn["w"] = 0.5
+    syn["src"][tombs] = 0xFFFFFFFF
+    syn["dst"][tombs] = 0xFFFFFFFF
+    ob.set_synapses(syn)
+    ob.pass_serial()
+    assert int(ob.s.dims.n_syn) == len(expect)
+    assert ob.syn["dst"].tolist() == expect
 
 
 def test_structural_update_semantics():

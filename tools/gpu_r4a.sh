@@ -1,8 +1,18 @@
+#!/bin/bash
+# Round 4, first GPU call: the raw launcher's tests and bench, the structural
+# update's tests (plasticity suite, c5 full size), bench with plasticity, then
+# the SQ counters of the unchanged fused pass and the CPU baseline's scaling.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_raw.py tests/test_cpp_api.py -m gpu -x -v --timeout 500 --timeout-method thread > gpurun_out/raw_tests.log 2>&1 || { echo "raw tests failed"; tail -30 gpurun_out/raw_tests.log; exit 1; }
-tail -3 gpurun_out/raw_tests.log
-timeout -k 10 300 python -u bench.py --raw --steps 50 > gpurun_out/bench_raw.json 2> gpurun_out/bench_raw.err || { echo "raw bench failed"; tail -20 gpurun_out/bench_raw.err; exit 1; }
+(while sleep 50; do date +%s >> gpurun_out/heartbeat.txt; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+t() { timeout -k 10 "$@"; }
+t 700 python -u -m pytest tests/test_gpu_raw.py tests/test_cpp_api.py tests/test_gpu_plasticity.py tests/test_sharded_gpu.py -m gpu -x -v --timeout 600 --timeout-method thread > gpurun_out/r4a_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/r4a_tests.log; exit 1; }
+tail -3 gpurun_out/r4a_tests.log
+t 300 python -u bench.py --raw --steps 50 > gpurun_out/bench_raw.json 2> gpurun_out/bench_raw.err || { echo "raw bench failed"; tail -20 gpurun_out/bench_raw.err; exit 1; }
 cat gpurun_out/bench_raw.json
-timeout -k 10 240 python3 tools/pass_times.py 300 > gpurun_out/pt_base.txt 2>&1 && tools/sq_profile.sh gpurun_out/sq_base.txt && timeout -k 10 300 python3 tools/cpu_scaling.py 3 16 64 all > gpurun_out/cpu_scaling.txt 2>&1
+t 400 python -u bench.py --plasticity --steps 100 --no-cpu-baseline > gpurun_out/bench_c3p.json 2> gpurun_out/bench_c3p.err || { echo "c3p bench failed"; tail -20 gpurun_out/bench_c3p.err; exit 1; }
+t 900 python -u -m pytest tests/test_gpu_scale.py -k c5 -m gpu -x -v --timeout 850 --timeout-method thread > gpurun_out/r4a_c5.log 2>&1 || { echo "c5 test failed"; tail -40 gpurun_out/r4a_c5.log; exit 1; }
+tail -3 gpurun_out/r4a_c5.log
