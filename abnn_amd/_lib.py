@@ -234,6 +234,8 @@ def load() -> C.CDLL:
     _share_hip_runtime_with_torch()
     lib = C.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES + DEBUG_SIGNATURES:
+        if (name, res, args) in DEBUG_SIGNATURES and not hasattr(lib, name):
+            continue  # an older variant build (A/B timing) without this diagnostic
         fn = getattr(lib, name)  # AttributeError = the ABI is not exported
         fn.restype = res
         fn.argtypes = args

@@ -855,13 +855,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.chunk_penalty = 600;  // 24 us per full chunk: the dense input->output stretch spread over more
                             // ranges (ABNN_CHUNK_PENALTY: 25 -> 350 measured -6 us per pass in round 2;
                             // 600 with the 1024x8 gate, profiles/r03l_ab_k8.txt)
-    d.tail_prio = 0;  // a range's tail at the lowest issue priority: the streams still running go first
     d.apply_blocks = kWalkBlocks;
     if (const char* env = std::getenv("ABNN_APPLY_BLOCKS"))
         d.apply_blocks = (uint32_t)std::min<int>(kWalkBlocks, std::max(1, std::atoi(env)));
-    d.prio_clock = 0;
-    if (const char* env = std::getenv("ABNN_PRIO_CLOCK")) d.prio_clock = std::atoi(env) ? 1u : 0u;
-    if (const char* env = std::getenv("ABNN_TAIL_PRIO")) d.tail_prio = (uint32_t)std::min(4, std::max(0, std::atoi(env)));
     if (const char* env = std::getenv("ABNN_CHUNK_PENALTY")) d.chunk_penalty = (uint32_t)std::max(0, std::atoi(env));
     d.fused_max_blocks = (uint32_t)std::max(0, fused_blocks_per_cu(gate_block, gate_k, filter_words, p.track_visits != 0)) *
                          (uint32_t)cus;
@@ -895,19 +891,11 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.spec_mode = 1;
     d.spec_margin = -1;
     if (const char* env = std::getenv("ABNN_SPEC_MARGIN")) d.spec_margin = std::atoi(env);
-    d.cost_tail = 1;
-    if (const char* env = std::getenv("ABNN_COST_TAIL")) d.cost_tail = std::atoi(env) ? 1u : 0u;
     d.flush_at = kChunk;
     if (const char* env = std::getenv("ABNN_FLUSH_AT"))
         d.flush_at = (uint32_t)std::min<int>((int)kChunk, std::max(64, std::atoi(env)));
     d.lean = 1;
     if (const char* env = std::getenv("ABNN_LEAN")) d.lean = std::atoi(env) != 0;
-    d.wt_sc1 = 0;
-    if (const char* env = std::getenv("ABNN_WT_SC1")) d.wt_sc1 = std::atoi(env) != 0;
-    d.lds_tail = 1;
-    if (const char* env = std::getenv("ABNN_LDS_TAIL")) d.lds_tail = std::atoi(env) != 0;
-    d.next_helpers = 1;
-    if (const char* env = std::getenv("ABNN_NEXT_HELPERS")) d.next_helpers = std::atoi(env) != 0;
     if (const char* env = std::getenv("ABNN_SPEC")) d.spec_mode = (uint32_t)std::min(2, std::max(0, std::atoi(env)));
     d.bitmap = b->bitmap_buf[0];
     d.filter = b->filter_buf[0];

@@ -160,8 +160,6 @@ struct DeviceState {
     uint32_t adapt_gain;      // a boundary moves adapt_gain / 4 of the way to its target (1..4, ABNN_ADAPT_GAIN; default 1)
     uint32_t chunk_penalty;   // partition cost added per full chunk, 40-ns units (ABNN_CHUNK_PENALTY)
     uint32_t apply_blocks;    // k_claim / k_apply grid (<= kWalkBlocks; ABNN_APPLY_BLOCKS)
-    uint32_t tail_prio;       // gate issue priority for a wave's tail, 0..3 (4: keep; ABNN_TAIL_PRIO, default 0)
-    uint32_t prio_clock;      // gate priority rotation by wall clock (1) or by iteration (0; ABNN_PRIO_CLOCK)
     uint32_t range_map;       // gate wave -> range: 0 blocked (workgroup b: ranges b*NW..), 1 interleaved (ABNN_RANGE_MAP=1)
     // fused pass: look-back words [gate_blocks]; gate costs of the previous
     // pass (read by the prologue when prologue_adapt) and of this one
@@ -170,19 +168,12 @@ struct DeviceState {
     uint32_t* cost_out;
     uint2* cand_list;         // fused: per range its first kCandCap spike candidates {survivor index, dst}
                               // ([kFusedMaxRanges * kCandCap]; the walk reads these, not every survivor)
-    uint32_t cost_tail;       // fused: a range's partition cost includes its tail (default; ABNN_COST_TAIL=0: off)
     uint32_t flush_at;        // fused: staged events that send a wave's stage through the refractory stage
                               // (<= kChunk; ABNN_FLUSH_AT)
     int32_t spec_margin;      // fused: workgroups predicted below the cut = last cut + spec_margin (ABNN_SPEC_MARGIN, -1)
     uint32_t spec_mode;       // fused: speculative weight stores 0 off, 1 below the predicted cut (default),
                               // 2 everywhere (ABNN_SPEC; 2 exercises the restore path)
-    uint32_t next_helpers;    // fused: the next bitmap's pass-independent items go to the workgroups past the
-                              // predicted cut, after their look-back (1, default), or to every workgroup
-                              // while it publishes (0; ABNN_NEXT_HELPERS)
-    uint32_t lds_tail;        // fused: a range's last refractory stage keeps its survivors in LDS for the
-                              // walk (1, default; ABNN_LDS_TAIL=0: in g2x like the others)
     uint32_t lean;            // fused single-GPU pass without plasticity: the lean kernel (ABNN_LEAN, default 1)
-    uint32_t wt_sc1;          // weight stores write-through (sc1) instead of non-temporal (ABNN_WT_SC1)
     uint32_t shard_mode;      // fused pass = the first launch of a sharded pass (k_gate: no stamps, exchange record)
     int32_t* xchg;            // ... its exchange record (abnn.h: summary + local spike list)
     uint32_t prologue_adapt;  // the previous pass was fused over the same ranges: its costs move the next

@@ -130,15 +130,13 @@ __device__ __forceinline__ void set_src(const SynArrays& a, uint64_t i, uint32_t
     if (a.src32) a.src32[i] = v;
 }
 
-// A weight store (brain.metal:122).  Non-temporal by default: a plain 4-B
-// store leaves scattered dirty partial lines whose write-back lands in the
-// middle of the next pass's record stream.  wt_sc1: write-through (sc1) --
-// the line leaves the XCD's L2 at once instead of at the kernel's end.
+// A weight store (brain.metal:122), non-temporal: a plain 4-B store leaves
+// scattered dirty partial lines whose write-back lands in the middle of the
+// next pass's record stream (write-through sc1 stores measured equal,
+// profiles/r03c_ab_wt_sc1.txt).
 __device__ __forceinline__ void store_w(const DeviceState& d, uint64_t i, float w)
 {
-    float* p = w_ptr(d.syn, i);
-    if (d.wt_sc1) __hip_atomic_store((gu32*)p, __float_as_uint(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __builtin_nontemporal_store(w, p);
+    __builtin_nontemporal_store(w, w_ptr(d.syn, i));
 }
 
 // Record visited by local event t: itself (sweep, brain.metal:70) or its pick.
@@ -1345,7 +1343,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // and a margin -- the ones from it on take the next bitmap's
     // pass-independent items (fused_end); 0: every workgroup does
     uint32_t hw0 = 0;
-    if (kFused && d.next_helpers && !d.shard_mode && spec_wgs + 3u + gridDim.x / 4u <= gridDim.x) hw0 = spec_wgs + 3u;
+    if (kFused && !d.shard_mode && spec_wgs + 3u + gridDim.x / 4u <= gridDim.x) hw0 = spec_wgs + 3u;
     uint32_t* st_off = s_stage[wid];
     uint32_t* st_src = s_stage[wid] + SE;
     // Records in flight.  Sweep: the packed src stream (engine.h, SynArrays):
@@ -1498,13 +1496,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // order the last of a SIMD's four waves streams ~15 % slower than the
         // first.  Rotating every wave through the four ranks every four
         // iterations equalises them (tools/ubench_soa.hip, profiles/r01p_*).
-        // prio_clock: the rank follows the wall clock (~10 us per step) instead
-        // of the wave's own iteration count, so the four waves of a SIMD never
-        // share a rank (iteration counts drift apart, and on a tie the arbiter
-        // favours the oldest wave)
-        if (((it - it_begin) & 3u) == 0)
-            set_priority((d.prio_clock ? (uint32_t)(__builtin_amdgcn_s_memrealtime() >> 10)
-                                       : (uint32_t)((it - it_begin) >> 2)) + wid / 4u);
+        if (((it - it_begin) & 3u) == 0) set_priority((uint32_t)((it - it_begin) >> 2) + wid / 4u);
 #pragma unroll
         for (int k = 0; k < KD; ++k) dst[k] = kTrack ? x.dd[k] : 0u;
         issue(x, it + kDepth, it + kDepth < it_end);  // the buffer's next iteration in flight first
@@ -1618,9 +1610,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         d.wave_clock[kWaveClock * r + 6] = chunk_t;
         d.wave_clock[kWaveClock * r + 7] = nch;
     }
-    // the tail (latency-bound) runs at the issue priority tail_prio, not at
-    // whatever rank the rotation left the wave in (4: keep)
-    if (d.tail_prio < 4) set_priority(d.tail_prio);
+    // the tail (latency-bound) runs at the lowest issue priority: the streams
+    // still running go first (profiles/r03g_ab_gain1_tailprio0.txt)
+    __builtin_amdgcn_s_setprio(0);
     // the range's last chunk: refractory stage by this wave
     const uint64_t tb = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
     // fused, single GPU, no synaptogenesis (its src list is global): the
@@ -1629,17 +1621,17 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     uint4* tail_lds = nullptr;
     if constexpr (kFused) {
         static_assert(2 * SE * 4 >= 256 * sizeof(uint4), "the stage holds 256 tail survivors");
-        if (d.lds_tail && !d.shard_mode && !d.g2src && pend <= 256u) tail_lds = reinterpret_cast<uint4*>(s_stage[wid]);
+        // (the lean instance runs neither: shard mode and synaptogenesis are off)
+        if ((kLean || (!d.shard_mode && !d.g2src)) && pend <= 256u) tail_lds = reinterpret_cast<uint4*>(s_stage[wid]);
     }
     const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, true>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
                                                                r, tot.z, s_f2, stage_at, tail_lds);
     const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
     const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
     if constexpr (kFused) {
-        // fused: the look-back waits for stream + tail, so with cost_tail the
-        // partition balances that (the tail's length follows the range's
-        // staged events)
-        const uint64_t gf = d.cost_tail ? ((__builtin_amdgcn_s_memrealtime() - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty : gt;
+        // fused: the look-back waits for stream + tail, so the partition
+        // balances that (the tail's length follows the range's staged events)
+        const uint64_t gf = ((__builtin_amdgcn_s_memrealtime() - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
         const bool tl = tail_lds != nullptr;
         fused_end<BLOCK, NW, kLean>(d, kp, r, region, tot.x + c.x, tl ? tot.y : tot.y + c.y, tl ? tot.z : tot.z + c.z,
                              tl ? c.y : 0u, tl ? c.z : 0u, tail_lds, (uint32_t)gf, len == 0, spec, now, Rw, rbw, pass_f,

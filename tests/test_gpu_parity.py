@@ -108,10 +108,8 @@ def test_edge_cases(gpu, over):
 
 
 @pytest.mark.parametrize("env", [{"ABNN_FUSED": "0"}, {"ABNN_SPEC": "2"}, {"ABNN_SPEC": "0"},
-                                 {"ABNN_LDS_TAIL": "0"}, {"ABNN_LEAN": "0"}, {"ABNN_NEXT_HELPERS": "0"},
-                                 {"ABNN_GATE": "1024x16f32"}],
-                         ids=["two-kernel", "spec-everywhere", "spec-off", "tail-in-g2x", "full-instance",
-                              "next-items-everywhere", "gate-1024x16"])
+                                 {"ABNN_LEAN": "0"}, {"ABNN_GATE": "1024x16f32"}],
+                         ids=["two-kernel", "spec-everywhere", "spec-off", "full-instance", "gate-1024x16"])
 @pytest.mark.parametrize("over", [{}, dict(max_spikes=1), dict(max_spikes=200_000), dict(events=777_777),
                                   dict(max_spikes=5_000, base_scale=4.0)],
                          ids=["default", "budget1", "budget-huge", "partial", "dense-candidates"])
@@ -120,9 +118,7 @@ def test_pass_variants(gpu, monkeypatch, env, over):
     two-kernel pass (k_gate + k_apply, also the sharded and random-mode path),
     and the fused pass with its speculative weight stores everywhere (every
     workgroup past the budget's end restores its weights) or nowhere, with
-    the ranges' last survivors in g2x instead of LDS, with the full (not the
-    lean) kernel instance, with the next bitmap's pass-independent items on
-    every workgroup instead of those past the predicted cut, and with the
+    the full (not the lean) kernel instance, and with the
     1024x16 gate shape (the default is 1024x8).
     dense-candidates: the input->output records' ranges hold more spike
     candidates than a range lists (kCandCap), so the fused walk's list path,
