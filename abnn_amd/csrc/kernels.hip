@@ -1105,31 +1105,13 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     // unless the budget is larger than it
     const bool spk_lds = !shard && budget <= kFusedMaxRanges;
     // every workgroup's word published = every refractory stage of the pass
-    // done: no lastFired read is left, the stamps may land.  Wave 0 waits for
-    // that before its walk (its loads then wait for no store of the walk).
+    // done: no lastFired read is left, the stamps may land.  A stamping
+    // workgroup walks first (every wave), and wave 0 then polls for every
+    // word and stamps the workgroup's spikes from LDS: after the pass's last
+    // word only the poll and one store instruction are left on the critical
+    // path (round 3 polled before wave 0's walk, which then followed the
+    // last word).
     uint32_t tot = 0, t0 = 0;
-    if (wid == 0 && stamping) {
-        tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
-        if (first) {
-            // the next pass's prediction (refrac_chunk's spec): the workgroups
-            // below the one where the budget ran out, less one
-            uint32_t run = 0, cut = gridDim.x;
-#pragma unroll
-            for (uint32_t i = 0; i < kLbMaxWords; ++i) {
-                const uint32_t inc = wave_incl_scan(vals[i]) + run;  // prefix through word 64 i + lane
-                const uint64_t hit = __ballot(inc >= budget && inc - vals[i] < budget);
-                if (hit && cut == gridDim.x) cut = i * 64 + (uint32_t)__builtin_ctzll(hit);
-                run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-            }
-            // the event-0 flag (refrac_chunk): stored and drained before its
-            // workgroup's word was published
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            t0 = __hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("" ::"v"(t0));  // consumed here, before any store of the walk (see range_walk)
-            if (lane == 0) d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
-        }
-    }
-    const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
     // the budget walk of k_apply over this range alone, in event order
     ApplyCtx ac{R, rb, now, pass, false, false, true, false, !kLean && kp.w_prune > 0.0f,
                 !kLean && d.grown != nullptr && kp.p_new > 0.0f, true, 0u, 0u, 0u};
@@ -1174,7 +1156,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         wc[9] = C;
         wc[10] = excl_wg;
         wc[11] = wu;
-        if (wid == 0) wc[12] = stamping ? t_seen : 0;
+        if (wid == 0) wc[12] = 0;  // t_seen below (stamping workgroups)
         wc[14] = t_rw;  // range_walk done (then the LDS tail's walk, the helpers' items: t_walk)
     }
     // LDS only (the statistics, the LDS spike list): the walks' stores stay in flight
@@ -1211,21 +1193,45 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         return;
     }
     uint64_t* wc0 = wcb + (uint64_t)kWaveClock * r;  // diagnostics, wave 0: exit
-    if (stamping) {
-        if (spk_lds) {
-            for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
-                const uint32_t nrn = L.cc[i - s0];
-                if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
-            }
-        } else {
-            const uint32_t* ring = d.fired_ring + (pass & (kFiredRing - 1)) * (uint64_t)budget;
-            for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
-                const uint32_t nrn = ring[i];
-                if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
-            }
+    if (!stamping || wid != 0) {
+        if (threadIdx.x == 0) wc0[13] = __builtin_amdgcn_s_memrealtime();
+        return;
+    }
+    // wave 0 of a stamping workgroup: every word, then the stamps (its first
+    // sweep waits for the walk's stores: off the critical path, the last
+    // word comes later)
+    tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
+    if (first) {
+        // the next pass's prediction (refrac_chunk's spec): the workgroups
+        // below the one where the budget ran out, less one
+        uint32_t run = 0, cut = gridDim.x;
+#pragma unroll
+        for (uint32_t i = 0; i < kLbMaxWords; ++i) {
+            const uint32_t inc = wave_incl_scan(vals[i]) + run;  // prefix through word 64 i + lane
+            const uint64_t hit = __ballot(inc >= budget && inc - vals[i] < budget);
+            if (hit && cut == gridDim.x) cut = i * 64 + (uint32_t)__builtin_ctzll(hit);
+            run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        }
+        // the event-0 flag (refrac_chunk): stored and drained before its
+        // workgroup's word was published
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        t0 = __hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
+    }
+    const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
+    if (spk_lds) {
+        for (uint32_t i = s0 + lane; i < s1; i += 64) {
+            const uint32_t nrn = L.cc[i - s0];
+            if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
+        }
+    } else {
+        const uint32_t* ring = d.fired_ring + (pass & (kFiredRing - 1)) * (uint64_t)budget;
+        for (uint32_t i = s0 + lane; i < s1; i += 64) {
+            const uint32_t nrn = ring[i];
+            if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
         }
     }
-    if (first && threadIdx.x == 0) {  // the pass's end: every workgroup has read the pass-start scalars
+    if (first && lane == 0) {  // the pass's end: every workgroup has read the pass-start scalars
         d.n_fired_ring[pass & (kFiredRing - 1)] = tot;
         if (t0 != 0u && budget > 0) *d.rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
         *d.clock = now + kp.clock_inc;                                        // brain.metal:129
@@ -1233,7 +1239,10 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         __hip_atomic_store((gu32*)&d.work->t0_g2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         d.work->epoch = epoch + 1u;
     }
-    if (threadIdx.x == 0) wc0[13] = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+        wc0[12] = t_seen;
+        wc0[13] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // ---------------------------------------------------------------------------

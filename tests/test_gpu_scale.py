@@ -52,6 +52,47 @@ def test_c3_full_size_parity(gpu, monkeypatch, env):
                               o.syn[first:first + n].view(np.uint32)), f"records [{first}, {first + n})"
 
 
+def test_c3_random_mode_full_size(gpu):
+    """Random-edge mode (README §4; abnn.h) at config 3: the 1B-record graph,
+    150M Philox picks per pass over all of it (the src32 mirror, the claim
+    words, k_claim's highest-event-wins stores and the two-kernel path at
+    full size), 12 passes from the fresh graph through the transient (passes
+    3-5 gate every pick) into the steady state, with the reward changed
+    mid-run.  GPU vs the threaded oracle holding the whole graph: every
+    neuron's lastFired, the statistics, the scalars and the checksum of all
+    1e9 records, plus bit-exact records over a sample of 10M-record windows."""
+    from abnn_amd import CONFIGS, Brain
+    from oracle import oracle as O
+
+    wl = CONFIGS["c3"]
+    g = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, mode=1, seed=9)
+    o = O.OracleBrain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, mode=1, seed=9)
+    assert g.visited_events() == wl.events
+    g.build_random_graph(1)
+    o.build_random_graph(1, nthreads=16)
+    for x in (g, o):
+        x.set_auto_stimulus(0, wl.n_input)
+    for k in range(12):
+        if k == 7:
+            g.set_reward(0.5)
+            o.set_reward(0.5)
+        g.encode_traversal(1)
+        o.pass_threaded(1, nthreads=16)
+    g.synchronize()
+    sg, so = g.scalars(), o.scalars()
+    assert sg["clock"] == so["clock"] == 12 and sg["pass_index"] == so["pass_index"]
+    assert np.float32(sg["rbar"]) == np.float32(so["rbar"])
+    st = g.stats()
+    assert st == o.stats()
+    assert st["fired"] > 2560 * 4 and st["updated"] > st["fired"]
+    assert np.array_equal(g.last_fired(), o.last_fired)
+    assert g.checksum() == o.checksum()
+    step = 10_000_000
+    for first in range(0, wl.n_syn, 97_000_000):
+        assert np.array_equal(g.download_synapses(first, step).view(np.uint32),
+                              o.syn[first:first + step].view(np.uint32)), f"records [{first}, {first + step})"
+
+
 def test_c4_eight_virtual_shards_of_the_1b_graph(gpu):
     """Config 4's workload on one GPU: the 1B-synapse c3 graph in 8 contiguous
     shards of 125M records, 150M events per shard per pass (so every shard
