@@ -257,10 +257,15 @@ __device__ __forceinline__ uint32_t filter_t(uint32_t j, uint32_t lg) { return _
         : "+v"(acc)                                                                               \
         : "v"(amt), "v"(val))
 
-template <int DB>
-__device__ __forceinline__ void filter_test(const uint2* s_fb, uint32_t v, uint32_t& HA, uint32_t& HB)
+// The filter block of code v (one 8-B LDS read).
+__device__ __forceinline__ uint2 filter_block(const uint2* s_fb, uint32_t v)
 {
-    const uint2 f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s_fb) + (v & 0xFFF8u));
+    return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s_fb) + (v & 0xFFF8u));
+}
+
+template <int DB>
+__device__ __forceinline__ void filter_test(const uint2 f, uint32_t v, uint32_t& HA, uint32_t& HB)
+{
     uint32_t hb;  // v's bits 0..2 over (v >> 19)'s: bits 3..4 = v[23:22]
     asm("v_bfi_b32 %0, 7, %1, %2" : "=v"(hb) : "v"(v), "v"(v >> 19));
     if constexpr (DB == 0) {
@@ -1105,13 +1110,31 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     // unless the budget is larger than it
     const bool spk_lds = !shard && budget <= kFusedMaxRanges;
     // every workgroup's word published = every refractory stage of the pass
-    // done: no lastFired read is left, the stamps may land.  A stamping
-    // workgroup walks first (every wave), and wave 0 then polls for every
-    // word and stamps the workgroup's spikes from LDS: after the pass's last
-    // word only the poll and one store instruction are left on the critical
-    // path (round 3 polled before wave 0's walk, which then followed the
-    // last word).
+    // done: no lastFired read is left, the stamps may land.  Wave 0 waits for
+    // that before its walk (its loads then wait for no store of the walk).
     uint32_t tot = 0, t0 = 0;
+    if (wid == 0 && stamping) {
+        tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
+        if (first) {
+            // the next pass's prediction (refrac_chunk's spec): the workgroups
+            // below the one where the budget ran out, less one
+            uint32_t run = 0, cut = gridDim.x;
+#pragma unroll
+            for (uint32_t i = 0; i < kLbMaxWords; ++i) {
+                const uint32_t inc = wave_incl_scan(vals[i]) + run;  // prefix through word 64 i + lane
+                const uint64_t hit = __ballot(inc >= budget && inc - vals[i] < budget);
+                if (hit && cut == gridDim.x) cut = i * 64 + (uint32_t)__builtin_ctzll(hit);
+                run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            }
+            // the event-0 flag (refrac_chunk): stored and drained before its
+            // workgroup's word was published
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            t0 = __hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("" ::"v"(t0));  // consumed here, before any store of the walk (see range_walk)
+            if (lane == 0) d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
+        }
+    }
+    const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
     // the budget walk of k_apply over this range alone, in event order
     ApplyCtx ac{R, rb, now, pass, false, false, true, false, !kLean && kp.w_prune > 0.0f,
                 !kLean && d.grown != nullptr && kp.p_new > 0.0f, true, 0u, 0u, 0u};
@@ -1156,7 +1179,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         wc[9] = C;
         wc[10] = excl_wg;
         wc[11] = wu;
-        if (wid == 0) wc[12] = 0;  // t_seen below (stamping workgroups)
+        if (wid == 0) wc[12] = stamping ? t_seen : 0;
         wc[14] = t_rw;  // range_walk done (then the LDS tail's walk, the helpers' items: t_walk)
     }
     // LDS only (the statistics, the LDS spike list): the walks' stores stay in flight
@@ -1193,45 +1216,21 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         return;
     }
     uint64_t* wc0 = wcb + (uint64_t)kWaveClock * r;  // diagnostics, wave 0: exit
-    if (!stamping || wid != 0) {
-        if (threadIdx.x == 0) wc0[13] = __builtin_amdgcn_s_memrealtime();
-        return;
-    }
-    // wave 0 of a stamping workgroup: every word, then the stamps (its first
-    // sweep waits for the walk's stores: off the critical path, the last
-    // word comes later)
-    tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
-    if (first) {
-        // the next pass's prediction (refrac_chunk's spec): the workgroups
-        // below the one where the budget ran out, less one
-        uint32_t run = 0, cut = gridDim.x;
-#pragma unroll
-        for (uint32_t i = 0; i < kLbMaxWords; ++i) {
-            const uint32_t inc = wave_incl_scan(vals[i]) + run;  // prefix through word 64 i + lane
-            const uint64_t hit = __ballot(inc >= budget && inc - vals[i] < budget);
-            if (hit && cut == gridDim.x) cut = i * 64 + (uint32_t)__builtin_ctzll(hit);
-            run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        }
-        // the event-0 flag (refrac_chunk): stored and drained before its
-        // workgroup's word was published
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        t0 = __hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0) d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
-    }
-    const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
-    if (spk_lds) {
-        for (uint32_t i = s0 + lane; i < s1; i += 64) {
-            const uint32_t nrn = L.cc[i - s0];
-            if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
-        }
-    } else {
-        const uint32_t* ring = d.fired_ring + (pass & (kFiredRing - 1)) * (uint64_t)budget;
-        for (uint32_t i = s0 + lane; i < s1; i += 64) {
-            const uint32_t nrn = ring[i];
-            if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
+    if (stamping) {
+        if (spk_lds) {
+            for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
+                const uint32_t nrn = L.cc[i - s0];
+                if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
+            }
+        } else {
+            const uint32_t* ring = d.fired_ring + (pass & (kFiredRing - 1)) * (uint64_t)budget;
+            for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
+                const uint32_t nrn = ring[i];
+                if (nrn < d.n_nrn) d.last_fired[nrn] = now;  // brain.metal:125-126
+            }
         }
     }
-    if (first && lane == 0) {  // the pass's end: every workgroup has read the pass-start scalars
+    if (first && threadIdx.x == 0) {  // the pass's end: every workgroup has read the pass-start scalars
         d.n_fired_ring[pass & (kFiredRing - 1)] = tot;
         if (t0 != 0u && budget > 0) *d.rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
         *d.clock = now + kp.clock_inc;                                        // brain.metal:129
@@ -1239,10 +1238,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         __hip_atomic_store((gu32*)&d.work->t0_g2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         d.work->epoch = epoch + 1u;
     }
-    if (lane == 0) {
-        wc0[12] = t_seen;
-        wc0[13] = __builtin_amdgcn_s_memrealtime();
-    }
+    if (threadIdx.x == 0) wc0[13] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------------------
@@ -1540,13 +1536,23 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 fm |= (__builtin_amdgcn_ubfe(fb[k].x, src[k], 1) & __builtin_amdgcn_ubfe(fb[k].y, src[k] + ft[k], 1)) << k;
             fm &= vmask;
         } else {
+            // every block read issued before the first test: the reads are
+            // independent, and each one waited for (the round-3 code let the
+            // compiler reuse one register pair, so the eight 8-B LDS reads of
+            // an iteration ran one after another, each behind its bank
+            // conflicts: SQ_LDS_BANK_CONFLICT is half of SQ_LDS_IDX_ACTIVE).  Measured
+            // equal in time (profiles/r04c_*): the waves' waits became issue
+            // stalls -- the stream loop is issue-bound on its SIMD
+            uint2 fb[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) fb[k] = filter_block(s_fb, src[k]);
 #pragma unroll
             for (int g = 0; g < K / 4; ++g) {
                 uint32_t HA, HB;
-                filter_test<0>(s_fb, src[4 * g], HA, HB);
-                filter_test<1>(s_fb, src[4 * g + 1], HA, HB);
-                filter_test<2>(s_fb, src[4 * g + 2], HA, HB);
-                filter_test<3>(s_fb, src[4 * g + 3], HA, HB);
+                filter_test<0>(fb[4 * g], src[4 * g], HA, HB);
+                filter_test<1>(fb[4 * g + 1], src[4 * g + 1], HA, HB);
+                filter_test<2>(fb[4 * g + 2], src[4 * g + 2], HA, HB);
+                filter_test<3>(fb[4 * g + 3], src[4 * g + 3], HA, HB);
                 H[g] = HA & HB & 0x01010101u;
             }
             if (base + IE > d.events) {  // only the sweep's last iteration (wave-uniform)

@@ -27,18 +27,19 @@
 //                  candidate (brain.metal:91-92), u32 age (brain.metal:116);
 //                  survivors appended to the wave's survivor sequence, held
 //                  in 4-KiB chunks of a BOUNDED pool (one atomic per chunk).
-//   k_raw_scan   : one workgroup: the groups' capped candidate prefix (the
-//                  ordered budget of C1, brain.metal:85-98 without its races),
-//                  the budget cut, then the pass end on the scalars: *budget
-//                  left, rBar (brain.metal:110-113), one clock tick
-//                  (brain.metal:129).
+//   k_raw_scan_local + k_raw_scan : the groups' capped candidate prefix
+//                  (the ordered budget of C1, brain.metal:85-98 without its
+//                  races) in 4096-group blocks, then one workgroup: the
+//                  blocks' prefix, the budget cut, the pass end on the
+//                  scalars: *budget left, rBar (brain.metal:110-113), one
+//                  clock tick (brain.metal:129).
 //   k_raw_apply  : the groups below the cut: the weight update of their
 //                  survivors below the budget (brain.metal:101-122) and the
-//                  spike list in budget order.  A group whose survivors did
-//                  not fit the pool is recomputed from its records (the pass-
-//                  start lastF: the stamps are deferred).
-//   k_raw_stamp  : the spike list's stamps (brain.metal:125-126), after every
-//                  lastF read of the pass (C1).
+//                  spikes' stamps (brain.metal:125-126): it reads no lastF.
+//                  A group whose survivors did not fit the pool is recomputed
+//                  from its records with the pass-start lastF; in such a pass
+//                  the spikes go to a list in budget order instead and
+//   k_raw_stamp  : stamps them after every lastF read of the pass (C1).
 //
 // renormalise_clock_and_times (brain.metal:135-145): k_raw_renorm subtracts
 // the clock read by every thread, k_raw_zero_clock zeroes it afterwards (the
@@ -69,11 +70,13 @@ constexpr uint32_t kRawFB = 8192;                    // filter blocks (64 KiB of
 constexpr uint32_t kRawFLg = 13;
 constexpr uint32_t kRawSpikeCap = 65536;             // spike list entries (deferred stamps)
 constexpr uint32_t kRawScanThreads = 1024;
+constexpr uint32_t kRawScanBlock = 4 * kRawScanThreads;  // groups per k_raw_scan_local workgroup
+static_assert(kRawWaves % kRawScanThreads == 0, "k_raw_scan sums the gate waves' statistics in whole rounds");
 constexpr uint32_t kRawApplyWGs = 1024;              // x 4 waves, grid-stride over the groups below the cut
 constexpr uint32_t kRawNone = 0xFFFFFFFFu;
 
 // Workspace (16-B aligned pieces):
-//   hdr | filter (FB uint2) | gcand[NG] | gpre[NG] | ginfo[NG] {S, seq} |
+//   hdr | filter (FB uint2) | gcand[NG] | gpre[NG] | btot[NG / 4096] | ginfo[NG] {S, seq} |
 //   wlim[W] | wstat[W] | ctab[W][maxc] | spikes[L] | pool[cap][kRawChunk] uint4
 struct RawHdr {
     uint32_t now, budget0, t0, ncand;  // pass-start clock and budget; event 0 survived; spikes (capped)
@@ -82,7 +85,8 @@ struct RawHdr {
     uint32_t gcut;                     // groups below the budget's cut: [0, gcut)
     uint32_t direct;                   // budget0 > the spike list: apply stamps itself
     uint32_t err;                      // a recomputed group met direct stamps (abnn_traversal_workspace_error)
-    uint32_t pad[2];
+    uint32_t ovf;                      // some wave's survivors overflowed the pool this pass (groups recomputed)
+    uint32_t pad;
     uint64_t g1, g2;                   // the pass's pre-gated and refractory-surviving events (diagnostics)
 };
 static_assert(sizeof(RawHdr) == 64, "workspace header");
@@ -91,7 +95,8 @@ struct RawWs {
     RawHdr* hdr;
     uint2* filter;
     uint32_t* gcand;   // spike candidates per group
-    uint32_t* gpre;    // capped exclusive candidate prefix per group
+    uint32_t* gpre;    // exclusive candidate prefix per group within its scan block of 4096 groups
+    uint32_t* btot;    // per scan block: its candidates; then (k_raw_scan) the blocks before it, capped
     uint2* ginfo;      // {survivors, first index in the owning wave's survivor sequence}
     uint32_t* wlim;    // per wave: survivor-sequence entries stored (the rest overflowed the pool)
     uint2* wstat;      // per wave: {pre-gated, survivors} of its groups (k_raw_scan sums them)
@@ -113,7 +118,8 @@ inline uint64_t raw_fixed_bytes(uint64_t E)
 {
     const uint64_t ng = raw_groups(E);
     const uint64_t L = std::min<uint64_t>(E, kRawSpikeCap);
-    return 64 + kRawFB * 8 + al16(4 * ng) * 2 + al16(8 * ng) + al16(4ull * kRawWaves) + al16(8ull * kRawWaves) +
+    return 64 + kRawFB * 8 + al16(4 * ng) * 2 + al16(4 * ((ng + kRawScanBlock - 1) / kRawScanBlock)) + al16(8 * ng) +
+           al16(4ull * kRawWaves) + al16(8ull * kRawWaves) +
            al16(4ull * kRawWaves * raw_maxc(ng)) + al16(4 * L);
 }
 
@@ -145,6 +151,8 @@ inline RawWs raw_ws(void* base, uint64_t E, uint64_t bytes)
     p += al16(4 * ng);
     w.gpre = reinterpret_cast<uint32_t*>(p);
     p += al16(4 * ng);
+    w.btot = reinterpret_cast<uint32_t*>(p);
+    p += al16(4 * ((ng + kRawScanBlock - 1) / kRawScanBlock));
     w.ginfo = reinterpret_cast<uint2*>(p);
     p += al16(8 * ng);
     w.wlim = reinterpret_cast<uint32_t*>(p);
@@ -183,17 +191,20 @@ __device__ __forceinline__ bool raw_filter_pass(const uint2* s_fb, uint32_t src)
 }
 
 // ---------------------------------------------------------------------------
-// k_raw_filter: workgroup b builds filter blocks [8 b, 8 b + 8).  The words
+// k_raw_filter: workgroup b builds filter blocks [4 b, 4 b + 4).  The words
 // of block g are j = h << 13 | ((g ^ t(h)) & 8191), h = 0 .. H-1 (t depends on
 // h only); half a wave reads one word's 32 lastF values (128 B), so a wave
-// instruction covers two words and the ballot returns both.  Every lastF
-// value is read once by the whole grid.
+// instruction covers two words and the ballot returns both; a wave issues
+// all its reads at once (config 3: H = 20, 20 words per wave, one round
+// trip).  Every lastF value is read once by the whole grid.
+constexpr uint32_t kRawFilterBlocks = 4;  // filter blocks per workgroup
 __global__ __launch_bounds__(256) void k_raw_filter(const uint32_t* lastF, const uint32_t* clock, uint32_t n_nrn,
                                                     KernelParams kp, RawWs ws)
 {
-    __shared__ uint32_t s_lo[8], s_hi[8];
+    constexpr uint32_t NB = kRawFilterBlocks, kU = 12;  // word pairs in flight per wave
+    __shared__ uint32_t s_lo[NB], s_hi[NB];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (threadIdx.x < 8) {
+    if (threadIdx.x < NB) {
         s_lo[threadIdx.x] = 0u;
         s_hi[threadIdx.x] = 0u;
     }
@@ -201,34 +212,36 @@ __global__ __launch_bounds__(256) void k_raw_filter(const uint32_t* lastF, const
         ws.hdr->chunks = 0u;
         ws.hdr->t0 = 0u;
         ws.hdr->err = 0u;
+        ws.hdr->ovf = 0u;
     }
     __syncthreads();
     const uint32_t now = *clock;
     const uint32_t words = (n_nrn + 31u) / 32u, H = (words + kRawFB - 1) >> kRawFLg;
-    const uint32_t tasks = 8u * H;  // (block, h) pairs of this workgroup
-    constexpr uint32_t kU = 4;
+    const uint32_t tasks = NB * H;  // (block, h) pairs of this workgroup
     for (uint32_t x0 = wv * 2u * kU; x0 < tasks; x0 += 4u * 2u * kU) {  // wave-uniform
         uint32_t v[kU];
         uint32_t jw[kU];
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
             const uint32_t x = x0 + 2u * u + (lane >> 5);  // this half-wave's task
-            const uint32_t gl = x & 7u, h = x >> 3, g = blockIdx.x * 8u + gl;
+            const uint32_t gl = x % NB, h = x / NB, g = blockIdx.x * NB + gl;
             const uint32_t t = __umul24(h, 0x9E5u);
             const uint32_t j = h << kRawFLg | ((g ^ t) & (kRawFB - 1));
-            jw[u] = x < tasks ? j : kRawNone;
             const uint64_t n = (uint64_t)j * 32u + (lane & 31u);
-            v[u] = (x < tasks && n < n_nrn) ? lastF[n] : 0u;
             const bool ok = x < tasks && n < n_nrn;
-            v[u] = ok ? ((now - v[u]) <= kp.window_pre ? 1u : 0u) : 0u;  // brain.metal:73-77 (u32 age)
+            jw[u] = x < tasks ? j : kRawNone;
+            v[u] = ok ? lastF[n] : now;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
-            const uint64_t m = __ballot(v[u] != 0u);
+            const uint32_t x = x0 + 2u * u + (lane >> 5);
+            const uint64_t n = (uint64_t)(jw[u] == kRawNone ? 0u : jw[u]) * 32u + (lane & 31u);
+            const bool bit = jw[u] != kRawNone && n < n_nrn && (now - v[u]) <= kp.window_pre;  // brain.metal:73-77 (u32)
+            const uint64_t m = __ballot(bit);
             if ((lane & 31u) == 0 && jw[u] != kRawNone) {
                 const uint32_t bits = (uint32_t)(m >> (lane & 32u));
                 if (bits) {
-                    const uint32_t x = x0 + 2u * u + (lane >> 5), gl = x & 7u, r = raw_t(jw[u]) & 31u;
+                    const uint32_t gl = x % NB, r = raw_t(jw[u]) & 31u;
                     atomicOr(&s_lo[gl], bits);
                     atomicOr(&s_hi[gl], (bits << r) | (bits >> ((32u - r) & 31u)));
                 }
@@ -236,7 +249,7 @@ __global__ __launch_bounds__(256) void k_raw_filter(const uint32_t* lastF, const
         }
     }
     __syncthreads();
-    if (threadIdx.x < 8) ws.filter[blockIdx.x * 8u + threadIdx.x] = make_uint2(s_lo[threadIdx.x], s_hi[threadIdx.x]);
+    if (threadIdx.x < NB) ws.filter[blockIdx.x * NB + threadIdx.x] = make_uint2(s_lo[threadIdx.x], s_hi[threadIdx.x]);
 }
 
 // ---------------------------------------------------------------------------
@@ -332,6 +345,7 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_gate(const uint4* __restrict_
                     id = wave_uniform(id);
                     if (id >= ws.pool_chunks) {  // the pool is spent: the rest of the sequence is not stored
                         lim = have * kRawChunk;
+                        if (lane == 0) ws.hdr->ovf = 1u;  // k_raw_apply will recompute: stamps deferred
                         break;
                     }
                     if (lane == 0) ws.ctab[(uint64_t)v * ws.maxc + have] = id;
@@ -387,17 +401,24 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_gate(const uint4* __restrict_
     }
 }
 
-__global__ __launch_bounds__(kRawScanThreads) void k_raw_scan(RawWs ws, uint32_t E, uint32_t* clock, uint32_t* budget,
-                                                              const float* reward, float* rbar, KernelParams kp)
+// The ordered budget in two launches.  k_raw_scan_local: workgroup b scans
+// groups [4096 b, 4096 b + 4096) -- one coalesced 16-B load per thread --
+// into gpre (exclusive, within the block) and the block's total (btot[b]).
+__global__ __launch_bounds__(kRawScanThreads) void k_raw_scan_local(RawWs ws)
 {
-    __shared__ uint32_t s_wave[kRawScanThreads / 64], s_cut[kRawScanThreads / 64];
+    __shared__ uint32_t s_wave[kRawScanThreads / 64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t b0 = *budget, NG = ws.ng;
-    const uint32_t per = (NG + kRawScanThreads - 1) / kRawScanThreads, q0 = threadIdx.x * per;
-    uint64_t sum = 0;
-    for (uint32_t q = q0; q < q0 + per && q < NG; ++q) sum += ws.gcand[q];
-    const uint32_t v = (uint32_t)(sum < 0xFFFFFFFFull ? sum : 0xFFFFFFFFull);
-    const uint32_t inc = wave_incl_scan(v);  // groups x 1024 < 2^32 events: no overflow
+    const uint32_t g0 = blockIdx.x * kRawScanBlock + 4 * threadIdx.x, NG = ws.ng;
+    uint4 c = make_uint4(0u, 0u, 0u, 0u);
+    if (g0 + 3 < NG) {
+        c = *reinterpret_cast<const uint4*>(ws.gcand + g0);  // 16-B aligned: g0 % 4 == 0, gcand 16-B aligned
+    } else {
+        if (g0 < NG) c.x = ws.gcand[g0];
+        if (g0 + 1 < NG) c.y = ws.gcand[g0 + 1];
+        if (g0 + 2 < NG) c.z = ws.gcand[g0 + 2];
+    }
+    const uint32_t v = c.x + c.y + c.z + c.w;  // a group holds <= 1024 candidates: no overflow in a block
+    const uint32_t inc = wave_incl_scan(v);
     if (lane == 63) s_wave[wv] = inc;
     __syncthreads();
     uint32_t before = 0, total = 0;
@@ -405,30 +426,91 @@ __global__ __launch_bounds__(kRawScanThreads) void k_raw_scan(RawWs ws, uint32_t
         before += w < wv ? s_wave[w] : 0u;
         total += s_wave[w];
     }
-    uint32_t run = before + inc - v, below = 0;
-    for (uint32_t q = q0; q < q0 + per && q < NG; ++q) {
-        ws.gpre[q] = run < b0 ? run : b0;
-        below += run < b0 ? 1u : 0u;  // the prefix is monotone: the groups below the cut are [0, gcut)
-        run += ws.gcand[q];
+    const uint32_t e = before + inc - v;
+    if (g0 + 3 < NG) {
+        *reinterpret_cast<uint4*>(ws.gpre + g0) = make_uint4(e, e + c.x, e + c.x + c.y, e + c.x + c.y + c.z);
+    } else {
+        if (g0 < NG) ws.gpre[g0] = e;
+        if (g0 + 1 < NG) ws.gpre[g0 + 1] = e + c.x;
+        if (g0 + 2 < NG) ws.gpre[g0 + 2] = e + c.x + c.y;
     }
-    const uint32_t bw = wave_incl_scan(below);
-    if (lane == 63) s_cut[wv] = bw;
-    // the gate waves' statistics (a wave past the last group wrote zeros)
-    uint64_t a1 = 0, a2 = 0;
-    for (uint32_t w = threadIdx.x; w < kRawWaves; w += kRawScanThreads) {
-        const uint2 x = ws.wstat[w];
-        a1 += x.x;
-        a2 += x.y;
-    }
+    if (threadIdx.x == 0) ws.btot[blockIdx.x] = total;
+}
+
+// k_raw_scan: one workgroup.  The blocks' totals become capped exclusive
+// prefixes (btot), the cut (the groups below the budget, [0, gcut): the
+// prefix is monotone) is found inside the block where the budget runs out,
+// then the pass end on the scalars, which nothing later in the pass reads:
+// *budget left, rBar (brain.metal:110-113), one clock tick (brain.metal:129).
+// A group's capped budget position is min(btot[g / 4096] + gpre[g], budget).
+__global__ __launch_bounds__(kRawScanThreads) void k_raw_scan(RawWs ws, uint32_t E, uint32_t* clock, uint32_t* budget,
+                                                              const float* reward, float* rbar, KernelParams kp)
+{
+    __shared__ uint32_t s_wave[kRawScanThreads / 64], s_cut[kRawScanThreads / 64];
+    __shared__ uint32_t s_blk[2];  // the block where the budget runs out, its offset
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t b0 = *budget, NG = ws.ng, NB = (NG + kRawScanBlock - 1) / kRawScanBlock;
     __shared__ unsigned long long s_g[2];
-    if (threadIdx.x == 0) s_g[0] = s_g[1] = 0ull;
+    if (threadIdx.x == 0) {
+        s_blk[0] = NB;
+        s_blk[1] = 0u;
+        s_g[0] = s_g[1] = 0ull;
+    }
+    // the gate waves' statistics (a wave past the last group wrote zeros),
+    // loaded beside the block totals (one round trip)
+    uint2 wst[kRawWaves / kRawScanThreads];
+#pragma unroll
+    for (uint32_t i = 0; i < kRawWaves / kRawScanThreads; ++i) wst[i] = ws.wstat[i * kRawScanThreads + threadIdx.x];
+    // blocks: NB <= 1024 at any u32 record count
+    const uint32_t bt = threadIdx.x < NB ? ws.btot[threadIdx.x] : 0u;
+    const uint64_t bt64 = bt;
+    uint32_t inc = wave_incl_scan(bt);  // per-block totals <= 4096 x 1024: u32 prefix is exact below 2^32 events
+    if (lane == 63) s_wave[wv] = inc;
     __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t w = 0; w < kRawScanThreads / 64; ++w) {
+        before += w < wv ? s_wave[w] : 0u;
+        total += s_wave[w];
+    }
+    const uint32_t ex = before + inc - (uint32_t)bt64;
+    if (threadIdx.x < NB) {
+        ws.btot[threadIdx.x] = ex < b0 ? ex : b0;
+        if (ex < b0 && ex + bt >= b0) {  // the budget runs out inside this block
+            s_blk[0] = threadIdx.x;
+            s_blk[1] = ex;
+        }
+    }
+    __syncthreads();
+    // gcut: the groups with a budget position below b0
+    uint32_t gcut;
+    const uint32_t cb = s_blk[0];
+    if (b0 == 0) {
+        gcut = 0;   // no budget: no update (C1)
+    } else if (cb >= NB) {
+        gcut = NG;  // the budget never runs out
+    } else {
+        uint32_t below = 0;
+        for (uint32_t q = threadIdx.x; q < kRawScanBlock; q += kRawScanThreads) {
+            const uint32_t g = cb * kRawScanBlock + q;
+            below += (g < NG && s_blk[1] + ws.gpre[g] < b0) ? 1u : 0u;
+        }
+        const uint32_t bw = wave_incl_scan(below);
+        if (lane == 63) s_cut[wv] = bw;
+        __syncthreads();
+        uint32_t nb = 0;
+        for (uint32_t w = 0; w < kRawScanThreads / 64; ++w) nb += s_cut[w];
+        gcut = cb * kRawScanBlock + nb;
+    }
+    uint64_t a1 = 0, a2 = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kRawWaves / kRawScanThreads; ++i) {
+        a1 += wst[i].x;
+        a2 += wst[i].y;
+    }
     if (a1) atomicAdd(&s_g[0], (unsigned long long)a1);
     if (a2) atomicAdd(&s_g[1], (unsigned long long)a2);
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t gcut = 0;
-        for (uint32_t w = 0; w < kRawScanThreads / 64; ++w) gcut += s_cut[w];
         const uint32_t now = *clock;
         const float R = *reward, rb = *rbar;
         const uint32_t t0 = E > 0 ? ws.hdr->t0 : 0u;
@@ -440,7 +522,10 @@ __global__ __launch_bounds__(kRawScanThreads) void k_raw_scan(RawWs ws, uint32_t
         h->R = R;
         h->rb = rb;
         h->gcut = gcut;
-        h->direct = b0 > ws.spike_cap ? 1u : 0u;
+        // no group recomputed (nothing overflowed the pool): k_raw_apply reads
+        // no lastF, so it stamps the spikes itself; else they wait for
+        // k_raw_stamp, unless the budget is beyond the spike list
+        h->direct = (b0 > ws.spike_cap || h->ovf == 0u) ? 1u : 0u;
         h->g1 = ws.ng ? s_g[0] : 0ull;
         h->g2 = ws.ng ? s_g[1] : 0ull;
         *budget = b0 - nc;                                               // brain.metal:95-98 (C1: no wrap)
@@ -458,7 +543,7 @@ __device__ __forceinline__ void raw_apply_one(uint4* syn, uint32_t* lastF, const
     const float w = updated_weight(kp, __uint_as_float(e.z), cand, h.R, h.rb, __uint_as_float(e.y & 0x7FFFFFFFu));
     reinterpret_cast<float*>(syn + e.x)[2] = w;  // brain.metal:122 (src, dst, pad unchanged)
     if (cand) {
-        if (h.direct) lastF[e.w] = h.now;  // brain.metal:125-126 (no group recomputed: raw_apply_group)
+        if (h.direct) lastF[e.w] = h.now;  // brain.metal:125-126 (k_raw_scan: no lastF read is left)
         else ws.spikes[pre] = e.w;
     }
 }
@@ -470,40 +555,70 @@ __global__ __launch_bounds__(256) void k_raw_apply(uint4* syn, uint32_t* lastF, 
     const RawHdr h = *ws.hdr;  // pass-start scalars (k_raw_scan)
     const uint32_t nw = gridDim.x * 4u;
     for (uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6); g < h.gcut; g += nw) {  // wave-uniform
-        uint32_t P = ws.gpre[g];
+        uint32_t P = ws.btot[g / kRawScanBlock] + ws.gpre[g];  // < budget0: g < gcut
         const uint2 gi = ws.ginfo[g];
         const uint32_t S = gi.x, s0 = gi.y, v = g % kRawWaves, lim = ws.wlim[v];
         if (S == 0) continue;
-        if (lim == kRawNone || s0 + S <= lim) {  // stored: walk the wave's sequence [s0, s0 + S)
+        // a group holds <= 1024 events: all its survivors (or records) are
+        // loaded at once, 16 per lane, then walked in event order -- one
+        // round trip, not one per 64 (the dense input->output groups)
+        constexpr uint32_t RW = kRawGroup / 64;
+        if (lim == kRawNone || s0 + S <= lim) {  // stored: the wave's sequence [s0, s0 + S)
             const uint32_t* ct = ws.ctab + (uint64_t)v * ws.maxc;
-            for (uint32_t b0 = 0; b0 < S && P < h.budget0; b0 += 64) {  // wave-uniform
-                const uint32_t q = b0 + lane, x = s0 + q;
-                const bool ok = q < S;
-                const uint4 e = ok ? ws.pool[(uint64_t)ct[x / kRawChunk] * kRawChunk + x % kRawChunk] : make_uint4(0u, 0u, 0u, 0u);
-                const bool cand = ok && (e.y >> 31);
+            const uint32_t c0 = s0 / kRawChunk, nc = (s0 + S - 1) / kRawChunk - c0 + 1;  // <= 5 chunks
+            const uint32_t cid = lane < nc ? ct[c0 + lane] : 0u;
+            uint4 e[RW];
+#pragma unroll
+            for (uint32_t j = 0; j < RW; ++j) {
+                const uint32_t q = j * 64 + lane, x = s0 + q;
+                const uint32_t id = (uint32_t)__shfl((int)cid, (int)(q < S ? x / kRawChunk - c0 : 0u), 64);
+                e[j] = q < S ? ws.pool[(uint64_t)id * kRawChunk + x % kRawChunk] : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < RW; ++j) {
+                if (j * 64 >= S || P >= h.budget0) break;  // wave-uniform
+                const bool ok = j * 64 + lane < S;
+                const bool cand = ok && (e[j].y >> 31);
                 const uint64_t bc = __ballot(cand);
                 const uint32_t pre = P + mbcnt64(bc);  // spike candidates before this event
-                if (ok && pre < h.budget0) raw_apply_one(syn, lastF, ws, h, kp, e, cand, pre);
+                if (ok && pre < h.budget0) raw_apply_one(syn, lastF, ws, h, kp, e[j], cand, pre);
                 P += (uint32_t)__popcll(bc);
             }
             continue;
         }
         // not stored (the pool ran out): the group again from its records,
         // with the pass-start lastF (the stamps wait for k_raw_stamp)
-        if (h.direct && lane == 0) ws.hdr->err = 1u;
-        for (uint32_t b0 = 0; b0 < kRawGroup && P < h.budget0; b0 += 64) {  // wave-uniform
-            const uint64_t t = (uint64_t)g * kRawGroup + b0 + lane;
-            const uint4 r = t < E ? syn[t] : make_uint4(kRawNone, kRawNone, 0u, 0u);
-            const bool ok = r.x < n_nrn && r.y < n_nrn;
-            const uint32_t a = ok ? lastF[r.x] : h.now, b = ok ? lastF[r.y] : h.now;
-            const bool g2 = ok && h.now - a <= kp.window_pre && h.now - b > kp.refractory;  // brain.metal:73-83
-            const bool cand = g2 && spike_candidate(kp, __uint_as_float(r.z), t, h.now);    // brain.metal:91-92
-            const uint64_t bc = __ballot(cand);
-            const uint32_t pre = P + mbcnt64(bc);
-            if (g2 && pre < h.budget0)
-                raw_apply_one(syn, lastF, ws, h, kp,
-                              make_uint4((uint32_t)t, __float_as_uint((float)(h.now - b)), r.z, r.y), cand, pre);
-            P += (uint32_t)__popcll(bc);
+        if (h.direct && lane == 0) ws.hdr->err = 1u;  // (direct here only with a budget beyond the list)
+        constexpr uint32_t RH = RW / 2;  // two halves: records and their lastF in flight, no spills
+        for (uint32_t h0 = 0; h0 < RW && P < h.budget0; h0 += RH) {  // wave-uniform
+            uint4 rc[RH];
+#pragma unroll
+            for (uint32_t j = 0; j < RH; ++j) {
+                const uint64_t t = (uint64_t)g * kRawGroup + (h0 + j) * 64 + lane;
+                rc[j] = t < E ? syn[t] : make_uint4(kRawNone, kRawNone, 0u, 0u);
+            }
+            uint32_t la[RH], lb[RH];
+#pragma unroll
+            for (uint32_t j = 0; j < RH; ++j) {
+                const bool ok = rc[j].x < n_nrn && rc[j].y < n_nrn;
+                la[j] = ok ? lastF[rc[j].x] : h.now;
+                lb[j] = ok ? lastF[rc[j].y] : h.now;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < RH; ++j) {
+                if (P >= h.budget0) break;  // wave-uniform
+                const uint64_t t = (uint64_t)g * kRawGroup + (h0 + j) * 64 + lane;
+                const bool ok = rc[j].x < n_nrn && rc[j].y < n_nrn;
+                const bool g2 = ok && h.now - la[j] <= kp.window_pre && h.now - lb[j] > kp.refractory;  // brain.metal:73-83
+                const bool cand = g2 && spike_candidate(kp, __uint_as_float(rc[j].z), t, h.now);        // brain.metal:91-92
+                const uint64_t bc = __ballot(cand);
+                const uint32_t pre = P + mbcnt64(bc);
+                if (g2 && pre < h.budget0)
+                    raw_apply_one(syn, lastF, ws, h, kp,
+                                  make_uint4((uint32_t)t, __float_as_uint((float)(h.now - lb[j])), rc[j].z, rc[j].y),
+                                  cand, pre);
+                P += (uint32_t)__popcll(bc);
+            }
         }
     }
 }
@@ -577,7 +692,8 @@ abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream)
     const RawWs ws = raw_ws(a->workspace, E, a->workspace_bytes);
     const KernelParams kp = raw_params(*a);
     uint4* syn = reinterpret_cast<uint4*>(a->syn);
-    hipLaunchKernelGGL(k_raw_filter, dim3(kRawFB / 8), dim3(256), 0, s, a->last_fired, a->clock, a->n_nrn, kp, ws);
+    hipLaunchKernelGGL(k_raw_filter, dim3(kRawFB / kRawFilterBlocks), dim3(256), 0, s, a->last_fired, a->clock,
+                       a->n_nrn, kp, ws);
     if (ws.ng) {
         RawTiming& tm = raw_timing();
         std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
@@ -590,6 +706,9 @@ abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream)
             tm.ev.push_back(ev);
         }
     }
+    if (ws.ng)
+        hipLaunchKernelGGL(k_raw_scan_local, dim3((ws.ng + kRawScanBlock - 1) / kRawScanBlock), dim3(kRawScanThreads), 0,
+                           s, ws);
     hipLaunchKernelGGL(k_raw_scan, dim3(1), dim3(kRawScanThreads), 0, s, ws, (uint32_t)E, a->clock, a->budget, a->reward,
                        a->rbar, kp);
     if (ws.ng) {
