@@ -1033,7 +1033,7 @@ struct FusedLds {
 // can: the look-back's first sweep is issued before the publishing store, the
 // tail's survivors and the workgroup's spikes stay in LDS, LDS-only barriers,
 // and wave 0 sees every word published before it walks (and stores).
-template <int BLOCK, int NW, bool kLean>
+template <int BLOCK, int NW, bool kLean, bool kShard>
 __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelParams& kp, uint32_t r, uint64_t region,
                                           uint32_t g1, uint32_t Sg, uint32_t Cg, uint32_t St, uint32_t Ct,
                                           const uint4* tl, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
@@ -1045,7 +1045,8 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     const uint32_t tag = epoch + 1u;
     // kLean: the single-GPU pass without plasticity (less code: the end of
     // the pass runs from a cold instruction cache)
-    const bool shard = !kLean && d.shard_mode;
+    // kShard (with kLean): the sharded pass's first launch without plasticity
+    const bool shard = kShard || (!kLean && d.shard_mode);
     const uint64_t t_tail = __builtin_amdgcn_s_memrealtime();
     const uint32_t S = Sg + St, C = Cg + Ct;  // the range's survivors and spike candidates
     uint32_t order = 0;
@@ -1272,7 +1273,7 @@ __device__ __forceinline__ void set_priority(uint32_t p)
 // weight update of k_apply: apply_event), and the last workgroup ends the pass
 // (fused_finalize).  Its survivors are written contiguously from the range's
 // region start (no per-chunk slots: the wave walks them itself).
-template <int BLOCK, int K, int FW, bool kTrack, bool kRandom, bool kFused, bool kLean = false>
+template <int BLOCK, int K, int FW, bool kTrack, bool kRandom, bool kFused, bool kLean = false, bool kShard = false>
 __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 {
     constexpr int NW = BLOCK / 64;
@@ -1637,7 +1638,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     if constexpr (kFused) {
         static_assert(2 * SE * 4 >= 256 * sizeof(uint4), "the stage holds 256 tail survivors");
         // (the lean instance runs neither: shard mode and synaptogenesis are off)
-        if ((kLean || (!d.shard_mode && !d.g2src)) && pend <= 256u) tail_lds = reinterpret_cast<uint4*>(s_stage[wid]);
+        // (the shard instance's walk is the next launch: its tail goes to g2x)
+        const bool lds_ok = kShard ? false : (kLean || (!d.shard_mode && !d.g2src));
+        if (lds_ok && pend <= 256u) tail_lds = reinterpret_cast<uint4*>(s_stage[wid]);
     }
     const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, true>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
                                                                r, tot.z, s_f2, stage_at, tail_lds);
@@ -1648,7 +1651,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // balances that (the tail's length follows the range's staged events)
         const uint64_t gf = ((__builtin_amdgcn_s_memrealtime() - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
         const bool tl = tail_lds != nullptr;
-        fused_end<BLOCK, NW, kLean>(d, kp, r, region, tot.x + c.x, tl ? tot.y : tot.y + c.y, tl ? tot.z : tot.z + c.z,
+        fused_end<BLOCK, NW, kLean, kShard>(d, kp, r, region, tot.x + c.x, tl ? tot.y : tot.y + c.y, tl ? tot.z : tot.z + c.z,
                              tl ? c.y : 0u, tl ? c.z : 0u, tail_lds, (uint32_t)gf, len == 0, spec, now, Rw, rbw, pass_f,
                              epoch, s_fz, t_stream, hw0, chunk_t, nch, wcb);
         return;
@@ -2434,10 +2437,13 @@ template <int BLOCK, int K, int FW>
 hipError_t launch_fused_shape(const DeviceState& d, const KernelParams& kp, hipStream_t s)
 {
     const dim3 g(d.gate_blocks), b(BLOCK);
-    // lean: the single-GPU pass without pruning or synaptogenesis
-    const bool lean = d.lean && !d.shard_mode && !(kp.w_prune > 0.0f) && !(d.grown != nullptr && kp.p_new > 0.0f);
+    // lean: the pass without pruning or synaptogenesis -- single-GPU, or the
+    // first launch of a sharded pass (less code in the pass end)
+    const bool plastic = kp.w_prune > 0.0f || (d.grown != nullptr && kp.p_new > 0.0f);
+    const bool lean = d.lean && !plastic;
     if (kp.track_visits) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, true, false, true>), g, b, 0, s, d, kp);
-    else if (lean) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false, true, true>), g, b, 0, s, d, kp);
+    else if (lean && !d.shard_mode) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false, true, true>), g, b, 0, s, d, kp);
+    else if (lean) hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false, true, true, true>), g, b, 0, s, d, kp);
     else hipLaunchKernelGGL((k_gate<BLOCK, K, FW, false, false, true>), g, b, 0, s, d, kp);
     return hipGetLastError();
 }
@@ -2466,9 +2472,12 @@ int occupancy_fused_shape(bool track)
         const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, true, false, true>, BLOCK, 0);
         return e == hipSuccess ? n : 0;
     }
+    int q = 0;
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gate<BLOCK, K, FW, false, false, true>, BLOCK, 0);
     const hipError_t f = hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, k_gate<BLOCK, K, FW, false, false, true, true>, BLOCK, 0);
-    return e == hipSuccess && f == hipSuccess ? std::min(n, m) : 0;
+    const hipError_t h = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &q, k_gate<BLOCK, K, FW, false, false, true, true, true>, BLOCK, 0);
+    return e == hipSuccess && f == hipSuccess && h == hipSuccess ? std::min(n, std::min(m, q)) : 0;
 }
 
 // Compiled gate shapes: threads per workgroup x events per lane x filter words.

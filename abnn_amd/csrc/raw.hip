@@ -74,9 +74,11 @@ constexpr uint32_t kRawScanBlock = 4 * kRawScanThreads;  // groups per k_raw_sca
 static_assert(kRawWaves % kRawScanThreads == 0, "k_raw_scan sums the gate waves' statistics in whole rounds");
 constexpr uint32_t kRawApplyWGs = 1024;              // x 4 waves, grid-stride over the groups below the cut
 constexpr uint32_t kRawNone = 0xFFFFFFFFu;
+constexpr uint32_t kRawCtab = 0xFFFFFFFEu;  // ginfo: the group's survivors span > 2 chunks (ctab lookup)
+constexpr uint32_t kRawRedo = 0xFFFFFFFDu;  // ginfo: not all stored (the pool ran out): recompute
 
 // Workspace (16-B aligned pieces):
-//   hdr | filter (FB uint2) | gcand[NG] | gpre[NG] | btot[NG / 4096] | ginfo[NG] {S, seq} |
+//   hdr | filter (FB uint2) | gcand[NG] | gpre[NG] | btot[NG / 4096] | ginfo[NG] {S, seq, chunks} |
 //   wlim[W] | wstat[W] | ctab[W][maxc] | spikes[L] | pool[cap][kRawChunk] uint4
 struct RawHdr {
     uint32_t now, budget0, t0, ncand;  // pass-start clock and budget; event 0 survived; spikes (capped)
@@ -97,7 +99,8 @@ struct RawWs {
     uint32_t* gcand;   // spike candidates per group
     uint32_t* gpre;    // exclusive candidate prefix per group within its scan block of 4096 groups
     uint32_t* btot;    // per scan block: its candidates; then (k_raw_scan) the blocks before it, capped
-    uint2* ginfo;      // {survivors, first index in the owning wave's survivor sequence}
+    uint4* ginfo;      // {survivors, first index in the owning wave's survivor sequence, pool chunk of
+                       //  that entry, the next chunk} (kRawCtab: > 2 chunks, kRawRedo: not all stored)
     uint32_t* wlim;    // per wave: survivor-sequence entries stored (the rest overflowed the pool)
     uint2* wstat;      // per wave: {pre-gated, survivors} of its groups (k_raw_scan sums them)
     uint32_t* ctab;    // per wave: pool chunk of every 256 entries of its sequence
@@ -118,7 +121,7 @@ inline uint64_t raw_fixed_bytes(uint64_t E)
 {
     const uint64_t ng = raw_groups(E);
     const uint64_t L = std::min<uint64_t>(E, kRawSpikeCap);
-    return 64 + kRawFB * 8 + al16(4 * ng) * 2 + al16(4 * ((ng + kRawScanBlock - 1) / kRawScanBlock)) + al16(8 * ng) +
+    return 64 + kRawFB * 8 + al16(4 * ng) * 2 + al16(4 * ((ng + kRawScanBlock - 1) / kRawScanBlock)) + al16(16 * ng) +
            al16(4ull * kRawWaves) + al16(8ull * kRawWaves) +
            al16(4ull * kRawWaves * raw_maxc(ng)) + al16(4 * L);
 }
@@ -153,8 +156,8 @@ inline RawWs raw_ws(void* base, uint64_t E, uint64_t bytes)
     p += al16(4 * ng);
     w.btot = reinterpret_cast<uint32_t*>(p);
     p += al16(4 * ((ng + kRawScanBlock - 1) / kRawScanBlock));
-    w.ginfo = reinterpret_cast<uint2*>(p);
-    p += al16(8 * ng);
+    w.ginfo = reinterpret_cast<uint4*>(p);
+    p += al16(16 * ng);
     w.wlim = reinterpret_cast<uint32_t*>(p);
     p += al16(4ull * kRawWaves);
     w.wstat = reinterpret_cast<uint2*>(p);
@@ -391,8 +394,18 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_gate(const uint4* __restrict_
         }
         if (pend) flush();
         if (lane == 0) {
+            // where the group's survivors are: the chunk of entry seq0 and the
+            // next one (a group's <= 256 survivors span at most two)
+            uint32_t ia = kRawNone, ib = kRawNone;
+            if (S) {
+                const uint32_t c0 = seq0 / kRawChunk, c1 = (seq0 + S - 1) / kRawChunk;
+                if (lim != kRawNone && seq0 + S > lim) ia = kRawRedo;
+                else if (c1 == c0) ia = cur;  // c1 = have - 1
+                else if (c1 == c0 + 1) { ia = prev; ib = cur; }
+                else ia = kRawCtab;
+            }
             ws.gcand[g] = C;
-            ws.ginfo[g] = make_uint2(S, seq0);
+            ws.ginfo[g] = make_uint4(S, seq0, ia, ib);
         }
     }
     if (lane == 0) {
@@ -548,77 +561,142 @@ __device__ __forceinline__ void raw_apply_one(uint4* syn, uint32_t* lastF, const
     }
 }
 
+// k_raw_apply: every wave takes kRawApplyGroups groups below the cut at a
+// time (strided over the waves): their {survivors, place} and budget positions in one round
+// trip (a lane per group), the survivors of all of them in a second (a group
+// keeps ~3 at config 3, the dense input->output groups up to 1024), then the
+// walk in event order.  The groups below the cut are ~25 % of all at config
+// 3, so per-group round trips would be a chain of ~9 per wave.
+constexpr uint32_t kRawApplyGroups = 16;
+
+__device__ __forceinline__ uint4 raw_pool_entry(const RawWs& ws, const uint4& gi, uint32_t v, uint32_t q)
+{
+    const uint32_t x = gi.y + q, c = x / kRawChunk;
+    const uint32_t id = gi.z == kRawCtab ? ws.ctab[(uint64_t)v * ws.maxc + c]
+                                         : (c == gi.y / kRawChunk ? gi.z : gi.w);
+    return ws.pool[(uint64_t)id * kRawChunk + x % kRawChunk];
+}
+
+// One group below the cut with more than 64 survivors (a dense stretch), or
+// whose survivors did not fit the pool (recomputed from its records with the
+// pass-start lastF: the stamps then wait for k_raw_stamp).
+__device__ __forceinline__ void raw_apply_group(uint4* syn, uint32_t* lastF, uint32_t n_nrn, uint32_t E,
+                                             const KernelParams& kp, const RawWs& ws, const RawHdr& h, uint32_t g,
+                                             uint4 gi, uint32_t P)
+{
+    const uint32_t lane = threadIdx.x & 63, S = gi.x, v = g % kRawWaves;
+    if (gi.z != kRawRedo) {  // stored: the wave's sequence [s0, s0 + S), 4 x 64 in flight
+        constexpr uint32_t RW = 4;
+        for (uint32_t b0 = 0; b0 < S && P < h.budget0; b0 += RW * 64) {  // wave-uniform
+            uint4 x[RW];
+#pragma unroll
+            for (uint32_t j = 0; j < RW; ++j)
+                x[j] = b0 + j * 64 + lane < S ? raw_pool_entry(ws, gi, v, b0 + j * 64 + lane) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (uint32_t j = 0; j < RW; ++j) {
+                if (b0 + j * 64 >= S || P >= h.budget0) break;  // wave-uniform
+                const bool ok = b0 + j * 64 + lane < S;
+                const bool cand = ok && (x[j].y >> 31);
+                const uint64_t bc = __ballot(cand);
+                const uint32_t pre = P + mbcnt64(bc);
+                if (ok && pre < h.budget0) raw_apply_one(syn, lastF, ws, h, kp, x[j], cand, pre);
+                P += (uint32_t)__popcll(bc);
+            }
+        }
+        return;
+    }
+    if (h.direct && lane == 0) ws.hdr->err = 1u;  // (direct here only with a budget beyond the list)
+    constexpr uint32_t RH = kRawGroup / 64 / 2;  // two halves: records and their lastF in flight
+    for (uint32_t h0 = 0; h0 < 2 * RH && P < h.budget0; h0 += RH) {  // wave-uniform
+        uint4 rc[RH];
+#pragma unroll
+        for (uint32_t j = 0; j < RH; ++j) {
+            const uint64_t t = (uint64_t)g * kRawGroup + (h0 + j) * 64 + lane;
+            rc[j] = t < E ? syn[t] : make_uint4(kRawNone, kRawNone, 0u, 0u);
+        }
+        uint32_t la[RH], lb[RH];
+#pragma unroll
+        for (uint32_t j = 0; j < RH; ++j) {
+            const bool ok = rc[j].x < n_nrn && rc[j].y < n_nrn;
+            la[j] = ok ? lastF[rc[j].x] : h.now;
+            lb[j] = ok ? lastF[rc[j].y] : h.now;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < RH; ++j) {
+            if (P >= h.budget0) break;  // wave-uniform
+            const uint64_t t = (uint64_t)g * kRawGroup + (h0 + j) * 64 + lane;
+            const bool ok = rc[j].x < n_nrn && rc[j].y < n_nrn;
+            const bool g2 = ok && h.now - la[j] <= kp.window_pre && h.now - lb[j] > kp.refractory;  // brain.metal:73-83
+            const bool cand = g2 && spike_candidate(kp, __uint_as_float(rc[j].z), t, h.now);        // brain.metal:91-92
+            const uint64_t bc = __ballot(cand);
+            const uint32_t pre = P + mbcnt64(bc);
+            if (g2 && pre < h.budget0)
+                raw_apply_one(syn, lastF, ws, h, kp,
+                              make_uint4((uint32_t)t, __float_as_uint((float)(h.now - lb[j])), rc[j].z, rc[j].y), cand,
+                              pre);
+            P += (uint32_t)__popcll(bc);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_raw_apply(uint4* syn, uint32_t* lastF, uint32_t n_nrn, uint32_t E,
                                                    KernelParams kp, RawWs ws)
 {
+    constexpr uint32_t GA = kRawApplyGroups;
     const uint32_t lane = threadIdx.x & 63;
     const RawHdr h = *ws.hdr;  // pass-start scalars (k_raw_scan)
     const uint32_t nw = gridDim.x * 4u;
-    for (uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6); g < h.gcut; g += nw) {  // wave-uniform
-        uint32_t P = ws.btot[g / kRawScanBlock] + ws.gpre[g];  // < budget0: g < gcut
-        const uint2 gi = ws.ginfo[g];
-        const uint32_t S = gi.x, s0 = gi.y, v = g % kRawWaves, lim = ws.wlim[v];
-        if (S == 0) continue;
-        // a group holds <= 1024 events: all its survivors (or records) are
-        // loaded at once, 16 per lane, then walked in event order -- one
-        // round trip, not one per 64 (the dense input->output groups)
-        constexpr uint32_t RW = kRawGroup / 64;
-        if (lim == kRawNone || s0 + S <= lim) {  // stored: the wave's sequence [s0, s0 + S)
-            const uint32_t* ct = ws.ctab + (uint64_t)v * ws.maxc;
-            const uint32_t c0 = s0 / kRawChunk, nc = (s0 + S - 1) / kRawChunk - c0 + 1;  // <= 5 chunks
-            const uint32_t cid = lane < nc ? ct[c0 + lane] : 0u;
-            uint4 e[RW];
+    // slot i of round r of wave w: group (r GA + i) nw + w -- strided, so the
+    // dense groups at the start of the sweep spread over many waves
+    const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);
+    for (uint32_t r0 = 0; r0 * nw < h.gcut; r0 += GA) {  // wave-uniform
+        const uint32_t g0 = r0 * nw + w;  // the round's first group; slot i is g0 + i nw
+        // lane i < GA: slot i
+        const uint32_t gl = g0 + (lane < GA ? lane : 0u) * nw;
+        const bool mine = lane < GA && gl < h.gcut;
+        const uint4 gi_l = mine ? ws.ginfo[gl] : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t pre_l = mine ? ws.btot[gl / kRawScanBlock] + ws.gpre[gl] : h.budget0;
+        // survivors of every group with at most 64 (one per lane), all in flight
+        uint4 e[GA];
 #pragma unroll
-            for (uint32_t j = 0; j < RW; ++j) {
-                const uint32_t q = j * 64 + lane, x = s0 + q;
-                const uint32_t id = (uint32_t)__shfl((int)cid, (int)(q < S ? x / kRawChunk - c0 : 0u), 64);
-                e[j] = q < S ? ws.pool[(uint64_t)id * kRawChunk + x % kRawChunk] : make_uint4(0u, 0u, 0u, 0u);
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < RW; ++j) {
-                if (j * 64 >= S || P >= h.budget0) break;  // wave-uniform
-                const bool ok = j * 64 + lane < S;
-                const bool cand = ok && (e[j].y >> 31);
-                const uint64_t bc = __ballot(cand);
-                const uint32_t pre = P + mbcnt64(bc);  // spike candidates before this event
-                if (ok && pre < h.budget0) raw_apply_one(syn, lastF, ws, h, kp, e[j], cand, pre);
-                P += (uint32_t)__popcll(bc);
-            }
-            continue;
+        for (uint32_t i = 0; i < GA; ++i) {
+            const uint32_t S = (uint32_t)__builtin_amdgcn_readlane((int)gi_l.x, (int)i);
+            const uint4 gi = make_uint4(S, (uint32_t)__builtin_amdgcn_readlane((int)gi_l.y, (int)i),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)gi_l.z, (int)i),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)gi_l.w, (int)i));
+            const bool direct_load = S <= 64 && gi.z != kRawRedo;
+            e[i] = direct_load && lane < S ? raw_pool_entry(ws, gi, (g0 + i * nw) % kRawWaves, lane) : make_uint4(0u, 0u, 0u, 0u);
         }
-        // not stored (the pool ran out): the group again from its records,
-        // with the pass-start lastF (the stamps wait for k_raw_stamp)
-        if (h.direct && lane == 0) ws.hdr->err = 1u;  // (direct here only with a budget beyond the list)
-        constexpr uint32_t RH = RW / 2;  // two halves: records and their lastF in flight, no spills
-        for (uint32_t h0 = 0; h0 < RW && P < h.budget0; h0 += RH) {  // wave-uniform
-            uint4 rc[RH];
+        uint32_t slow = 0;  // groups for raw_apply_group (wave-uniform bit mask)
 #pragma unroll
-            for (uint32_t j = 0; j < RH; ++j) {
-                const uint64_t t = (uint64_t)g * kRawGroup + (h0 + j) * 64 + lane;
-                rc[j] = t < E ? syn[t] : make_uint4(kRawNone, kRawNone, 0u, 0u);
+        for (uint32_t i = 0; i < GA; ++i) {
+            const uint32_t g = g0 + i * nw;
+            const uint32_t S = (uint32_t)__builtin_amdgcn_readlane((int)gi_l.x, (int)i);
+            const uint32_t gz = (uint32_t)__builtin_amdgcn_readlane((int)gi_l.z, (int)i);
+            if (g >= h.gcut || S == 0) continue;  // wave-uniform
+            if (S > 64 || gz == kRawRedo) {
+                slow |= 1u << i;
+                continue;
             }
-            uint32_t la[RH], lb[RH];
-#pragma unroll
-            for (uint32_t j = 0; j < RH; ++j) {
-                const bool ok = rc[j].x < n_nrn && rc[j].y < n_nrn;
-                la[j] = ok ? lastF[rc[j].x] : h.now;
-                lb[j] = ok ? lastF[rc[j].y] : h.now;
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < RH; ++j) {
-                if (P >= h.budget0) break;  // wave-uniform
-                const uint64_t t = (uint64_t)g * kRawGroup + (h0 + j) * 64 + lane;
-                const bool ok = rc[j].x < n_nrn && rc[j].y < n_nrn;
-                const bool g2 = ok && h.now - la[j] <= kp.window_pre && h.now - lb[j] > kp.refractory;  // brain.metal:73-83
-                const bool cand = g2 && spike_candidate(kp, __uint_as_float(rc[j].z), t, h.now);        // brain.metal:91-92
-                const uint64_t bc = __ballot(cand);
-                const uint32_t pre = P + mbcnt64(bc);
-                if (g2 && pre < h.budget0)
-                    raw_apply_one(syn, lastF, ws, h, kp,
-                                  make_uint4((uint32_t)t, __float_as_uint((float)(h.now - lb[j])), rc[j].z, rc[j].y),
-                                  cand, pre);
-                P += (uint32_t)__popcll(bc);
-            }
+            // the common case: prefetched above
+            const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pre_l, (int)i);  // < budget0: g < gcut
+            const bool ok = lane < S;
+            const bool cand = ok && (e[i].y >> 31);
+            const uint64_t bc = __ballot(cand);
+            const uint32_t pre = P + mbcnt64(bc);  // spike candidates before this event
+            if (ok && pre < h.budget0) raw_apply_one(syn, lastF, ws, h, kp, e[i], cand, pre);
+        }
+        // groups are independent (each one's budget position is known), so
+        // the rare big or recomputed ones may come last
+        while (slow) {  // wave-uniform
+            const uint32_t i = (uint32_t)__builtin_ctz(slow);
+            slow &= slow - 1u;
+            const uint4 gi = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)gi_l.x, (int)i),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)gi_l.y, (int)i),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)gi_l.z, (int)i),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)gi_l.w, (int)i));
+            raw_apply_group(syn, lastF, n_nrn, E, kp, ws, h, g0 + i * nw, gi,
+                            (uint32_t)__builtin_amdgcn_readlane((int)pre_l, (int)i));
         }
     }
 }
@@ -712,7 +790,7 @@ abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream)
     hipLaunchKernelGGL(k_raw_scan, dim3(1), dim3(kRawScanThreads), 0, s, ws, (uint32_t)E, a->clock, a->budget, a->reward,
                        a->rbar, kp);
     if (ws.ng) {
-        const uint32_t g = (uint32_t)std::min<uint64_t>((ws.ng + 3) / 4, kRawApplyWGs);
+        const uint32_t g = (uint32_t)std::min<uint64_t>((ws.ng + 4 * kRawApplyGroups - 1) / (4 * kRawApplyGroups), kRawApplyWGs);
         hipLaunchKernelGGL(k_raw_apply, dim3(g), dim3(256), 0, s, syn, a->last_fired, a->n_nrn, (uint32_t)E, kp, ws);
         hipLaunchKernelGGL(k_raw_stamp, dim3(1), dim3(1024), 0, s, a->last_fired, ws);
     }

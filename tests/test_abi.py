@@ -167,7 +167,7 @@ def _raw_ws_bytes(n_syn: int, events: int) -> tuple[int, int]:
     E = min((events + 255) // 256 * 256, n_syn)
     g, W = (E + 1023) // 1024, 4096
     maxc = (g + W - 1) // W * 4 + 1
-    fixed = 64 + 8192 * 8 + 2 * al(4 * g) + al(4 * ((g + 4095) // 4096)) + al(8 * g) + al(4 * W) + al(8 * W) + al(4 * W * maxc) + al(4 * min(E, 65536))
+    fixed = 64 + 8192 * 8 + 2 * al(4 * g) + al(4 * ((g + 4095) // 4096)) + al(16 * g) + al(4 * W) + al(8 * W) + al(4 * W * maxc) + al(4 * min(E, 65536))
     pool = (W + (E // 64 + 255) // 256 + 64) * 4096 if E else 0
     return fixed, fixed + pool
 
