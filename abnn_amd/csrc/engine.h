@@ -50,6 +50,12 @@ struct alignas(16) PassWork {
     uint32_t spec_wgs;     // fused pass: gate workgroups predicted below the budget cut (the last pass's, less one)
     uint32_t pad;
     unsigned long long shard_g2;  // sharded fused pass: refractory survivors of the shard (the summary's word 3)
+    // sharded fused pass: the pass-start scalars as the gate launch read them
+    // (written by its workgroup 0), so every k_shard_walk workgroup reads
+    // these and its workgroup 0 ends the pass at once, without a ticket
+    unsigned long long ps_now, ps_pass;
+    float ps_R, ps_rb;
+    uint32_t pad2[2];
     abnn_stats stats;      // host-kept counters (grown); the device ones live in DeviceState::wg_stats
 };
 

@@ -1213,6 +1213,10 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
             sm[3] = (int64_t)__hip_atomic_load(&d.work->shard_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             d.work->shard_g2 = 0;
             d.work->epoch = epoch + 1u;
+            d.work->ps_now = now;  // the pass-start scalars for k_shard_walk (C1)
+            d.work->ps_pass = pass;
+            d.work->ps_R = R;
+            d.work->ps_rb = rb;
         }
         return;
     }
@@ -2187,11 +2191,11 @@ __global__ __launch_bounds__(NW * 64) void k_shard_walk(DeviceState d, KernelPar
     // diagnostics (tools/shard_clock.py): per workgroup, 100-MHz ticks
     uint64_t* ck = d.apply_clock + 8ull * (blockIdx.x % kWalkBlocks);
     if (threadIdx.x == 0) ck[0] = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0) {  // pass-start scalars (C1): the last workgroup rewrites them
-        s_R = *d.reward;
-        s_rb = *d.rbar;
-        s_now = *d.clock;
-        s_pass = *d.pass_index;
+    if (threadIdx.x == 0) {  // pass-start scalars (C1), as the gate launch read them: workgroup 0
+        s_R = d.work->ps_R;   // rewrites the live ones (finalize_pass) while others still start
+        s_rb = d.work->ps_rb;
+        s_now = d.work->ps_now;
+        s_pass = d.work->ps_pass;
     }
     if (threadIdx.x < 3) s_stat[threadIdx.x] = 0u;
     __syncthreads();
@@ -2232,12 +2236,10 @@ __global__ __launch_bounds__(NW * 64) void k_shard_walk(DeviceState d, KernelPar
         if (s_stat[0]) atomicAdd((ull*)&st->updated, (ull)s_stat[0]);
         if (s_stat[1]) atomicAdd((ull*)&st->fired, (ull)s_stat[1]);
         if (s_stat[2]) atomicAdd((ull*)&st->pruned, (ull)s_stat[2]);
-        if (blockIdx.x == 0) d.n_fired_ring[pass & (kFiredRing - 1)] = (uint32_t)nsp;
-        const uint32_t ticket = __hip_atomic_fetch_add((gu32*)(&d.work->ticket), 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
         ck[5] = __builtin_amdgcn_s_memrealtime();
-        ck[6] = ticket == gridDim.x - 1;
-        if (ticket == gridDim.x - 1) {
+        ck[6] = blockIdx.x == 0;
+        if (blockIdx.x == 0) {  // the pass's end: no workgroup reads the live scalars (ps_* above)
+            d.n_fired_ring[pass & (kFiredRing - 1)] = (uint32_t)nsp;
             const int64_t mine = *reinterpret_cast<const int64_t*>(gathered + rank * xchg_words(kp.max_spikes));
             if (off >= budget) d.work->spec_wgs = 0u;                        // the whole shard past the cut
             else if (off + (uint64_t)mine < budget) d.work->spec_wgs = gridDim.x;  // ... below it

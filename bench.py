@@ -302,11 +302,20 @@ def raw_main(args) -> None:
         },
         "cpu_baseline": None,
     }
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=_JSON_OUT, flush=True)
+
+
+_JSON_OUT = sys.stdout
 
 
 def main():
     args = parse()
+    # stdout carries the ONE JSON line: anything else the process prints on
+    # file descriptor 1 (RCCL's init banner, runtime notices) goes to stderr
+    sys.stdout.flush()
+    global _JSON_OUT
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if args.raw:
         if int(os.environ.get("WORLD_SIZE", "1")) != 1:
             raise SystemExit("--raw runs on one GPU")
@@ -490,7 +499,7 @@ def main():
             },
             "roofline": roofline, "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=_JSON_OUT, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
