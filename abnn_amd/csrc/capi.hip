@@ -1398,6 +1398,20 @@ abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, vo
     return st;
 }
 
+// Diagnostics (abnn_debug.h): `count` in-place all-gathers of `bytes` per
+// rank from `buf` (rank order, world x bytes), the sharded pass's exchange
+// alone (tools/allgather_time.py).
+abnn_status abnn_debug_comm_allgather(abnn_comm* c, void* buf, uint64_t bytes, uint32_t count, void* stream)
+{
+    REQUIRE(c && buf, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    char* base = static_cast<char*>(buf);
+    for (uint32_t i = 0; i < count; ++i)
+        RCCL_TRY(rccl_api().all_gather(base + bytes * c->rank, base, bytes, ncclInt8, c->comm, s));
+    return ABNN_OK;
+}
+
 abnn_status abnn_comm_sync_visits(abnn_brain* b, abnn_comm* c, void* stream)
 {
     REQUIRE(b && c, "null argument");

@@ -37,6 +37,11 @@ abnn_status abnn_debug_raw_stats(const void* workspace, uint64_t* out2, void* st
 abnn_status abnn_debug_raw_gate_timing(int enable);
 abnn_status abnn_debug_raw_gate_time(double* total_ms, uint32_t* launches);
 
+/* The sharded pass's exchange alone: `count` in-place all-gathers of
+ * `bytes` per rank on the library's RCCL communicator (enqueued on `stream`;
+ * buf holds world x bytes, this rank's record at rank x bytes). */
+abnn_status abnn_debug_comm_allgather(abnn_comm* c, void* buf, uint64_t bytes, uint32_t count, void* stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif
