@@ -1003,6 +1003,37 @@ __device__ __forceinline__ uint32_t spec_prediction(const DeviceState& d, uint32
     return v < 0 ? 0u : (v > (int64_t)G ? G : (uint32_t)v);
 }
 
+// The bitmap and filter images of the pass after next (the next pass builds
+// them: k_apply, the fused pass, or k_bitmap) zeroed, a slice per workgroup;
+// this pass's stimulus stamped by workgroup 0 (every refractory stage of the
+// pass reads a stimulus neuron's lastFired as now without loading it).
+__device__ __forceinline__ void zero_next_images(const DeviceState& d, uint32_t FW, uint32_t BLOCK, uint64_t now)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nz = d.n_bitmap_words + 2 * FW + kF2Words, per = (nz + gridDim.x - 1) / gridDim.x;
+    for (uint32_t i = blockIdx.x * per + tid; i < min(nz, (blockIdx.x + 1) * per); i += BLOCK) {
+        if (i < d.n_bitmap_words) d.bitmap_clear[i] = 0u;
+        else d.filter_clear[i - d.n_bitmap_words] = 0u;
+    }
+    if (blockIdx.x == 0)
+        for (uint64_t i = tid; i < d.stim_count; i += BLOCK) d.last_fired[d.stim_first + i] = now;
+}
+
+// s_waitcnt vmcnt(N) lgkmcnt(0) for the counts of record loads the gate's
+// prologue leaves in flight.  The builtin, not inline asm: the compiler's
+// wait-count tracking then knows the older LDS-DMAs are done (after an asm
+// wait it would still count them pending and drain vmcnt(0) before the
+// stream loop's first LDS read, every iteration).  gfx9 encoding: vmcnt
+// [3:0] and [15:14], expcnt [6:4] (7: no wait), lgkmcnt [11:8].
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+    asm volatile("" ::: "memory");
+}
+
 // LDS of the fused pass's end (per workgroup).
 template <int NW>
 struct FusedLds {
@@ -1203,6 +1234,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         // sharded pass: no stamps, no pass end here (k_shard_walk, after the
         // exchange); workgroup 0 writes the exchange summary (abnn.h) once
         // every word is published
+        zero_next_images(d, kCodeFilterWords, BLOCK, now);
         if (!first || wid != 0) return;
         const uint32_t tt = wg_poll(d, gridDim.x, tag, budget, false, vals);
         if (lane == 0) {
@@ -1243,6 +1275,8 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         __hip_atomic_store((gu32*)&d.work->t0_g2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         d.work->epoch = epoch + 1u;
     }
+    // last: no load of this pass follows these stores
+    zero_next_images(d, kCodeFilterWords, BLOCK, now);
     if (threadIdx.x == 0) wc0[13] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -1404,30 +1438,33 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             }
         }
     };
+    __builtin_amdgcn_sched_barrier(0);  // the LDS-DMAs above stay older than the records (see the wait below)
     issue(A, it_begin, it_begin < it_end);
     if constexpr (kDepth == 2) issue(B, it_begin + 1, it_begin + 1 < it_end);
-    {
+    if constexpr (!kFused) {
         // the bitmap and images of the pass after next are zeroed here (the
-        // next pass builds them: k_apply, the fused pass, or k_bitmap), a
-        // slice per workgroup; this pass's stimulus is stamped by workgroup 0
-        // (the refractory stage reads it as now)
-        const uint32_t nz = d.n_bitmap_words + 2 * FW + kF2Words, per = (nz + gridDim.x - 1) / gridDim.x;
-        for (uint32_t i = blockIdx.x * per + tid; i < min(nz, (blockIdx.x + 1) * per); i += BLOCK) {
-            if (i < d.n_bitmap_words) d.bitmap_clear[i] = 0u;
-            else d.filter_clear[i - d.n_bitmap_words] = 0u;
-        }
-        if (blockIdx.x == 0)
-            for (uint64_t i = tid; i < d.stim_count; i += BLOCK) d.last_fired[d.stim_first + i] = now;
-        if constexpr (kFused) {
-            if (tid < 5) s_fz.stat[tid] = 0u;
-            if (tid == 0) s_fz.done = 0u;
-            if (tid == 0) s_fz.sg2 = 0u;
-            if (tid < kSetCache) s_fz.setc[tid] = ~0ull;
-        }
+        // next pass builds them: k_apply or k_bitmap), a slice per workgroup;
+        // this pass's stimulus is stamped by workgroup 0 (the refractory stage
+        // reads it as now).  The fused pass does both at its end (fused_end).
+        zero_next_images(d, FW, BLOCK, now);
+        lds_barrier();
+    } else {
+        if (tid < 5) s_fz.stat[tid] = 0u;
+        if (tid == 0) s_fz.done = 0u;
+        if (tid == 0) s_fz.sg2 = 0u;
+        if (tid < kSetCache) s_fz.setc[tid] = ~0ull;
+        // the filter images in LDS for every wave, the first records still in
+        // flight: this wave's LDS-DMAs are older than its kDepth iterations of
+        // record loads, and vmcnt retires in order.  (A release fence here
+        // would wait for vmcnt(0): the records' whole round trip, and until
+        // round 4 the prologue's zeroing stores too, before the stream began.)
+        // (kTrack: the {dst, w} pairs of the same events too, one iteration deep)
+        constexpr int kRecLoads = kDepth * (3 * NG + (kTrack ? 2 * NG : 0));
+        __builtin_amdgcn_sched_barrier(0);
+        wait_vm_lgkm0<kRecLoads>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
-    // the filter images in LDS for every wave; the prologue's global stores
-    // (zeroing, stimulus) and the first records stay in flight
-    lds_barrier();
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     // diagnostics (tools/wave_clock.py): the fused pass keeps the last
     // kWaveClockPasses passes' clocks (slot pass % kWaveClockPasses)
@@ -1630,9 +1667,14 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         d.wave_clock[kWaveClock * r + 6] = chunk_t;
         d.wave_clock[kWaveClock * r + 7] = nch;
     }
-    // the tail (latency-bound) runs at the lowest issue priority: the streams
-    // still running go first (profiles/r03g_ab_gain1_tailprio0.txt)
-    __builtin_amdgcn_s_setprio(0);
+    // the tail (a latency-bound chain of two gathers, few instructions) and
+    // the pass's end run at the highest issue priority.  At the lowest (round
+    // 3) a SIMD's tails lost every tie to its streams and then went by wave
+    // age: the youngest waves' tails took 10-13 us against 6-8 for the oldest
+    // (tools/wc_multi.py), and the partition, which balances stream + tail,
+    // could not correct a cost that follows the wave slot, not the range
+    // (profiles/r04k_*: tails 6-7.5 us, -0.4 us per pass)
+    __builtin_amdgcn_s_setprio(3);
     // the range's last chunk: refractory stage by this wave
     const uint64_t tb = kFused ? region + tot.y : region + (uint64_t)nch * kChunk;
     // fused, single GPU, no synaptogenesis (its src list is global): the
