@@ -1092,9 +1092,8 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     // The next pass's bitmap build items that do not depend on this pass (the
     // spike lists of passes p+1-W..p-1, the stimulus): item x to workgroup
     // h0 + x % (G - h0), by waves [w0, NW) of it.  With h0 > 0 only the
-    // workgroups past the predicted budget cut take them, after their
-    // look-back (they have no walk); with h0 = 0 every workgroup's waves 1..
-    // take them while wave 0 publishes and polls.
+    // workgroups past the predicted budget cut take them (they have no walk),
+    // with h0 = 0 every workgroup.
     auto next_share = [&](uint32_t w0) {
         const uint64_t nitems = next_items(d, kp), HG = gridDim.x - h0, hb = blockIdx.x - h0;
         for (uint64_t s0 = (uint64_t)(wid - w0) * 64; s0 * HG + hb < nitems; s0 += (uint64_t)(NW - w0) * 64) {
@@ -1103,7 +1102,10 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
             wave_set_next_dedup(d, it.i < it.lim, it.n, L.setc);
         }
     };
-    if (h0 == 0 && wid != 0 && d.build_next) next_share(1);
+    // (waves 1.. take them while wave 0 publishes and polls: the workgroups
+    // past the predicted cut have no walk after it, so the items would
+    // otherwise come after their look-back, on the pass's critical path)
+    if (wid != 0 && d.build_next && (h0 == 0 || blockIdx.x >= h0)) next_share(1);
     if (wid == 0) {
         uint32_t c = lane < (uint32_t)NW ? L.cand[lane] : 0u;
         c = wave_sum(c);
@@ -1190,7 +1192,6 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
             d.range_info[r] = make_uint4((uint32_t)(P < budget ? P : budget), S, C, (spec ? 1u : 0u) | (empty ? 2u : 0u));
         range_spikes_local(d, kp, r, region, S, C, P, d.xchg + 2 * ABNN_SUMMARY_WORDS);
     }
-    if (h0 > 0 && blockIdx.x >= h0 && d.build_next) next_share(0);
     const uint64_t t_walk = __builtin_amdgcn_s_memrealtime();
     const uint32_t wu = wave_sum(ac.upd) + upd_rest, wf = wave_sum(ac.nf), wp = wave_sum(ac.npr);
     if (lane == 0) {
