@@ -705,7 +705,8 @@ __device__ __forceinline__ void apply_event(const DeviceState& d, const KernelPa
 // cc[NR] = total) reaches k / NR of the total, rounded to the nearest
 // iteration.
 __device__ __forceinline__ uint32_t adapted_bound(const DeviceState& d, const uint32_t* cc, const uint32_t* rb,
-                                                  uint32_t NR, uint32_t k, uint32_t total_cost, uint32_t from)
+                                                  uint32_t NR, uint32_t k, uint32_t total_cost, uint32_t from,
+                                                  uint32_t gain = 0)
 {
     uint32_t nb = from;
     if (d.adapt_ranges && k > 0 && k < NR && total_cost > 0) {
@@ -721,7 +722,7 @@ __device__ __forceinline__ uint32_t adapted_bound(const DeviceState& d, const ui
         const uint32_t cr = cc[lo + 1] - cc[lo];
         const uint64_t tfp = (uint64_t)rb[lo] * 256u +
                              (cr ? (uint64_t)(T - cc[lo]) * (rb[lo + 1] - rb[lo]) * 256u / cr : 0u);
-        const uint32_t g = d.adapt_gain;
+        const uint32_t g = gain ? gain : d.adapt_gain;
         nb = (uint32_t)(((uint64_t)from * 256u * (4u - g) + tfp * g + 512u) >> 10);
     }
     return nb;
@@ -814,13 +815,14 @@ __device__ void fused_next_bounds(const DeviceState& d, uint32_t* cc)
     // rows read at once, each row scanned across the wave (DPP) on top of the
     // rows before it, in place
     const uint32_t rows = (NR + 63) / 64;  // NR <= kFusedMaxRanges
-    uint32_t run = 0;
+    uint32_t run = 0, cmax = 0;
     for (uint32_t j0 = 0; j0 < rows; j0 += 8) {  // wave-uniform
         uint32_t v[8];
 #pragma unroll
         for (uint32_t u = 0; u < 8; ++u) {
             const uint32_t q = (j0 + u) * 64 + lane;
             v[u] = q < NR ? cc[q] : 0u;
+            cmax = v[u] > cmax ? v[u] : cmax;
         }
 #pragma unroll
         for (uint32_t u = 0; u < 8; ++u) {
@@ -835,7 +837,19 @@ __device__ void fused_next_bounds(const DeviceState& d, uint32_t* cc)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    if (mine) d.range_bounds_next[k] = adapted_bound(d, cc, d.range_bounds_prev, NR, k, total, d.range_bounds[k]);
+    // a range above 4x the mean cost (a dense stretch the records just grew:
+    // a structural update's hole takes the array's last records, the grown
+    // ones of the update before, whose src fired -- all pre-gated, refractory
+    // chunk after chunk) moves every boundary the whole way to the measured
+    // target this pass, instead of a quarter of it for ~10 passes at twice
+    // the pass time; one gain for every boundary keeps the ranges ordered.
+    // Steady-state noise (the slowest range ~1.2x the mean) never reaches it.
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t x = (uint32_t)__shfl_xor((int)cmax, o, 64);
+        cmax = x > cmax ? x : cmax;
+    }
+    const uint32_t gain = (uint64_t)cmax * NR > 4ull * total ? 4u : 0u;
+    if (mine) d.range_bounds_next[k] = adapted_bound(d, cc, d.range_bounds_prev, NR, k, total, d.range_bounds[k], gain);
 }
 
 // The walk of one range's survivors (the fused pass's g2x entries, contiguous
