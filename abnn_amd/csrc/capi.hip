@@ -98,8 +98,10 @@ struct abnn_brain {
     uint64_t rot = 0;              // passes run by this handle: the bitmap buffers' rotation (never reset)
     // structural updates (compact_every > 0): the second record buffer the
     // compaction writes into (swapped with d.syn), and its scan scratch
-    SynArrays syn_alt{};
     uint64_t* compact_offsets = nullptr;
+    uint32_t* compact_flags = nullptr;  // the in-place compaction's per-block read flags (epoch-tagged)
+    unsigned long long* span_words = nullptr;  // the update's device words (kernels.hip k_span_init)
+    uint32_t compact_epoch = 0;
     uint64_t structural_updates = 0;  // run so far (abnn_structural_updates)
     uint64_t last_pass = ~0ull;       // pass_index of the last pass (its spike list: abnn_get_budget)
     // host-mapped error word: a fused pass whose look-back wait gave up sets it
@@ -141,14 +143,13 @@ void free_all(abnn_brain* b)
     if (!b) return;
     (void)hipSetDevice(b->device);
     void* ptrs[] = {b->d.syn.lo,    b->d.syn.hi,     b->d.syn.dw,     b->d.syn.src32,
-                    b->syn_alt.lo,  b->syn_alt.hi,   b->syn_alt.dw,   b->syn_alt.src32,
                     b->d.last_fired, b->d.last_visited,  b->scalar_block,
                     b->bitmap_buf[0], b->bitmap_buf[1], b->bitmap_buf[2], b->filter_buf[0], b->filter_buf[1],
                     b->filter_buf[2], b->cost_buf[0], b->cost_buf[1], b->d.lb_status, b->d.cand_list,
                     b->d.range_info,    b->d.range_g1,  b->d.g2x,
                     b->d.chunk_cnt,
                     b->d.wg_stats, b->d.claim,  b->d.g2src,      b->d.grown,
-                    b->d.dead,      b->compact_offsets,
+                    b->d.dead,      b->compact_offsets, b->compact_flags, b->span_words,
                     b->d.work,      b->idx_scratch,
                     b->u64_scratch,  b->d.wave_clock,  b->d.apply_clock, b->d.fired_ring, b->d.n_fired_ring, b->d.range_bounds,  b->d.range_bounds_next, b->d.range_bounds_prev,
                     const_cast<uint32_t*>(b->d.dummy)};
@@ -355,84 +356,40 @@ abnn_status reset_ranges(abnn_brain* b)
 // records (or the tail shifts down), then the grown records are appended in
 // (pass, slot) order while capacity lasts.  Synchronous; runs between passes.
 // Only the span and D records move: the tally's bounds give the span's blocks,
-// which are compacted into the spare buffer (syn_alt) at their final places
-// and copied back, so a sweep's update costs O(events), not O(n_syn).
+// whose live records move down to their final places in place (one pass over
+// the span, no spare buffer), so a sweep's update costs O(events), not
+// O(n_syn), and the records take their own size in HBM, not twice it.
 abnn_status structural_update(abnn_brain* b)
 {
     DeviceState& d = b->d;
     const uint64_t n = b->dims.n_syn, cap = b->dims.syn_capacity;
     ST_TRY(sync_all(b));
     const uint64_t nb = (n + kCompactChunk - 1) / kCompactChunk;
-    uint32_t* dead = d.dead;  // tombstones per block: the weight update's pruning tally + uploads
-    uint64_t* offsets = b->compact_offsets;
-    const SynArrays alt = b->syn_alt;
-    hipError_t e = hipSuccess;
-    uint64_t live = n;
-    if (dead && nb) {
-        // {first block, last block + 1, tombstones}, in offsets[0..2] (scratch until the offsets)
-        unsigned long long bounds[3] = {~0ull, 0ull, 0ull};
-        auto* dev = reinterpret_cast<unsigned long long*>(offsets);
-        e = hipMemcpy(dev, bounds, sizeof(bounds), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = launch_dead_bounds(dead, nb, dev, nullptr);
-        if (e == hipSuccess) e = hipMemcpy(bounds, dev, sizeof(bounds), hipMemcpyDeviceToHost);
-        const uint64_t D = bounds[2];
-        if (e == hipSuccess && D) {
-            const uint64_t bf = bounds[0], bl = bounds[1];  // blocks [bf, bl) hold every tombstone
-            std::vector<uint32_t> hc(bl - bf);
-            std::vector<uint64_t> ho(bl - bf);
-            e = hipMemcpy(hc.data(), dead + bf, hc.size() * 4, hipMemcpyDeviceToHost);
-            uint64_t o = bf * kCompactChunk;  // the records before the first tombstone keep their places
-            for (uint64_t i = 0; i < hc.size(); ++i) {
-                ho[i] = o;
-                o += std::min<uint64_t>(kCompactChunk, n - (bf + i) * kCompactChunk) - hc[i];
-            }
-            unsigned long long z = 0;  // 1 + the last tombstone (in block bl - 1)
-            if (e == hipSuccess) e = hipMemcpy(dev, &z, 8, hipMemcpyHostToDevice);
-            const uint64_t lb = (bl - 1) * kCompactChunk;
-            if (e == hipSuccess) e = launch_last_tomb(d.syn, lb, std::min<uint64_t>(kCompactChunk, n - lb), dev, nullptr);
-            if (e == hipSuccess) e = hipMemcpy(&z, dev, 8, hipMemcpyDeviceToHost);
-            if (e == hipSuccess && (z <= lb || z > n || z < D)) e = hipErrorUnknown;  // the tally and the records disagree
-            if (e == hipSuccess) e = hipMemcpy(offsets, ho.data(), ho.size() * 8, hipMemcpyHostToDevice);
-            // the span's live records at their final places in alt, then back
-            if (e == hipSuccess) e = launch_compact(d.syn, n, offsets, alt, bf, bl - bf, nullptr);
-            const uint64_t s0 = bf * kCompactChunk;
-            if (e == hipSuccess) e = launch_copy_records(alt, s0, d.syn, s0, z - D - s0, nullptr);
-            // the hole [z - D, z): the last D records, or the tail shifted down
-            if (e == hipSuccess)
-                e = n - z >= D ? launch_copy_records(d.syn, n - D, d.syn, z - D, D, nullptr)
-                               : launch_copy_records(d.syn, z, d.syn, z - D, n - z, nullptr);
-            if (e == hipSuccess) e = hipMemset(dead + bf, 0, (bl - bf) * 4);
-            live = n - D;
-        }
-    }
-    uint64_t added = 0;
-    if (e == hipSuccess && d.grown) {
-        const uint64_t slots = (uint64_t)b->params.compact_every * b->params.max_spikes;
-        std::vector<uint4> g(slots);
-        e = hipMemcpy(g.data(), d.grown, slots * sizeof(uint4), hipMemcpyDeviceToHost);
-        std::vector<abnn_synapse> app;
-        for (uint64_t j = 0; e == hipSuccess && j < slots && live + app.size() < cap; ++j)
-            if (g[j].w == 1u) {
-                float w;
-                std::memcpy(&w, &g[j].z, 4);
-                app.push_back({g[j].x, g[j].y, w, 0.0f});
-            }
-        if (e == hipSuccess && !app.empty() && records_h2d(d.syn, live, app.size(), app.data()) != ABNN_OK)
-            e = hipErrorUnknown;
-        if (e == hipSuccess) e = hipMemset(d.grown, 0, slots * sizeof(uint4));
-        added = app.size();
-    }
+    const uint64_t slots = d.grown ? (uint64_t)b->params.compact_every * b->params.max_spikes : 0;
+    // the whole update on the device (kernels.hip launch_structural_update):
+    // the tally's span, its offsets, the in-place compaction, the hole, the
+    // grown records; one synchronisation reads D and the records appended
+    b->compact_epoch += 1;
+    *b->err_host = 0;
+    unsigned long long* sp = b->span_words;
+    hipError_t e = launch_structural_update(d.syn, n, cap, d.dead, nb, b->compact_offsets, sp, b->compact_flags,
+                                            b->compact_epoch, d.err_word, (uint32_t)b->cus, d.grown, slots,
+                                            reinterpret_cast<unsigned long long*>(&d.work->stats.grown), nullptr);
+    unsigned long long w[5] = {0, 0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpy(w, sp, sizeof(w), hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
         set_err(std::string("structural update: ") + hipGetErrorString(e));
         return ABNN_ERR_HIP;
     }
-    b->dims.n_syn = live + added;
+    if (const uint32_t err = *b->err_host) {
+        *b->err_host = 0;
+        set_err(err == 2 ? "structural update: the tombstone tally and the records disagree"
+                         : "structural update: the in-place compaction's wait timed out; the records are not valid");
+        return ABNN_ERR_HIP;
+    }
+    b->dims.n_syn = n - w[2] + w[4];
     b->structural_updates += 1;
-    uint64_t grown = 0;
-    HIP_TRY(hipMemcpy(&grown, &d.work->stats.grown, 8, hipMemcpyDeviceToHost));
-    grown += added;
-    HIP_TRY(hipMemcpy(&d.work->stats.grown, &grown, 8, hipMemcpyHostToDevice));
     const uint32_t old_iters = d.iters, old_ranges = d.n_ranges;
     configure(b);
     if (d.n_ranges == old_ranges && old_iters > 0) {
@@ -912,8 +869,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, cap)) != ABNN_OK) return fail(s);
     if (p.compact_every > 0) {  // structural updates: the compaction's second buffer + scratch
         const uint64_t nb = (cap + kCompactChunk - 1) / kCompactChunk;
-        if ((s = alloc_syn(&b->syn_alt, cap + kDummyRecords, p.mode == ABNN_MODE_RANDOM)) != ABNN_OK) return fail(s);
         if ((s = dalloc(&b->compact_offsets, nb + 4)) != ABNN_OK) return fail(s);  // + the span's 3 words
+        if ((s = dalloc(&b->compact_flags, nb)) != ABNN_OK) return fail(s);
+        if ((s = dalloc(&b->span_words, 8)) != ABNN_OK) return fail(s);
         // the tombstone tally: pruning's, and an upload's (a saved pruned brain)
         if ((s = dalloc(&d.dead, nb)) != ABNN_OK) return fail(s);
     }

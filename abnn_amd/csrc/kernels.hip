@@ -2348,6 +2348,188 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint
     }
 }
 
+// The structural update's compaction of the span's blocks [b0, b0 + nblk), IN
+// PLACE, in one pass over the records (round 4: the span went to the spare
+// buffer and was copied back, two passes).  A live record only ever moves
+// down, and by less than the records before its block hold tombstones: block
+// c writes into blocks c_lo..c (c_lo from its offset), so it may write only
+// once each of those has READ its records (registers).  Block c publishes
+// rd[c] = epoch once its loads have landed, then polls the flags of
+// c_lo..c-1.  A persistent grid (one workgroup per CU, all resident) takes
+// blocks in increasing order, strided: the lowest unfinished block waits for
+// none, so no cycle; every poll is bounded (err, never a hang).
+__global__ __launch_bounds__(kCompactThreads) void k_compact_inplace(SynArrays syn, uint64_t n, const uint64_t* offsets,
+                                                                     const unsigned long long* sp, uint32_t* rd,
+                                                                     uint32_t epoch, uint32_t* err)
+{
+    __shared__ uint64_t s_wave[kCompactThreads / 64];
+    __shared__ uint32_t s_bad;
+    const uint32_t lane = threadIdx.x & 63;
+    // the span's blocks (k_dead_bounds); the records from z on (after the
+    // last tombstone, in its block) stay where they are: the hole's fill
+    // takes the array's end (k_span_fill)
+    const uint64_t b0 = sp[0], D = sp[2], z = sp[3], lb = D ? (sp[1] - 1) * kCompactChunk : 0u;
+    // (a tally that disagrees with the records moves nothing: k_span_fill reports it)
+    const uint64_t nblk = D && z > lb && z <= n && z >= D ? sp[1] - sp[0] : 0u;
+    for (uint64_t c = blockIdx.x; c < nblk; c += gridDim.x) {  // workgroup-uniform
+        const uint64_t base = (b0 + c) * kCompactChunk;
+        uint32_t rs[4];
+        uint64_t rdw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t i = base + (uint64_t)j * kCompactThreads + threadIdx.x;
+            const bool in = i < z;  // z <= n
+            rs[j] = in ? src_of(syn, i) : kSrcNone;
+            rdw[j] = in ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(syn.dw + i)) : 0ull;
+        }
+        const uint64_t o0 = offsets[c];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's records are in registers
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s_bad = 0u;
+            __hip_atomic_store(rd + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // the blocks this one writes into, below it, must have read theirs
+        const uint64_t c_lo = o0 / kCompactChunk - b0;  // o0 >= b0 * kCompactChunk
+        if (threadIdx.x < 64 && c_lo < c) {
+            for (uint64_t j0 = c_lo; j0 < c; j0 += 64) {  // wave-uniform
+                const uint64_t j = j0 + lane;
+                for (uint32_t spins = 0;; ++spins) {
+                    const bool ok = j >= c || __hip_atomic_load(rd + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+                    if (__ballot(!ok) == 0) break;
+                    if (spins >= kLbSpinLimit) {
+                        if (lane == 0) {
+                            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            s_bad = 1u;
+                        }
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+        }
+        __syncthreads();
+        if (s_bad) continue;  // (reported: the records are then not trusted)
+        uint64_t o = o0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool live = rs[j] != kSrcNone;
+            uint64_t tot;
+            const uint64_t pre = block_exclusive_scan(live ? 1u : 0u, &tot, s_wave);
+            if (live) {
+                set_src(syn, o + pre, rs[j]);
+                __builtin_nontemporal_store(rdw[j], reinterpret_cast<uint64_t*>(syn.dw + o + pre));
+            }
+            o += tot;
+        }
+    }
+}
+
+// The structural update driven from the device (round 4: one host
+// synchronisation per update instead of six, no host copy of the grown
+// slots).  sp = the update's words: [0] first block with a tombstone, [1] last
+// such block + 1, [2] tombstones D, [3] z = 1 + the last tombstone, [4]
+// records appended; offsets[i] = where block bf + i's first live record goes.
+__global__ void k_span_init(unsigned long long* sp)
+{
+    if (threadIdx.x == 0) {
+        sp[0] = ~0ull;
+        sp[1] = sp[2] = sp[3] = sp[4] = 0ull;
+    }
+}
+
+// offsets over the span's blocks [bf, bl): the records before the first
+// tombstone keep their places, every block's live records follow the lower
+// blocks' (one workgroup; the span lies in the sweep's window: ~E / 4096
+// blocks)
+__global__ __launch_bounds__(kScanThreads) void k_span_offsets(const uint32_t* dead, uint64_t n,
+                                                               const unsigned long long* sp, uint64_t* offsets)
+{
+    __shared__ uint64_t s_wave[kScanThreads / 64];
+    if (sp[2] == 0) return;
+    const uint64_t bf = sp[0], bl = sp[1];
+    uint64_t run = bf * kCompactChunk;
+    for (uint64_t i0 = 0; i0 < bl - bf; i0 += kScanThreads) {  // workgroup-uniform
+        const uint64_t i = i0 + threadIdx.x, b = bf + i;
+        uint64_t live = 0;
+        if (i < bl - bf) {
+            const uint64_t len = n - b * kCompactChunk < kCompactChunk ? n - b * kCompactChunk : kCompactChunk;
+            live = len - dead[b];
+        }
+        uint64_t tot;
+        const uint64_t pre = block_exclusive_scan<kScanThreads>(live, &tot, s_wave);
+        if (i < bl - bf) offsets[i] = run + pre;
+        run += tot;
+    }
+}
+
+// z over the last block with a tombstone
+__global__ __launch_bounds__(256) void k_span_last(SynArrays a, uint64_t n, unsigned long long* sp)
+{
+    if (sp[2] == 0) return;
+    const uint64_t lb = (sp[1] - 1) * kCompactChunk, count = n - lb < kCompactChunk ? n - lb : kCompactChunk;
+    unsigned long long m = 0;
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < count; k += (uint64_t)gridDim.x * 256)
+        if (src_of(a, lb + k) == kSrcNone) m = lb + k + 1;
+    if (m) atomicMax(sp + 3, m);
+}
+
+// After the compaction: the hole [z - D, z) takes the last D records, or the
+// tail [z, n) shifts down when it is shorter (abnn.h); the tally of the
+// span's blocks is cleared.  A tally that disagrees with the records (z not
+// in the last block, or fewer records than tombstones) is reported (err = 2)
+// and nothing moves.
+__global__ __launch_bounds__(256) void k_span_fill(SynArrays a, uint64_t n, const unsigned long long* sp, uint32_t* dead,
+                                                   uint32_t* err)
+{
+    const uint64_t D = sp[2];
+    if (D == 0) return;
+    const uint64_t bf = sp[0], bl = sp[1], z = sp[3], lb = (bl - 1) * kCompactChunk;
+    if (z <= lb || z > n || z < D) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    const uint64_t f0 = n - z >= D ? n - D : z, count = n - z >= D ? D : n - z, t0 = z - D;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < count; k += stride) {
+        set_src(a, t0 + k, src_of(a, f0 + k));
+        __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(a.dw + f0 + k)),
+                                    reinterpret_cast<uint64_t*>(a.dw + t0 + k));
+    }
+    for (uint64_t b = bf + (uint64_t)blockIdx.x * 256 + threadIdx.x; b < bl; b += stride) dead[b] = 0u;
+}
+
+// The grown records (slots in (pass, slot) order, w = 1: used) appended after
+// the n - D live records while capacity lasts; sp[4] = how many; the slots
+// cleared for the next period.  One workgroup.
+__global__ __launch_bounds__(kScanThreads) void k_append_grown(SynArrays a, uint64_t n, uint64_t cap, uint4* grown,
+                                                               uint64_t slots, unsigned long long* sp,
+                                                               unsigned long long* stats_grown)
+{
+    __shared__ uint64_t s_wave[kScanThreads / 64];
+    const uint64_t live = n - sp[2];
+    uint64_t run = 0;
+    for (uint64_t j0 = 0; j0 < slots; j0 += kScanThreads) {  // workgroup-uniform
+        const uint64_t j = j0 + threadIdx.x;
+        const uint4 g = j < slots ? grown[j] : make_uint4(0u, 0u, 0u, 0u);
+        const bool used = g.w == 1u;
+        uint64_t tot;
+        const uint64_t pre = block_exclusive_scan<kScanThreads>(used ? 1u : 0u, &tot, s_wave);
+        const uint64_t pos = live + run + pre;
+        if (used && pos < cap) {
+            set_src(a, pos, g.x);
+            a.dw[pos] = make_uint2(g.y, g.z);
+        }
+        if (j < slots) grown[j] = make_uint4(0u, 0u, 0u, 0u);
+        run += tot;
+    }
+    if (threadIdx.x == 0) {
+        const uint64_t added = live + run <= cap ? run : cap - live;
+        sp[4] = added;
+        *stats_grown += added;  // abnn_stats.grown (host-kept counter block)
+    }
+}
+
 // The structural update's span (abnn.h contract): out = {first block with a
 // tombstone, last such block + 1, tombstones} from the per-block tally.
 __global__ __launch_bounds__(256) void k_dead_bounds(const uint32_t* dead, uint64_t nb, unsigned long long* out)
@@ -2709,6 +2891,30 @@ hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offs
 {
     if (n == 0 || nblocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_compact, dim3((uint32_t)nblocks), dim3(kCompactThreads), 0, s, syn, n, offsets, dst, b0);
+    return hipGetLastError();
+}
+
+// The structural update's removal and append, all on `s` (sp: 5 device words,
+// see k_span_init): span bounds, offsets, z, the in-place compaction (one
+// workgroup per CU), the hole, the grown records.
+hipError_t launch_structural_update(const SynArrays& syn, uint64_t n, uint64_t cap, uint32_t* dead, uint64_t nb,
+                                    uint64_t* offsets, unsigned long long* sp, uint32_t* flags, uint32_t epoch,
+                                    uint32_t* err, uint32_t cus, uint4* grown, uint64_t slots,
+                                    unsigned long long* stats_grown, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_span_init, dim3(1), dim3(64), 0, s, sp);
+    if (dead && nb && n) {
+        hipLaunchKernelGGL(k_dead_bounds, dim3((uint32_t)std::min<uint64_t>((nb + 255) / 256, 1024)), dim3(256), 0, s,
+                           dead, nb, sp);
+        hipLaunchKernelGGL(k_span_offsets, dim3(1), dim3(kScanThreads), 0, s, dead, n, sp, offsets);
+        hipLaunchKernelGGL(k_span_last, dim3(16), dim3(256), 0, s, syn, n, sp);
+        hipLaunchKernelGGL(k_compact_inplace, dim3(cus), dim3(kCompactThreads), 0, s, syn, n, offsets, sp, flags, epoch,
+                           err);
+        hipLaunchKernelGGL(k_span_fill, dim3(1024), dim3(256), 0, s, syn, n, sp, dead, err);
+    }
+    if (grown && slots)
+        hipLaunchKernelGGL(k_append_grown, dim3(1), dim3(kScanThreads), 0, s, syn, n, cap, grown, slots, sp,
+                           stats_grown);
     return hipGetLastError();
 }
 

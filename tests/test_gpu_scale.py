@@ -161,8 +161,8 @@ def test_c4_eight_virtual_shards_of_the_1b_graph(gpu):
 
 
 def test_c5_4b_records_plasticity(gpu):
-    """Config 5's size on one GPU: 4e9 records (44 GB of packed records, plus
-    the structural update's spare buffer), sweep mode, reward 0.25, pruning
+    """Config 5's size on one GPU: 4e9 records (44 GB of packed records; the
+    structural update compacts in place), sweep mode, reward 0.25, pruning
     and synaptogenesis with a structural update every 10 passes (two inside
     the test).  Every pass: at most max_spikes spikes, one clock tick, n_syn =
     n_syn(before) - pruned + grown across updates, no tombstone left in the
