@@ -275,6 +275,7 @@ def raw_main(args) -> None:
     # pre-gated event (+ 16 B per update and 4 B per spike, not counted: the
     # update/stamp kernels, < 0.1 % of the bytes at config 3)
     survey = 20 * E + 4 * g1
+    traffic, traffic_note = load_traffic("raw_" + wl.name)
     out = {
         "metric": "traversal events/sec at 1B synapses, 5M neurons; achieved HBM GB/s",
         "value": E * args.steps / dt, "unit": "events/s", "n_gpus": 1, "steps": args.steps,
@@ -289,7 +290,12 @@ def raw_main(args) -> None:
                    "host_writes_per_pass": "lastF[inputs] = clock, budget = kMaxSpikes (2 torch kernels)"},
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic.get("bytes_per_launch") if traffic else None,
+            "traffic_source": ("profiles/traffic_raw_%s.json (rocprofv3 PMC of k_raw_gate, FETCH_SIZE x2 + "
+                               "WRITE_SIZE; tag %s, kernel sources %s)" % (wl.name, traffic.get("tag"),
+                                                                           traffic.get("source_sha"))
+                               if traffic else traffic_note),
             "kernel": "k_raw_gate", "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": n_gate.value,
             "launch_ms_source": "HIP event pair around every k_raw_gate launch (abnn_debug_raw_gate_timing)",
             "algorithmic_bytes_per_launch": stream_bytes,

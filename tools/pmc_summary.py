@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh run into committed evidence under profiles/.
+usage: tools/pmc_summary.py OUTDIR TAG CONFIG [KERNEL]   (KERNEL: k_gate)
 
 * profiles/<tag>_kernel_stats.csv  : rocprofv3 --stats output (whole run)
 * profiles/<tag>_steady_state.txt  : per-kernel medians over the last 30 passes
@@ -17,6 +18,9 @@ import shutil
 import statistics
 import sys
 
+# the kernel summarised (argv[4]; k_raw_gate for the reference-layout path)
+KERNEL = sys.argv[4] if len(sys.argv) > 4 else "k_gate"
+
 
 def find(d, pat):
     hits = glob.glob(os.path.join(d, "**", pat), recursive=True)
@@ -28,12 +32,12 @@ def steady(trace_csv, n_last=30):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # a pass runs from one k_gate to the next (k_bitmap, when launched,
     # precedes the gate and is counted with the previous pass)
-    idx = [i for i, r in enumerate(rows) if "k_gate" in r["Kernel_Name"].split("(")[0]]
+    idx = [i for i, r in enumerate(rows) if KERNEL in r["Kernel_Name"].split("(")[0]]
     per = {}
     starts = idx[-n_last:]
     for a in starts:
         j = a
-        while j < len(rows) and (j == a or "k_gate" not in rows[j]["Kernel_Name"].split("(")[0]):
+        while j < len(rows) and (j == a or KERNEL not in rows[j]["Kernel_Name"].split("(")[0]):
             r = rows[j]
             per.setdefault(r["Kernel_Name"].split("(")[0].split("<")[0].split(" ")[-1], []).append(
                 (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
@@ -49,7 +53,7 @@ def pmc_values(d, counter):
         return []
     vals = []
     for r in csv.DictReader(open(f)):
-        if "k_gate" in r.get("Kernel_Name", "").split("(")[0] and r.get("Counter_Name") == counter:
+        if KERNEL in r.get("Kernel_Name", "").split("(")[0] and r.get("Counter_Name") == counter:
             vals.append(float(r["Counter_Value"]))
     return vals
 
@@ -79,8 +83,10 @@ def main():
             steps = json.loads(bj)["steps"]
             rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
             g = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
-                 if "k_gate" in r["Kernel_Name"].split("(")[0]][-2 * steps:-steps]
-            lines.append(f"k_gate mean over the {len(g)} timed launches {statistics.mean(g):.2f} us "
+                 if KERNEL in r["Kernel_Name"].split("(")[0]]
+            # the fused bench samples `steps` more launches after its timed ones; --raw does not
+            g = g[-2 * steps:-steps] if KERNEL == "k_gate" else g[-steps:]
+            lines.append(f"{KERNEL} mean over the {len(g)} timed launches {statistics.mean(g):.2f} us "
                          f"(bench HIP events, span / passes: {json.loads(bj)['roofline']['avg_launch_ms'] * 1e3:.2f} us)")
         except (OSError, IndexError, KeyError, ValueError):
             pass
@@ -91,7 +97,7 @@ def main():
     from abnn_amd.build import kernel_source_sha
 
     # bench.py uses this record only while the kernel sources are these
-    res = {"config": cfg, "tag": tag, "kernel": "k_gate", "source_sha": kernel_source_sha(),
+    res = {"config": cfg, "tag": tag, "kernel": KERNEL, "source_sha": kernel_source_sha(),
            "commit": os.environ.get("ABNN_COMMIT", "")}
     if fetch and write:
         f_kib, w_kib = statistics.median(fetch), statistics.median(write)
@@ -103,7 +109,7 @@ def main():
             "correction": "FETCH_SIZE x2 (gfx950 stream undercount; calibrated for 4-B nt streams in profiles/r01l_fetch_calibration_dword.txt), KiB -> bytes",
             "launches_used": min(len(fetch), len(write)),
         })
-        lines.append(f"k_gate PMC per launch: FETCH_SIZE {f_kib:.0f} KiB (x2 -> {f_kib*2048/1e9:.3f} GB), "
+        lines.append(f"{KERNEL} PMC per launch: FETCH_SIZE {f_kib:.0f} KiB (x2 -> {f_kib*2048/1e9:.3f} GB), "
                      f"WRITE_SIZE {w_kib:.0f} KiB ({w_kib*1024/1e9:.4f} GB)")
         with open(f"profiles/traffic_{cfg}.json", "w") as f:
             json.dump(res, f, indent=1)
