@@ -101,6 +101,7 @@ struct abnn_brain {
     uint64_t* compact_offsets = nullptr;
     uint32_t* compact_flags = nullptr;  // the in-place compaction's per-block read flags (epoch-tagged)
     unsigned long long* span_words = nullptr;  // the update's device words (kernels.hip k_span_init)
+    uint32_t* grown_cnt = nullptr;             // used grown slots per 1024-slot block (k_grown_counts)
     uint32_t compact_epoch = 0;
     uint64_t structural_updates = 0;  // run so far (abnn_structural_updates)
     uint64_t last_pass = ~0ull;       // pass_index of the last pass (its spike list: abnn_get_budget)
@@ -149,7 +150,7 @@ void free_all(abnn_brain* b)
                     b->d.range_info,    b->d.range_g1,  b->d.g2x,
                     b->d.chunk_cnt,
                     b->d.wg_stats, b->d.claim,  b->d.g2src,      b->d.grown,
-                    b->d.dead,      b->compact_offsets, b->compact_flags, b->span_words,
+                    b->d.dead,      b->compact_offsets, b->compact_flags, b->span_words, b->grown_cnt,
                     b->d.work,      b->idx_scratch,
                     b->u64_scratch,  b->d.wave_clock,  b->d.apply_clock, b->d.fired_ring, b->d.n_fired_ring, b->d.range_bounds,  b->d.range_bounds_next, b->d.range_bounds_prev,
                     const_cast<uint32_t*>(b->d.dummy)};
@@ -373,7 +374,7 @@ abnn_status structural_update(abnn_brain* b)
     *b->err_host = 0;
     unsigned long long* sp = b->span_words;
     hipError_t e = launch_structural_update(d.syn, n, cap, d.dead, nb, b->compact_offsets, sp, b->compact_flags,
-                                            b->compact_epoch, d.err_word, (uint32_t)b->cus, d.grown, slots,
+                                            b->compact_epoch, d.err_word, (uint32_t)b->cus, d.grown, slots, b->grown_cnt,
                                             reinterpret_cast<unsigned long long*>(&d.work->stats.grown), nullptr);
     unsigned long long w[5] = {0, 0, 0, 0, 0};
     if (e == hipSuccess) e = hipMemcpy(w, sp, sizeof(w), hipMemcpyDeviceToHost);
@@ -878,6 +879,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (genesis) {
         if ((s = dalloc(&d.g2src, iters * iter_events)) != ABNN_OK) return fail(s);
         if ((s = dalloc(&d.grown, (uint64_t)p.compact_every * p.max_spikes)) != ABNN_OK) return fail(s);
+        if ((s = dalloc(&b->grown_cnt, ((uint64_t)p.compact_every * p.max_spikes + kScanThreads - 1) / kScanThreads + 1)) !=
+            ABNN_OK)
+            return fail(s);
     }
     if ((s = dalloc(&d.work, 1)) != ABNN_OK) return fail(s);
     if (hipHostMalloc(reinterpret_cast<void**>(&b->err_host), 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||

@@ -264,7 +264,7 @@ hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t fir
 // between non-overlapping ranges.
 hipError_t launch_structural_update(const SynArrays& syn, uint64_t n, uint64_t cap, uint32_t* dead, uint64_t nb,
                                     uint64_t* offsets, unsigned long long* sp, uint32_t* flags, uint32_t epoch,
-                                    uint32_t* err, uint32_t cus, uint4* grown, uint64_t slots,
+                                    uint32_t* err, uint32_t cus, uint4* grown, uint64_t slots, uint32_t* grown_cnt,
                                     unsigned long long* stats_grown, hipStream_t s);
 hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offsets, const SynArrays& dst,
                           uint64_t b0, uint64_t nblocks, hipStream_t s);

@@ -2362,6 +2362,12 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact_inplace(SynArrays s
                                                                      const unsigned long long* sp, uint32_t* rd,
                                                                      uint32_t epoch, uint32_t* err)
 {
+    // KB blocks per workgroup and round, all their loads in flight at once:
+    // round i takes blocks [i KB G, (i + 1) KB G), workgroup w the blocks
+    // (i KB + k) G + w.  Every workgroup flags its round's blocks before it
+    // waits, and a block waits only for lower ones (this round's or earlier),
+    // so the rounds cannot deadlock.
+    constexpr int KB = 2;
     __shared__ uint64_t s_wave[kCompactThreads / 64];
     __shared__ uint32_t s_bad;
     const uint32_t lane = threadIdx.x & 63;
@@ -2371,56 +2377,73 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact_inplace(SynArrays s
     const uint64_t b0 = sp[0], D = sp[2], z = sp[3], lb = D ? (sp[1] - 1) * kCompactChunk : 0u;
     // (a tally that disagrees with the records moves nothing: k_span_fill reports it)
     const uint64_t nblk = D && z > lb && z <= n && z >= D ? sp[1] - sp[0] : 0u;
-    for (uint64_t c = blockIdx.x; c < nblk; c += gridDim.x) {  // workgroup-uniform
-        const uint64_t base = (b0 + c) * kCompactChunk;
-        uint32_t rs[4];
-        uint64_t rdw[4];
+    const uint64_t G = gridDim.x;
+    for (uint64_t r0 = 0; r0 < nblk; r0 += KB * G) {  // workgroup-uniform
+        uint32_t rs[KB][4];
+        uint64_t rdw[KB][4], o0[KB];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint64_t i = base + (uint64_t)j * kCompactThreads + threadIdx.x;
-            const bool in = i < z;  // z <= n
-            rs[j] = in ? src_of(syn, i) : kSrcNone;
-            rdw[j] = in ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(syn.dw + i)) : 0ull;
+        for (int k = 0; k < KB; ++k) {
+            const uint64_t c = r0 + k * G + blockIdx.x;
+            const uint64_t base = (b0 + c) * kCompactChunk;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t i = base + (uint64_t)j * kCompactThreads + threadIdx.x;
+                const bool in = c < nblk && i < z;  // z <= n
+                rs[k][j] = in ? src_of(syn, i) : kSrcNone;
+                rdw[k][j] = in ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(syn.dw + i)) : 0ull;
+            }
+            o0[k] = c < nblk ? offsets[c] : 0u;
         }
-        const uint64_t o0 = offsets[c];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's records are in registers
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's records are in registers
         __syncthreads();
-        if (threadIdx.x == 0) {
-            s_bad = 0u;
-            __hip_atomic_store(rd + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x < KB) {
+            const uint64_t c = r0 + threadIdx.x * G + blockIdx.x;
+            if (c < nblk) __hip_atomic_store(rd + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        // the blocks this one writes into, below it, must have read theirs
-        const uint64_t c_lo = o0 / kCompactChunk - b0;  // o0 >= b0 * kCompactChunk
-        if (threadIdx.x < 64 && c_lo < c) {
-            for (uint64_t j0 = c_lo; j0 < c; j0 += 64) {  // wave-uniform
-                const uint64_t j = j0 + lane;
-                for (uint32_t spins = 0;; ++spins) {
-                    const bool ok = j >= c || __hip_atomic_load(rd + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-                    if (__ballot(!ok) == 0) break;
-                    if (spins >= kLbSpinLimit) {
-                        if (lane == 0) {
-                            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            s_bad = 1u;
+        if (threadIdx.x == 0) s_bad = 0u;
+        // the blocks each one writes into, below it, must have read theirs
+        if (threadIdx.x < 64) {
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+                const uint64_t c = r0 + k * G + blockIdx.x;
+                if (c >= nblk) break;
+                const uint64_t c_lo = o0[k] / kCompactChunk - b0;  // o0 >= b0 * kCompactChunk
+                for (uint64_t j0 = c_lo; j0 < c; j0 += 64) {       // wave-uniform
+                    const uint64_t jj = j0 + lane;
+                    for (uint32_t spins = 0;; ++spins) {
+                        const bool ok =
+                            jj >= c || __hip_atomic_load(rd + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+                        if (__ballot(!ok) == 0) break;
+                        if (spins >= kLbSpinLimit) {
+                            if (lane == 0) {
+                                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                s_bad = 1u;
+                            }
+                            break;
                         }
-                        break;
+                        __builtin_amdgcn_s_sleep(2);
                     }
-                    __builtin_amdgcn_s_sleep(2);
                 }
             }
         }
         __syncthreads();
         if (s_bad) continue;  // (reported: the records are then not trusted)
-        uint64_t o = o0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const bool live = rs[j] != kSrcNone;
-            uint64_t tot;
-            const uint64_t pre = block_exclusive_scan(live ? 1u : 0u, &tot, s_wave);
-            if (live) {
-                set_src(syn, o + pre, rs[j]);
-                __builtin_nontemporal_store(rdw[j], reinterpret_cast<uint64_t*>(syn.dw + o + pre));
+        for (int k = 0; k < KB; ++k) {
+            if (r0 + k * G + blockIdx.x >= nblk) break;  // workgroup-uniform
+            uint64_t o = o0[k];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool live = rs[k][j] != kSrcNone;
+                uint64_t tot;
+                // (LDS-only barriers: the stores stay in flight)
+                const uint64_t pre = block_exclusive_scan<kCompactThreads, true>(live ? 1u : 0u, &tot, s_wave);
+                if (live) {
+                    set_src(syn, o + pre, rs[k][j]);
+                    __builtin_nontemporal_store(rdw[k][j], reinterpret_cast<uint64_t*>(syn.dw + o + pre));
+                }
+                o += tot;
             }
-            o += tot;
         }
     }
 }
@@ -2501,30 +2524,38 @@ __global__ __launch_bounds__(256) void k_span_fill(SynArrays a, uint64_t n, cons
 
 // The grown records (slots in (pass, slot) order, w = 1: used) appended after
 // the n - D live records while capacity lasts; sp[4] = how many; the slots
-// cleared for the next period.  One workgroup.
+// cleared for the next period.  Two launches over 1024-slot blocks: the used
+// count of each, then each block's records at the lower blocks' count.
+__global__ __launch_bounds__(kScanThreads) void k_grown_counts(const uint4* grown, uint64_t slots, uint32_t* cnt)
+{
+    __shared__ uint64_t s_wave[kScanThreads / 64];
+    const uint64_t j = (uint64_t)blockIdx.x * kScanThreads + threadIdx.x;
+    const uint64_t c = block_sum<kScanThreads>(j < slots && grown[j].w == 1u ? 1u : 0u, s_wave);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = (uint32_t)c;
+}
+
 __global__ __launch_bounds__(kScanThreads) void k_append_grown(SynArrays a, uint64_t n, uint64_t cap, uint4* grown,
-                                                               uint64_t slots, unsigned long long* sp,
-                                                               unsigned long long* stats_grown)
+                                                               uint64_t slots, const uint32_t* cnt,
+                                                               unsigned long long* sp, unsigned long long* stats_grown)
 {
     __shared__ uint64_t s_wave[kScanThreads / 64];
     const uint64_t live = n - sp[2];
-    uint64_t run = 0;
-    for (uint64_t j0 = 0; j0 < slots; j0 += kScanThreads) {  // workgroup-uniform
-        const uint64_t j = j0 + threadIdx.x;
-        const uint4 g = j < slots ? grown[j] : make_uint4(0u, 0u, 0u, 0u);
-        const bool used = g.w == 1u;
-        uint64_t tot;
-        const uint64_t pre = block_exclusive_scan<kScanThreads>(used ? 1u : 0u, &tot, s_wave);
-        const uint64_t pos = live + run + pre;
-        if (used && pos < cap) {
-            set_src(a, pos, g.x);
-            a.dw[pos] = make_uint2(g.y, g.z);
-        }
-        if (j < slots) grown[j] = make_uint4(0u, 0u, 0u, 0u);
-        run += tot;
+    uint64_t below = 0;  // used slots in the lower blocks
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kScanThreads) below += cnt[b];
+    below = block_sum<kScanThreads>(below, s_wave);
+    const uint64_t j = (uint64_t)blockIdx.x * kScanThreads + threadIdx.x;
+    const uint4 g = j < slots ? grown[j] : make_uint4(0u, 0u, 0u, 0u);
+    const bool used = g.w == 1u;
+    uint64_t tot;
+    const uint64_t pre = block_exclusive_scan<kScanThreads>(used ? 1u : 0u, &tot, s_wave);
+    const uint64_t pos = live + below + pre;
+    if (used && pos < cap) {
+        set_src(a, pos, g.x);
+        a.dw[pos] = make_uint2(g.y, g.z);
     }
-    if (threadIdx.x == 0) {
-        const uint64_t added = live + run <= cap ? run : cap - live;
+    if (j < slots) grown[j] = make_uint4(0u, 0u, 0u, 0u);
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the last block knows the total
+        const uint64_t run = below + tot, added = live + run <= cap ? run : cap - live;
         sp[4] = added;
         *stats_grown += added;  // abnn_stats.grown (host-kept counter block)
     }
@@ -2899,7 +2930,7 @@ hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offs
 // workgroup per CU), the hole, the grown records.
 hipError_t launch_structural_update(const SynArrays& syn, uint64_t n, uint64_t cap, uint32_t* dead, uint64_t nb,
                                     uint64_t* offsets, unsigned long long* sp, uint32_t* flags, uint32_t epoch,
-                                    uint32_t* err, uint32_t cus, uint4* grown, uint64_t slots,
+                                    uint32_t* err, uint32_t cus, uint4* grown, uint64_t slots, uint32_t* grown_cnt,
                                     unsigned long long* stats_grown, hipStream_t s)
 {
     hipLaunchKernelGGL(k_span_init, dim3(1), dim3(64), 0, s, sp);
@@ -2912,9 +2943,12 @@ hipError_t launch_structural_update(const SynArrays& syn, uint64_t n, uint64_t c
                            err);
         hipLaunchKernelGGL(k_span_fill, dim3(1024), dim3(256), 0, s, syn, n, sp, dead, err);
     }
-    if (grown && slots)
-        hipLaunchKernelGGL(k_append_grown, dim3(1), dim3(kScanThreads), 0, s, syn, n, cap, grown, slots, sp,
+    if (grown && slots) {
+        const uint32_t gb = (uint32_t)((slots + kScanThreads - 1) / kScanThreads);
+        hipLaunchKernelGGL(k_grown_counts, dim3(gb), dim3(kScanThreads), 0, s, grown, slots, grown_cnt);
+        hipLaunchKernelGGL(k_append_grown, dim3(gb), dim3(kScanThreads), 0, s, syn, n, cap, grown, slots, grown_cnt, sp,
                            stats_grown);
+    }
     return hipGetLastError();
 }
 
