@@ -66,6 +66,7 @@ constexpr uint32_t kRawD = 4;                        // iterations per group = b
 constexpr uint32_t kRawGroup = kRawIt * kRawD;       // 1024 events: the scan / apply unit
 constexpr uint32_t kRawChunk = 256;                  // survivor entries (16 B) per pool chunk
 constexpr uint32_t kRawStage = 256;                  // staged hits per wave (flush above 192)
+constexpr uint32_t kRawOpen = 32;                    // groups whose hits may wait in the stage (gate)
 constexpr uint32_t kRawFB = 8192;                    // filter blocks (64 KiB of LDS)
 constexpr uint32_t kRawFLg = 13;
 constexpr uint32_t kRawSpikeCap = 65536;             // spike list entries (deferred stamps)
@@ -269,6 +270,8 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_gate(const uint4* __restrict_
     constexpr uint32_t NW = kRawBlock / 64;
     __shared__ uint2 s_fb[kRawFB];
     __shared__ uint4 s_st[NW][kRawStage];  // staged hits {event, src, dst, w}
+    __shared__ uint4 s_og[NW][kRawOpen];   // pending groups {group, first stage entry, survivors, candidates}
+    __shared__ uint32_t s_oseq[NW][kRawOpen];  // ... their first survivor's place in the wave's sequence
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = wave_uniform(tid >> 6);
     // the filter global -> LDS (LDS-DMA) before the first records are requested
 #pragma unroll
@@ -303,44 +306,67 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_gate(const uint4* __restrict_
     uint32_t lim = kRawNone;    // sequence entries stored (kRawNone: all so far)
     uint32_t n_g1 = 0;          // pre-gated events of this wave (diagnostics)
     const uint32_t window = kp.window_pre, refr = kp.refractory;
-    for (uint32_t g = v; g < NG; g += W) {  // wave-uniform
-        uint32_t pend = 0, S = 0, C = 0;
-        const uint32_t seq0 = seq;
-        // the staged hits through the gates; survivors appended to the sequence
-        auto flush = [&]() {
-            constexpr uint32_t RR = kRawStage / 64;
-            uint4 e[RR];
-            uint32_t a[RR], b[RR];
+    // The staged hits go through the gates only when the stage fills or
+    // kRawOpen groups with hits are pending (round 3 did it at the end of every
+    // group: its lastF round trip was issued behind the next group's record
+    // loads, and vmcnt retires in order, so each wave drained its whole
+    // pipeline once per 1024 events -- 13 % of the gate's time).  Per pending
+    // group (in this wave's LDS): {group, first stage entry, survivors so far,
+    // candidates so far} and its first survivor's place in the sequence.
+    uint4* og = s_og[wid];
+    uint32_t* oseq = s_oseq[wid];
+    uint32_t nopen = 0;   // pending groups (the last may be the current one)
+    bool cur_open = false;  // the current group is the last pending one
+    uint32_t pend = 0;
+    // ginfo of a finished group: where its survivors are
+    auto write_ginfo = [&](uint32_t g, uint32_t S, uint32_t C, uint32_t seq0) {
+        if (lane == 0) {
+            uint32_t ia = kRawNone, ib = kRawNone;
+            if (S) {
+                const uint32_t c0 = seq0 / kRawChunk;
+                if (lim != kRawNone && seq0 + S > lim) ia = kRawRedo;
+                else if (c0 + 1 == have) ia = cur;  // every survivor in the last chunk
+                else if (c0 + 2 == have) { ia = prev; ib = cur; }
+                else ia = kRawCtab;
+            }
+            ws.gcand[g] = C;
+            ws.ginfo[g] = make_uint4(S, seq0, ia, ib);
+        }
+    };
+    // every staged hit through the gates; survivors appended to the sequence
+    // and counted to their groups; the finished groups' ginfo written (keep:
+    // the current group stays pending, its next hits staged from entry 0)
+    auto flush = [&](bool keep_current) {
+        constexpr uint32_t RR = kRawStage / 64;
+        uint4 e[RR];
+        uint32_t a[RR], b[RR];
 #pragma unroll
-            for (uint32_t r = 0; r < RR; ++r) {
-                const uint32_t q = r * 64 + lane;
-                e[r] = q < pend ? st[q] : make_uint4(0u, kRawNone, kRawNone, 0u);
-                const bool ok = e[r].y < n_nrn && e[r].z < n_nrn;
-                a[r] = ok ? lastF[e[r].y] : now;  // brain.metal:73 (exact, for the filter's hits)
-                b[r] = ok ? lastF[e[r].z] : now;  // brain.metal:79, in the same round trip
-            }
-            uint64_t m2[RR], mc[RR];
-            uint32_t n = 0;
+        for (uint32_t r = 0; r < RR; ++r) {
+            const uint32_t q = r * 64 + lane;
+            e[r] = q < pend ? st[q] : make_uint4(0u, kRawNone, kRawNone, 0u);
+            const bool ok = e[r].y < n_nrn && e[r].z < n_nrn;
+            a[r] = ok ? lastF[e[r].y] : now;  // brain.metal:73 (exact, for the filter's hits)
+            b[r] = ok ? lastF[e[r].z] : now;  // brain.metal:79, in the same round trip
+        }
+        uint64_t m2[RR], mc[RR];
+        uint32_t n = 0;
 #pragma unroll
-            for (uint32_t r = 0; r < RR; ++r) {
-                const bool ok = e[r].y < n_nrn && e[r].z < n_nrn;
-                const bool g1 = ok && now - a[r] <= window;          // brain.metal:73-77
-                const bool g2 = g1 && now - b[r] > refr;             // brain.metal:79-83
-                const bool cand = g2 && spike_candidate(kp, __uint_as_float(e[r].w), e[r].x, now);  // brain.metal:91-92
-                m2[r] = __ballot(g2);
-                mc[r] = __ballot(cand);
-                n_g1 += (uint32_t)__popcll(__ballot(g1));
-                if (g2 && e[r].x == 0u) ws.hdr->t0 = 1u;             // event 0 reached the budget test (brain.metal:110)
-                e[r] = make_uint4(e[r].x, __float_as_uint((float)(now - b[r])) | (cand ? 0x80000000u : 0u), e[r].w,
-                                  e[r].z);
-                n += (uint32_t)__popcll(m2[r]);
-                C += (uint32_t)__popcll(mc[r]);
-            }
-            if (n == 0) {
-                pend = 0;
-                return;
-            }
-            // chunks for entries [seq, seq + n): at most two new ones
+        for (uint32_t r = 0; r < RR; ++r) {
+            const bool ok = e[r].y < n_nrn && e[r].z < n_nrn;
+            const bool g1 = ok && now - a[r] <= window;          // brain.metal:73-77
+            const bool g2 = g1 && now - b[r] > refr;             // brain.metal:79-83
+            const bool cand = g2 && spike_candidate(kp, __uint_as_float(e[r].w), e[r].x, now);  // brain.metal:91-92
+            m2[r] = __ballot(g2);
+            mc[r] = __ballot(cand);
+            n_g1 += (uint32_t)__popcll(__ballot(g1));
+            if (g2 && e[r].x == 0u) ws.hdr->t0 = 1u;             // event 0 reached the budget test (brain.metal:110)
+            e[r] = make_uint4(e[r].x, __float_as_uint((float)(now - b[r])) | (cand ? 0x80000000u : 0u), e[r].w,
+                              e[r].z);
+            n += (uint32_t)__popcll(m2[r]);
+        }
+        const uint32_t seq_before = seq;
+        if (n) {
+            // chunks for entries [seq, seq + n)
             if (lim == kRawNone) {
                 while (have * kRawChunk < seq + n) {  // wave-uniform
                     uint32_t id = 0;
@@ -362,15 +388,51 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_gate(const uint4* __restrict_
             for (uint32_t r = 0; r < RR; ++r) {
                 const uint32_t x = o + mbcnt64(m2[r]);
                 if (((m2[r] >> lane) & 1u) && (lim == kRawNone || x < lim)) {
-                    const uint32_t c = x / kRawChunk, id = c == have - 1 ? cur : prev;
+                    const uint32_t c = x / kRawChunk;
+                    const uint32_t id = c + 1 == have ? cur
+                                      : c + 2 == have ? prev
+                                                      : ws.ctab[(uint64_t)v * ws.maxc + c];
                     ws.pool[(uint64_t)id * kRawChunk + (x % kRawChunk)] = e[r];
                 }
                 o += (uint32_t)__popcll(m2[r]);
             }
             seq += n;
-            S += n;
-            pend = 0;
+        }
+        // the pending groups' shares (stage entries [st0_j, st0_j+1) are group j's)
+        auto range_mask = [](uint32_t lo, uint32_t hi, uint32_t r) -> uint64_t {  // lanes q in [lo, hi) of round r
+            const uint32_t b0 = r * 64;
+            const uint32_t l = lo > b0 ? (lo - b0 < 64 ? lo - b0 : 64) : 0, h = hi > b0 ? (hi - b0 < 64 ? hi - b0 : 64) : 0;
+            const uint64_t mh = h >= 64 ? ~0ull : ((1ull << h) - 1), ml = l >= 64 ? ~0ull : ((1ull << l) - 1);
+            return mh & ~ml;
         };
+        uint32_t kept = 0;
+        for (uint32_t j = 0; j < nopen; ++j) {  // wave-uniform
+            uint4 oj = og[j];  // {group, first entry, survivors, candidates}
+            const uint32_t hi = j + 1 < nopen ? og[j + 1].y : pend;
+            uint32_t sj = 0, cj = 0, before = 0;
+#pragma unroll
+            for (uint32_t r = 0; r < RR; ++r) {
+                const uint64_t m = range_mask(oj.y, hi, r);
+                sj += (uint32_t)__popcll(m2[r] & m);
+                cj += (uint32_t)__popcll(mc[r] & m);
+                before += (uint32_t)__popcll(m2[r] & range_mask(0, oj.y, r));
+            }
+            if (oj.z == 0 && sj) oseq[j] = seq_before + before;  // its first survivor's place
+            oj.z += sj;
+            oj.w += cj;
+            if (keep_current && cur_open && j + 1 == nopen) {  // the current group stays pending
+                og[0] = make_uint4(oj.x, 0u, oj.z, oj.w);
+                oseq[0] = oseq[j];
+                kept = 1;
+            } else {
+                write_ginfo(oj.x, oj.z, oj.w, oj.z ? oseq[j] : seq);
+            }
+        }
+        nopen = kept;
+        cur_open = kept != 0;
+        pend = 0;
+    };
+    for (uint32_t g = v; g < NG; g += W) {  // wave-uniform
 #pragma unroll
         for (uint32_t d = 0; d < kRawD; ++d) {
             uint32_t src[kRawK];
@@ -387,27 +449,32 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_gate(const uint4* __restrict_
                 const bool h = raw_filter_pass(s_fb, src[k]);
                 const uint64_t bm = __ballot(h);
                 if (bm == 0) continue;  // wave-uniform
+                if (!cur_open) {  // the group's first staged hit: it becomes pending
+                    if (lane == 0) {
+                        og[nopen] = make_uint4(g, pend, 0u, 0u);
+                        oseq[nopen] = 0u;
+                    }
+                    ++nopen;
+                    cur_open = true;
+                }
                 if (h) st[pend + mbcnt64(bm)] = make_uint4(rel + k * 64 + lane, rc[k].x, rc[k].y, rc[k].z);
                 pend += (uint32_t)__popcll(bm);
-                if (pend > kRawStage - 64) flush();
+                if (pend > kRawStage - 64) flush(true);
             }
         }
-        if (pend) flush();
-        if (lane == 0) {
-            // where the group's survivors are: the chunk of entry seq0 and the
-            // next one (a group's <= 256 survivors span at most two)
-            uint32_t ia = kRawNone, ib = kRawNone;
-            if (S) {
-                const uint32_t c0 = seq0 / kRawChunk, c1 = (seq0 + S - 1) / kRawChunk;
-                if (lim != kRawNone && seq0 + S > lim) ia = kRawRedo;
-                else if (c1 == c0) ia = cur;  // c1 = have - 1
-                else if (c1 == c0 + 1) { ia = prev; ib = cur; }
-                else ia = kRawCtab;
-            }
-            ws.gcand[g] = C;
-            ws.ginfo[g] = make_uint4(S, seq0, ia, ib);
+        // the group is done: without a pending share, its ginfo now (its
+        // survivors, if a flush inside it kept any, are all counted)
+        if (cur_open && nopen == 1 && pend == 0) {  // (a flush inside it took every hit: og[0] is it)
+            const uint4 oj = og[0];
+            write_ginfo(oj.x, oj.z, oj.w, oj.z ? oseq[0] : seq);
+            nopen = 0;
+        } else if (!cur_open) {
+            write_ginfo(g, 0u, 0u, seq);
         }
+        cur_open = false;
+        if (nopen >= kRawOpen) flush(false);
     }
+    if (nopen) flush(false);
     if (lane == 0) {
         ws.wlim[v] = lim;
         ws.wstat[v] = make_uint2(n_g1, seq);
