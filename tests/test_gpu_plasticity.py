@@ -137,3 +137,33 @@ def test_plasticity_virtual_shards_vs_oracle_shards(gpu):
     for g, o in pairs:
         _same(g, o, "shard")
         assert g.stats() == o.stats()
+
+
+@pytest.mark.parametrize("pattern", ["spread", "dense_block", "tail_short", "almost_all"])
+def test_structural_update_in_place_patterns(gpu, pattern):
+    """The device-driven structural update (kernels.hip launch_structural_update:
+    span offsets, the in-place compaction with per-block read flags, the
+    hole's fill) on uploaded tombstone patterns the passes' pruning does not
+    produce -- tombstones everywhere incl. the first and last record, a dense
+    run of 50k (live records move 12 blocks down: a block waits on many
+    lower ones), tombstones near the end (the tail shorter than D shifts
+    down), and all but every 1000th record -- against the oracle's restatement
+    of the contract (abnn.h), records and count after each update."""
+    kw = dict(w_prune=1e-30, p_new=0.0, compact_every=1)  # the passes prune nothing; the update removes the uploads'
+    g, o = _pair(0, **kw)
+    syn = g.download_synapses()
+    n = len(syn)
+    idx = np.arange(n)
+    dead = {"spread": (idx % 7 == 3) | (idx == 0) | (idx == n - 1),
+            "dense_block": (idx >= 10_000) & (idx < 60_000) | (idx % 97 == 5),
+            "tail_short": (idx >= 100_000) & (idx < 118_000),
+            "almost_all": idx % 1000 != 17}[pattern]
+    syn["src"][dead] = 0xFFFFFFFF
+    syn["dst"][dead] = 0xFFFFFFFF
+    g.upload_synapses(syn)
+    o.set_synapses(syn)
+    for k in range(2):
+        g.encode_traversal(1)
+        o.pass_serial()
+        _same(g, o, f"{pattern} pass {k}")
+    assert g.n_syn() <= n - int(dead.sum())
