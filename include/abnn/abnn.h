@@ -147,9 +147,11 @@ typedef struct abnn_params {
  *     the tail shifts down by D (O(z - a + D) records move; a sweep prunes
  *     only inside its visited window, so the update costs O(events), not
  *     O(n_syn)); then the synapses grown since the previous update are
- *     appended in (pass, slot) order while n_syn < syn_capacity.  n_syn, the visited events and
- *     the borrowed synapse pointer (abnn_state_ptrs) change here.  Sweep-mode
- *     event ids stay syn_offset + local index (syn_offset is fixed). */
+ *     appended in (pass, slot) order while n_syn < syn_capacity.  n_syn and
+ *     the visited events change here; the records are compacted in place (no
+ *     second buffer), so the borrowed synapse pointer (abnn_state_ptrs) stays
+ *     valid.  Sweep-mode event ids stay syn_offset + local index (syn_offset
+ *     is fixed). */
 #define ABNN_GENESIS_KEY 0xA24BAED4963EE407ull
 
 /* Random-edge mode (README §4 "pick a random synapse"; no reference code, so
