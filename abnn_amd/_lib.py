@@ -70,7 +70,7 @@ class Scalars(C.Structure):
 
 
 MODE_SWEEP, MODE_RANDOM = 0, 1  # abnn_params.mode (include/abnn/abnn.h)
-ABI_VERSION = 8
+ABI_VERSION = 9
 LAYOUT_VERSION = 3
 
 
@@ -173,6 +173,9 @@ SIGNATURES = [
     ("abnn_shard_commit", C.c_int, [_VP, _VP, _U32, _VP]),
     ("abnn_get_budget", C.c_int, [_VP, _PU32]),
     ("abnn_structural_updates", C.c_uint64, [_VP]),
+    ("abnn_shard_visits_delta", C.c_int, [_VP, _VP, _VP]),
+    ("abnn_shard_visits_merge", C.c_int, [_VP, _VP, _VP]),
+    ("abnn_renormalisations", C.c_uint64, [_VP]),
     ("abnn_traversal_workspace_bytes", C.c_uint64, [_U32, _U32]),
     ("abnn_traversal_workspace_min_bytes", C.c_uint64, [_U32, _U32]),
     ("abnn_traversal_workspace_error", C.c_int, [_VP, _PU32, _VP]),
@@ -219,6 +222,7 @@ DEBUG_SIGNATURES = [
     ("abnn_debug_raw_stats", C.c_int, [_VP, C.POINTER(C.c_uint64), _VP]),
     ("abnn_debug_raw_gate_timing", C.c_int, [C.c_int]),
     ("abnn_debug_raw_gate_time", C.c_int, [C.POINTER(C.c_double), _PU32]),
+    ("abnn_debug_set_compact_spin_limit", C.c_int, [_VP, _U32]),
 ]
 
 

@@ -134,6 +134,10 @@ class Brain:
         """Structural updates run so far (host count, no synchronisation)."""
         return int(self._lib.abnn_structural_updates(self._h))
 
+    def renormalisations(self) -> int:
+        """Renormalisations run so far (host count, no synchronisation)."""
+        return int(self._lib.abnn_renormalisations(self._h))
+
     # ---- synapses ------------------------------------------------------------------------------
     def upload_synapses(self, syn: np.ndarray, first: int = 0) -> None:
         syn = np.ascontiguousarray(syn, dtype=SYN_DTYPE)
@@ -235,6 +239,14 @@ class Brain:
 
     def shard_commit(self, gathered_ptr: int, world: int, stream=None) -> None:
         call("abnn_shard_commit", self._h, gathered_ptr, world, _stream_ptr(stream))
+
+    def shard_visits_delta(self, delta_ptr: int, stream=None) -> None:
+        """This shard's lastVisited merge deltas (u64 x N_NRN, device; abnn.h)."""
+        call("abnn_shard_visits_delta", self._h, delta_ptr, _stream_ptr(stream))
+
+    def shard_visits_merge(self, reduced_ptr: int, stream=None) -> None:
+        """Apply the all-reduced (MAX) deltas; clears this shard's visit marks."""
+        call("abnn_shard_visits_merge", self._h, reduced_ptr, _stream_ptr(stream))
 
     # ---- statistics / timing ------------------------------------------------------------------
     def stats(self) -> dict:

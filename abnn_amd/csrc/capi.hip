@@ -111,6 +111,17 @@ struct abnn_brain {
     // a sharded pass on the fused path: its first launch (k_gate in shard
     // mode) ran, k_shard_walk follows the exchange (abnn_shard_apply)
     bool pending_walk = false;
+    // the sharded lastVisited merge: a track_visits shard marks
+    // the neurons it visits (d.visit_mark); marks_dirty = a pass ran since the
+    // last merge or host write of lastVisited
+    bool marks_dirty = false;
+    uint64_t renorms = 0;  // renormalisations run (abnn_renormalisations)
+    // a structural update that failed part-way left the records invalid (the
+    // compaction works in place): every pass is refused until they are
+    // reloaded (abnn_load_bnn / abnn_load_flat / abnn_generate_synapses / an
+    // upload of every record)
+    bool records_invalid = false;
+    uint32_t compact_spin_limit = kLbSpinLimit;  // abnn_debug_set_compact_spin_limit
 };
 
 namespace {
@@ -144,7 +155,7 @@ void free_all(abnn_brain* b)
     if (!b) return;
     (void)hipSetDevice(b->device);
     void* ptrs[] = {b->d.syn.lo,    b->d.syn.hi,     b->d.syn.dw,     b->d.syn.src32,
-                    b->d.last_fired, b->d.last_visited,  b->scalar_block,
+                    b->d.last_fired, b->d.last_visited, b->d.visit_mark, b->scalar_block,
                     b->bitmap_buf[0], b->bitmap_buf[1], b->bitmap_buf[2], b->filter_buf[0], b->filter_buf[1],
                     b->filter_buf[2], b->cost_buf[0], b->cost_buf[1], b->d.lb_status, b->d.cand_list,
                     b->d.range_info,    b->d.range_g1,  b->d.g2x,
@@ -298,6 +309,19 @@ uint64_t tick_events(const abnn_brain* b)
 // reference's clock is a u32, so the test is on its low 32 bits
 bool renorm_due(const abnn_brain* b) { return (uint64_t)(uint32_t)b->clock_host > b->params.renorm_thresh; }
 
+constexpr const char* kRecordsInvalid =
+    "a failed structural update left the records invalid: reload them (abnn_load_bnn / abnn_load_flat / "
+    "abnn_generate_synapses / abnn_upload_synapses of every record) before the next pass";
+
+// A shard that tracks visits keeps per-neuron visit marks for the lastVisited
+// merge; allocated at creation when global_events is set, else
+// by the first sharded pass (zeros: nothing visited yet).
+abnn_status ensure_visit_marks(abnn_brain* b)
+{
+    if (!b->params.track_visits || b->d.visit_mark) return ABNN_OK;
+    return dalloc(&b->d.visit_mark, b->n_nrn);
+}
+
 void host_tick(abnn_brain* b)
 {
     if (tick_events(b) > 0) b->clock_host += b->params.clock_inc;  // brain.metal:129
@@ -374,19 +398,27 @@ abnn_status structural_update(abnn_brain* b)
     *b->err_host = 0;
     unsigned long long* sp = b->span_words;
     hipError_t e = launch_structural_update(d.syn, n, cap, d.dead, nb, b->compact_offsets, sp, b->compact_flags,
-                                            b->compact_epoch, d.err_word, (uint32_t)b->cus, d.grown, slots, b->grown_cnt,
+                                            b->compact_epoch, d.err_word, b->compact_spin_limit, (uint32_t)b->cus, d.grown,
+                                            slots, b->grown_cnt,
                                             reinterpret_cast<unsigned long long*>(&d.work->stats.grown), nullptr);
     unsigned long long w[5] = {0, 0, 0, 0, 0};
     if (e == hipSuccess) e = hipMemcpy(w, sp, sizeof(w), hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
-        set_err(std::string("structural update: ") + hipGetErrorString(e));
+        b->records_invalid = true;  // the update may have stopped part-way through its in-place moves
+        set_err(std::string("structural update: ") + hipGetErrorString(e) +
+                "; the records are not valid, reload them (abnn_load_bnn / abnn_load_flat)");
         return ABNN_ERR_HIP;
     }
     if (const uint32_t err = *b->err_host) {
+        // the compaction moves records in place, so a part-done update cannot
+        // be rolled back: passes are refused until the records are reloaded
         *b->err_host = 0;
-        set_err(err == 2 ? "structural update: the tombstone tally and the records disagree"
-                         : "structural update: the in-place compaction's wait timed out; the records are not valid");
+        b->records_invalid = true;
+        set_err(err == 2 ? "structural update: the tombstone tally and the records disagree; "
+                           "the records are not valid, reload them (abnn_load_bnn / abnn_load_flat)"
+                         : "structural update: the in-place compaction's wait timed out; "
+                           "the records are not valid, reload them (abnn_load_bnn / abnn_load_flat)");
         return ABNN_ERR_HIP;
     }
     b->dims.n_syn = n - w[2] + w[4];
@@ -597,6 +629,7 @@ abnn_status run_commit(abnn_brain* b, const int32_t* gathered, uint32_t world, b
     b->clean_passes += 1;
     if (renorm) {  // renormalise_if_needed, brain.cpp:125-141; kernel brain.metal:135-145
         HIP_TRY(launch_renorm(b->d, b->clock_host, s));
+        b->renorms += 1;
         const uint64_t base = b->clock_host;
         b->max_host_stamp = b->max_host_stamp > base ? b->max_host_stamp - base : 0;
         b->clean_passes = 0;  // the clock jumps back
@@ -830,6 +863,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if ((s = alloc_syn(&d.syn, cap + kDummyRecords, p.mode == ABNN_MODE_RANDOM)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_fired, n_nrn)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.last_visited, n_nrn)) != ABNN_OK) return fail(s);
+    // a shard (global_events set) that tracks visits marks them for the merge
+    if (p.track_visits && dims->global_events && (s = dalloc(&d.visit_mark, n_nrn)) != ABNN_OK) return fail(s);
     uint64_t* sb = nullptr;
     if ((s = dalloc(&sb, 3)) != ABNN_OK) return fail(s);  // {clock, reward|rbar, pass_index}
     b->scalar_block = sb;
@@ -984,6 +1019,8 @@ abnn_status abnn_get_budget(abnn_brain* b, uint32_t* remaining)
 
 uint64_t abnn_structural_updates(const abnn_brain* b) { return b ? b->structural_updates : 0; }
 
+uint64_t abnn_renormalisations(const abnn_brain* b) { return b ? b->renorms : 0; }
+
 abnn_status abnn_upload_synapses(abnn_brain* b, uint64_t first, const abnn_synapse* src, uint64_t n)
 {
     REQUIRE(b && (src || n == 0), "null argument");
@@ -991,6 +1028,7 @@ abnn_status abnn_upload_synapses(abnn_brain* b, uint64_t first, const abnn_synap
     ST_TRY(validate_records(b, src, n));
     ST_TRY(sync_all(b));
     ST_TRY(records_h2d(b->d.syn, first, n, src));
+    if (first == 0 && n == b->dims.n_syn) b->records_invalid = false;  // every record rewritten
     return retally(b, first, n);
 }
 
@@ -1013,7 +1051,8 @@ abnn_status abnn_generate_synapses(abnn_brain* b, uint64_t seed)
     ST_TRY(sync_all(b));
     HIP_TRY(launch_generate(b->d, b->dims.n_input, b->dims.n_output, seed, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
-    return ABNN_OK;
+    b->records_invalid = false;
+    return retally(b, 0, b->dims.n_syn);
 }
 
 abnn_status abnn_checksum_synapses(abnn_brain* b, uint64_t* out)
@@ -1060,6 +1099,9 @@ abnn_status abnn_set_last_visited(abnn_brain* b, uint64_t first, const uint64_t*
     REQUIRE(first <= b->n_nrn && n <= b->n_nrn - first, "range out of bounds");
     ST_TRY(sync_all(b));
     HIP_TRY(hipMemcpy(b->d.last_visited + first, src, n * 8, hipMemcpyHostToDevice));
+    // a host write is replicated on every shard (the neuron state is): it
+    // replaces whatever this shard visited before it
+    if (b->d.visit_mark && n) HIP_TRY(hipMemset(b->d.visit_mark + first, 0, n));
     return ABNN_OK;
 }
 
@@ -1092,6 +1134,11 @@ abnn_status abnn_get_scalars(abnn_brain* b, abnn_scalars* out)
 abnn_status abnn_set_scalars(abnn_brain* b, const abnn_scalars* in)
 {
     REQUIRE(b && in, "null argument");
+    // the merge takes the largest value among the shards that visited a
+    // neuron: the clock must not move back over unmerged visits
+    REQUIRE(!(b->marks_dirty && in->clock < b->clock_host),
+            "the clock moves back over unmerged lastVisited stamps: merge them first "
+            "(abnn_comm_sync_visits, or abnn_shard_visits_delta / _merge) on every rank");
     ST_TRY(sync_all(b));
     uint64_t blk[3];
     blk[0] = in->clock;
@@ -1171,7 +1218,9 @@ abnn_status abnn_set_auto_stimulus(abnn_brain* b, uint64_t first, uint64_t count
 abnn_status abnn_traverse(abnn_brain* b, uint32_t passes, void* stream)
 {
     REQUIRE(b, "null argument");
+    REQUIRE(!b->records_invalid, kRecordsInvalid);
     ST_TRY(pass_error(b));  // a pass already completed failed: enqueue nothing more
+    if (b->d.visit_mark && passes) b->marks_dirty = true;
     HIP_TRY(hipSetDevice(b->device));
     hipStream_t s = pick(b, stream);
     for (uint32_t i = 0; i < passes; ++i) {
@@ -1212,7 +1261,10 @@ abnn_status abnn_shard_gate(abnn_brain* b, void* xchg_dev, void* stream)
 {
     REQUIRE(b && xchg_dev, "null argument");
     REQUIRE(((uintptr_t)xchg_dev & 7u) == 0, "exchange record must be 8-B aligned");
+    REQUIRE(!b->records_invalid, kRecordsInvalid);
     HIP_TRY(hipSetDevice(b->device));
+    ST_TRY(ensure_visit_marks(b));
+    if (b->d.visit_mark) b->marks_dirty = true;
     hipStream_t s = pick(b, stream);
     b->pending_renorm = renorm_due(b);
     return run_gate(b, static_cast<int32_t*>(xchg_dev), s);
@@ -1239,6 +1291,44 @@ abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t 
     return run_commit(b, static_cast<const int32_t*>(gathered_dev), world, renorm, s);
 }
 
+// The lastVisited merge over a caller's exchange (abnn.h): this shard's deltas,
+// then the all-reduced ones applied.
+abnn_status abnn_shard_visits_delta(abnn_brain* b, void* delta_dev, void* stream)
+{
+    REQUIRE(b && delta_dev, "null argument");
+    HIP_TRY(hipSetDevice(b->device));
+    hipStream_t s = pick(b, stream);
+    uint64_t* delta = static_cast<uint64_t*>(delta_dev);
+    if (!b->params.track_visits) {  // lastVisited is never written: nothing to merge
+        HIP_TRY(hipMemsetAsync(delta, 0, b->n_nrn * 8, s));
+        return ABNN_OK;
+    }
+    ST_TRY(ensure_visit_marks(b));
+    HIP_TRY(launch_visits_delta(b->d.last_visited, b->d.visit_mark, delta, b->n_nrn, s));
+    return ABNN_OK;
+}
+
+abnn_status abnn_shard_visits_merge(abnn_brain* b, const void* reduced_dev, void* stream)
+{
+    REQUIRE(b && reduced_dev, "null argument");
+    HIP_TRY(hipSetDevice(b->device));
+    if (!b->params.track_visits) return ABNN_OK;
+    ST_TRY(ensure_visit_marks(b));
+    HIP_TRY(launch_visits_merge(b->d.last_visited, b->d.visit_mark, static_cast<const uint64_t*>(reduced_dev), b->n_nrn,
+                                pick(b, stream)));
+    b->marks_dirty = false;
+    return ABNN_OK;
+}
+
+// Diagnostics (abnn_debug.h): the in-place compaction's poll limit (0 = every
+// wait gives up at once: the structural update's error path).
+abnn_status abnn_debug_set_compact_spin_limit(abnn_brain* b, uint32_t limit)
+{
+    REQUIRE(b, "null argument");
+    b->compact_spin_limit = limit;
+    return ABNN_OK;
+}
+
 // ---- sharded passes over RCCL ------------------------------------------------
 
 struct abnn_comm {
@@ -1248,8 +1338,30 @@ struct abnn_comm {
     char* gathered = nullptr;   // world exchange records, rank order
     uint64_t rec_bytes = 0;
     uint64_t* scratch = nullptr;  // visited-events all-reduce
+    uint64_t* visits = nullptr;   // the lastVisited merge's deltas (n_nrn words, sized on first use)
+    uint64_t visits_n = 0;
     bool broken = false;          // an earlier pass failed on this rank (abnn.h: abort on every rank)
 };
+
+// The lastVisited merge on the stream: every rank's deltas
+// (k_visits_delta), one all-reduce(MAX) of n_nrn words in place, the merge.
+static abnn_status merge_visits(abnn_brain* b, abnn_comm* c, hipStream_t s)
+{
+    if (!b->params.track_visits) return ABNN_OK;  // lastVisited is never written
+    ST_TRY(ensure_visit_marks(b));
+    if (c->visits_n != b->n_nrn) {
+        if (c->visits) HIP_TRY(hipFree(c->visits));
+        c->visits = nullptr;
+        c->visits_n = 0;
+        ST_TRY(dalloc(&c->visits, b->n_nrn));
+        c->visits_n = b->n_nrn;
+    }
+    HIP_TRY(launch_visits_delta(b->d.last_visited, b->d.visit_mark, c->visits, b->n_nrn, s));
+    RCCL_TRY(rccl_api().all_reduce(c->visits, c->visits, b->n_nrn, ncclUint64, ncclMax, c->comm, s));
+    HIP_TRY(launch_visits_merge(b->d.last_visited, b->d.visit_mark, c->visits, b->n_nrn, s));
+    b->marks_dirty = false;
+    return ABNN_OK;
+}
 
 abnn_status abnn_comm_unique_id(void* id_out)
 {
@@ -1305,6 +1417,7 @@ abnn_status abnn_comm_destroy(abnn_comm* c)
     if (c->comm) rccl_api().comm_destroy(c->comm);
     if (c->gathered) (void)hipFree(c->gathered);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->visits) (void)hipFree(c->visits);
     delete c;
     return ABNN_OK;
 }
@@ -1329,8 +1442,11 @@ static abnn_status shard_traverse_passes(abnn_brain* b, abnn_comm* c, uint32_t p
         ST_TRY(abnn_shard_gate(b, mine, s));
         RCCL_TRY(r.all_gather(mine, c->gathered, rec, ncclInt8, c->comm, s));  // in place, rank order
         ST_TRY(abnn_shard_apply(b, c->gathered, c->world, c->rank, s));
-        const uint64_t updates = b->structural_updates;
+        const uint64_t updates = b->structural_updates, renorms = b->renorms;
         ST_TRY(abnn_shard_commit(b, c->gathered, c->world, s));
+        // the clock went back: merge lastVisited before the next pass stamps
+        // smaller values than this epoch's
+        if (b->renorms != renorms && b->params.track_visits) ST_TRY(merge_visits(b, c, s));
         if (b->structural_updates != updates) {
             // every shard's record count changed (all ranks update after the
             // same pass): re-sum the visited events for the clock-tick rule
@@ -1366,6 +1482,7 @@ abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, vo
 abnn_status abnn_debug_comm_allgather(abnn_comm* c, void* buf, uint64_t bytes, uint32_t count, void* stream)
 {
     REQUIRE(c && buf, "null argument");
+    REQUIRE(!c->broken, "communicator unusable after an earlier error on this rank: abort / destroy it on every rank");
     HIP_TRY(hipSetDevice(c->device));
     const hipStream_t s = static_cast<hipStream_t>(stream);
     char* base = static_cast<char*>(buf);
@@ -1377,11 +1494,17 @@ abnn_status abnn_debug_comm_allgather(abnn_comm* c, void* buf, uint64_t bytes, u
 abnn_status abnn_comm_sync_visits(abnn_brain* b, abnn_comm* c, void* stream)
 {
     REQUIRE(b && c, "null argument");
+    REQUIRE(c->device == b->device, "communicator and handle are on different devices");
+    REQUIRE(!c->broken, "communicator unusable after an earlier error on this rank: abort / destroy it on every rank");
     ST_TRY(sync_all(b));
     hipStream_t s = pick(b, stream);
-    RCCL_TRY(rccl_api().all_reduce(b->d.last_visited, b->d.last_visited, b->n_nrn, ncclUint64, ncclMax, c->comm, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return ABNN_OK;
+    abnn_status st = merge_visits(b, c, s);
+    if (st == ABNN_OK && hipStreamSynchronize(s) != hipSuccess) {
+        set_err("hipStreamSynchronize failed after the lastVisited merge");
+        st = ABNN_ERR_HIP;
+    }
+    if (st != ABNN_OK) c->broken = true;
+    return st;
 }
 
 // Diagnostics (not part of abnn.h): the last pass's per-wave gate times,
@@ -1576,6 +1699,7 @@ abnn_status abnn_load_bnn(abnn_brain* b, const char* path)
         }
     }
     std::fclose(f);
+    b->records_invalid = false;
     return retally(b, 0, b->dims.n_syn);
 }
 
@@ -1696,6 +1820,11 @@ abnn_status abnn_load_flat(abnn_brain* b, const char* path)
     if (!ok) {
         set_err(std::string("flat load failed: ") + path);
         return ABNN_ERR_IO;
+    }
+    b->records_invalid = false;
+    if (b->d.visit_mark) {  // lastVisited replaced on every shard (replicated state)
+        HIP_TRY(hipMemset(b->d.visit_mark, 0, b->n_nrn));
+        b->marks_dirty = false;
     }
     return retally(b, 0, N);
 }

@@ -127,6 +127,7 @@ struct DeviceState {
     SynArrays syn;            // [capacity + kDummyRecords] each
     uint64_t* last_fired;     // [n_nrn]
     uint64_t* last_visited;   // [n_nrn]
+    uint8_t* visit_mark;      // shard handles with track_visits: [n_nrn] visited since the last merge (else null)
     uint64_t* clock;          // [1]
     uint64_t* pass_index;     // [1] passes run (keys the random-mode picks)
     float* reward;            // [1]
@@ -256,22 +257,21 @@ hipError_t launch_apply(const DeviceState& d, const KernelParams& kp, const int3
 hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);
 hipError_t launch_pack_src(const SynArrays& a, const uint32_t* in_dev, uint64_t first, uint64_t n, hipStream_t s);
 hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t first, uint64_t n, hipStream_t s);
-// Structural update (abnn.h contract, capi.hip structural_update): blocks
-// [b0, b0 + nblocks) of kCompactChunk records stably compacted into `dst`,
-// block b0 + i from offsets[i] on (live counts from the tombstone tally);
-// the tally's span {first block, last block + 1, tombstones}; the last
-// tombstone of a record range (z = its index + 1, atomicMax); a record copy
-// between non-overlapping ranges.
+// Structural update (abnn.h contract, capi.hip structural_update), all on `s`:
+// the tally's span {first block, last block + 1, tombstones, z, appended} in
+// sp, its blocks' offsets, the in-place compaction (one workgroup per CU; a
+// poll that reaches spin_limit sets *err = 1 and is never a hang), the hole
+// filled from the array's end (*err = 2: the tally and the records disagree),
+// then the grown records appended -- skipped when *err is set.
 hipError_t launch_structural_update(const SynArrays& syn, uint64_t n, uint64_t cap, uint32_t* dead, uint64_t nb,
                                     uint64_t* offsets, unsigned long long* sp, uint32_t* flags, uint32_t epoch,
-                                    uint32_t* err, uint32_t cus, uint4* grown, uint64_t slots, uint32_t* grown_cnt,
-                                    unsigned long long* stats_grown, hipStream_t s);
-hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offsets, const SynArrays& dst,
-                          uint64_t b0, uint64_t nblocks, hipStream_t s);
-hipError_t launch_dead_bounds(const uint32_t* dead, uint64_t nb, unsigned long long* out, hipStream_t s);
-hipError_t launch_last_tomb(const SynArrays& a, uint64_t base, uint64_t count, unsigned long long* z, hipStream_t s);
-hipError_t launch_copy_records(const SynArrays& from, uint64_t f0, const SynArrays& to, uint64_t t0, uint64_t count,
-                               hipStream_t s);
+                                    uint32_t* err, uint32_t spin_limit, uint32_t cus, uint4* grown, uint64_t slots,
+                                    uint32_t* grown_cnt, unsigned long long* stats_grown, hipStream_t s);
+// The sharded lastVisited merge (kernels.hip k_visits_delta / k_visits_merge):
+// delta[i] = mark[i] ? lv[i] + 1 : 0; after the all-reduce(MAX), lv[i] =
+// reduced[i] - 1 where it is non-zero, and every mark clears.
+hipError_t launch_visits_delta(const uint64_t* lv, const uint8_t* mark, uint64_t* delta, uint64_t n, hipStream_t s);
+hipError_t launch_visits_merge(uint64_t* lv, uint8_t* mark, const uint64_t* reduced, uint64_t n, hipStream_t s);
 // dead[] (pruning tally) recounted for the blocks that hold records [first, first + count) of n
 hipError_t launch_tally_dead(const SynArrays& a, uint64_t n, uint32_t* dead, uint64_t first, uint64_t count,
                              hipStream_t s);

@@ -36,7 +36,8 @@
 //                bitmap cannot come from the last passes' spike lists (the
 //                first passes, host writes).
 //   k_renorm   : brain.metal:135-145 with the base passed by the host (no race).
-//   k_compact / k_tally_dead : the structural update (README §5).
+//   k_compact_inplace / k_span_* / k_tally_dead : the structural update (README §5).
+//   k_visits_delta / k_visits_merge : the sharded lastVisited merge.
 //
 // All fp32 arithmetic is compiled with -ffp-contract=off and written operation
 // for operation like the oracle, so weights are bit-identical to the CPU.
@@ -1629,6 +1630,13 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 if (((vmask >> k) & 1u) && dst[k] < nn) d.last_visited[dst[k]] = now;
+            // a shard handle also marks the neuron visited since the last
+            // lastVisited merge (k_visits_delta)
+            if (d.visit_mark) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (((vmask >> k) & 1u) && dst[k] < nn) d.visit_mark[dst[k]] = 1u;
+            }
         }
         if constexpr (!kRandom) {
 #pragma unroll
@@ -2315,36 +2323,29 @@ __global__ __launch_bounds__(256) void k_renorm(DeviceState d, uint64_t base)
 }
 
 // ---------------------------------------------------------------------------
-// Structural update (README §5): stable removal of the tombstones.  Block b
-// moves records [b * kCompactChunk, (b + 1) * kCompactChunk) to dst from
-// offsets[b] on, in four coalesced rounds of kCompactThreads consecutive
-// records (one block scan of the live flags per round), streaming both ways.
-__global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint64_t n, const uint64_t* offsets,
-                                                             SynArrays dst, uint64_t b0)
+// The sharded lastVisited merge.  Unsharded, lastVisited[n] is
+// the value of the LAST write: the `now` of the last pass that visited n, or
+// what the host wrote after it.  A shard knows which neurons it visited since
+// the last merge (visit_mark, set beside the lastVisited store); the others
+// hold the replicated value of the last merge or host write.  Between two
+// merges the clock only moves forward (a renormalisation is always followed
+// by a merge), so of the shards that visited n the latest pass wrote the
+// largest value: delta = visited ? value + 1 : 0 (clock values never reach
+// 2^64 - 1), all-reduce MAX over the shards, then a non-zero result replaces
+// the value on every shard and the marks clear.
+__global__ __launch_bounds__(256) void k_visits_delta(const uint64_t* lv, const uint8_t* mark, uint64_t* delta,
+                                                      uint64_t n)
 {
-    static_assert(kCompactThreads == kScanThreads, "block_exclusive_scan is sized for kScanThreads");
-    __shared__ uint64_t s_wave[kCompactThreads / 64];
-    const uint64_t base = (b0 + blockIdx.x) * kCompactChunk;  // offsets[blockIdx.x] is block b0 + blockIdx.x's
-    uint32_t rs[4];
-    uint64_t rdw[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // all loads in flight first
-        const uint64_t i = base + (uint64_t)j * kCompactThreads + threadIdx.x;
-        const bool in = i < n;
-        rs[j] = in ? src_of(syn, i) : kSrcNone;
-        rdw[j] = in ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(syn.dw + i)) : 0ull;
-    }
-    uint64_t o = offsets[blockIdx.x];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const bool live = rs[j] != kSrcNone;
-        uint64_t tot;
-        const uint64_t pre = block_exclusive_scan(live ? 1u : 0u, &tot, s_wave);
-        if (live) {
-            set_src(dst, o + pre, rs[j]);
-            __builtin_nontemporal_store(rdw[j], reinterpret_cast<uint64_t*>(dst.dw + o + pre));
-        }
-        o += tot;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        delta[i] = mark[i] ? lv[i] + 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_visits_merge(uint64_t* lv, uint8_t* mark, const uint64_t* reduced, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t r = reduced[i];
+        if (r) lv[i] = r - 1u;
+        mark[i] = 0u;
     }
 }
 
@@ -2360,7 +2361,7 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(SynArrays syn, uint
 // none, so no cycle; every poll is bounded (err, never a hang).
 __global__ __launch_bounds__(kCompactThreads) void k_compact_inplace(SynArrays syn, uint64_t n, const uint64_t* offsets,
                                                                      const unsigned long long* sp, uint32_t* rd,
-                                                                     uint32_t epoch, uint32_t* err)
+                                                                     uint32_t epoch, uint32_t* err, uint32_t spin_limit)
 {
     // KB blocks per workgroup and round, all their loads in flight at once:
     // round i takes blocks [i KB G, (i + 1) KB G), workgroup w the blocks
@@ -2413,8 +2414,10 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact_inplace(SynArrays s
                     for (uint32_t spins = 0;; ++spins) {
                         const bool ok =
                             jj >= c || __hip_atomic_load(rd + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-                        if (__ballot(!ok) == 0) break;
-                        if (spins >= kLbSpinLimit) {
+                        // (spin_limit 0: every wait gives up -- the debug knob
+                        // abnn_debug_set_compact_spin_limit tests the error path)
+                        if (__ballot(!ok) == 0 && spins < spin_limit) break;
+                        if (spins >= spin_limit) {
                             if (lane == 0) {
                                 __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                 s_bad = 1u;
@@ -2536,9 +2539,13 @@ __global__ __launch_bounds__(kScanThreads) void k_grown_counts(const uint4* grow
 
 __global__ __launch_bounds__(kScanThreads) void k_append_grown(SynArrays a, uint64_t n, uint64_t cap, uint4* grown,
                                                                uint64_t slots, const uint32_t* cnt,
-                                                               unsigned long long* sp, unsigned long long* stats_grown)
+                                                               unsigned long long* sp, unsigned long long* stats_grown,
+                                                               const uint32_t* err)
 {
     __shared__ uint64_t s_wave[kScanThreads / 64];
+    // a failed removal (err: a compaction wait gave up, or the tally and the
+    // records disagree) leaves n - D meaningless: append nothing
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const uint64_t live = n - sp[2];
     uint64_t below = 0;  // used slots in the lower blocks
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kScanThreads) below += cnt[b];
@@ -2579,28 +2586,6 @@ __global__ __launch_bounds__(256) void k_dead_bounds(const uint32_t* dead, uint6
         atomicMin(out, lo);
         atomicMax(out + 1, hi);
         atomicAdd(out + 2, sum);
-    }
-}
-
-// z = 1 + the index of the last tombstone among records [base, base + count)
-__global__ __launch_bounds__(256) void k_last_tomb(SynArrays a, uint64_t base, uint64_t count, unsigned long long* z)
-{
-    unsigned long long m = 0;
-    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < count; k += (uint64_t)gridDim.x * 256)
-        if (src_of(a, base + k) == kSrcNone) m = base + k + 1;
-    if (m) atomicMax(z, m);
-}
-
-// Records [f0, f0 + count) of `from` to [t0, t0 + count) of `to` (the
-// ranges never overlap within one array): src code (and the random-mode
-// mirror) and {dst, w}.
-__global__ __launch_bounds__(256) void k_copy_records(SynArrays from, uint64_t f0, SynArrays to, uint64_t t0,
-                                                      uint64_t count)
-{
-    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < count; k += (uint64_t)gridDim.x * 256) {
-        set_src(to, t0 + k, src_of(from, f0 + k));
-        __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(from.dw + f0 + k)),
-                                    reinterpret_cast<uint64_t*>(to.dw + t0 + k));
     }
 }
 
@@ -2917,21 +2902,13 @@ hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t fir
     return hipGetLastError();
 }
 
-hipError_t launch_compact(const SynArrays& syn, uint64_t n, const uint64_t* offsets, const SynArrays& dst,
-                          uint64_t b0, uint64_t nblocks, hipStream_t s)
-{
-    if (n == 0 || nblocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compact, dim3((uint32_t)nblocks), dim3(kCompactThreads), 0, s, syn, n, offsets, dst, b0);
-    return hipGetLastError();
-}
-
 // The structural update's removal and append, all on `s` (sp: 5 device words,
 // see k_span_init): span bounds, offsets, z, the in-place compaction (one
 // workgroup per CU), the hole, the grown records.
 hipError_t launch_structural_update(const SynArrays& syn, uint64_t n, uint64_t cap, uint32_t* dead, uint64_t nb,
                                     uint64_t* offsets, unsigned long long* sp, uint32_t* flags, uint32_t epoch,
-                                    uint32_t* err, uint32_t cus, uint4* grown, uint64_t slots, uint32_t* grown_cnt,
-                                    unsigned long long* stats_grown, hipStream_t s)
+                                    uint32_t* err, uint32_t spin_limit, uint32_t cus, uint4* grown, uint64_t slots,
+                                    uint32_t* grown_cnt, unsigned long long* stats_grown, hipStream_t s)
 {
     hipLaunchKernelGGL(k_span_init, dim3(1), dim3(64), 0, s, sp);
     if (dead && nb && n) {
@@ -2940,40 +2917,31 @@ hipError_t launch_structural_update(const SynArrays& syn, uint64_t n, uint64_t c
         hipLaunchKernelGGL(k_span_offsets, dim3(1), dim3(kScanThreads), 0, s, dead, n, sp, offsets);
         hipLaunchKernelGGL(k_span_last, dim3(16), dim3(256), 0, s, syn, n, sp);
         hipLaunchKernelGGL(k_compact_inplace, dim3(cus), dim3(kCompactThreads), 0, s, syn, n, offsets, sp, flags, epoch,
-                           err);
+                           err, spin_limit);
         hipLaunchKernelGGL(k_span_fill, dim3(1024), dim3(256), 0, s, syn, n, sp, dead, err);
     }
     if (grown && slots) {
         const uint32_t gb = (uint32_t)((slots + kScanThreads - 1) / kScanThreads);
         hipLaunchKernelGGL(k_grown_counts, dim3(gb), dim3(kScanThreads), 0, s, grown, slots, grown_cnt);
         hipLaunchKernelGGL(k_append_grown, dim3(gb), dim3(kScanThreads), 0, s, syn, n, cap, grown, slots, grown_cnt, sp,
-                           stats_grown);
+                           stats_grown, err);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_dead_bounds(const uint32_t* dead, uint64_t nb, unsigned long long* out, hipStream_t s)
+hipError_t launch_visits_delta(const uint64_t* lv, const uint8_t* mark, uint64_t* delta, uint64_t n, hipStream_t s)
 {
-    if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_dead_bounds, dim3((uint32_t)std::min<uint64_t>((nb + 255) / 256, 1024)), dim3(256), 0, s,
-                       dead, nb, out);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_visits_delta, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, lv,
+                       mark, delta, n);
     return hipGetLastError();
 }
 
-hipError_t launch_last_tomb(const SynArrays& a, uint64_t base, uint64_t count, unsigned long long* z, hipStream_t s)
+hipError_t launch_visits_merge(uint64_t* lv, uint8_t* mark, const uint64_t* reduced, uint64_t n, hipStream_t s)
 {
-    if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_last_tomb, dim3((uint32_t)std::min<uint64_t>((count + 255) / 256, 64)), dim3(256), 0, s, a,
-                       base, count, z);
-    return hipGetLastError();
-}
-
-hipError_t launch_copy_records(const SynArrays& from, uint64_t f0, const SynArrays& to, uint64_t t0, uint64_t count,
-                               hipStream_t s)
-{
-    if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_copy_records, dim3((uint32_t)std::min<uint64_t>((count + 255) / 256, 8192)), dim3(256), 0, s,
-                       from, f0, to, t0, count);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_visits_merge, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, lv,
+                       mark, reduced, n);
     return hipGetLastError();
 }
 

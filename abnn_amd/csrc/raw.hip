@@ -77,6 +77,7 @@ constexpr uint32_t kRawApplyWGs = 1024;              // x 4 waves, grid-stride o
 constexpr uint32_t kRawNone = 0xFFFFFFFFu;
 constexpr uint32_t kRawCtab = 0xFFFFFFFEu;  // ginfo: the group's survivors span > 2 chunks (ctab lookup)
 constexpr uint32_t kRawRedo = 0xFFFFFFFDu;  // ginfo: not all stored (the pool ran out): recompute
+constexpr uint32_t kRawInit = 0x52415731u;  // RawHdr::init of a workspace whose err word is live
 
 // Workspace (16-B aligned pieces):
 //   hdr | filter (FB uint2) | gcand[NG] | gpre[NG] | btot[NG / 4096] | ginfo[NG] {S, seq, chunks} |
@@ -86,10 +87,11 @@ struct RawHdr {
     float R, rb;                       // pass-start reward and rBar (brain.metal:105-106)
     uint32_t chunks;                   // pool chunks handed out this pass
     uint32_t gcut;                     // groups below the budget's cut: [0, gcut)
-    uint32_t direct;                   // budget0 > the spike list: apply stamps itself
-    uint32_t err;                      // a recomputed group met direct stamps (abnn_traversal_workspace_error)
+    uint32_t direct;                   // the spikes exceed the spike list: apply stamps itself
+    uint32_t err;                      // sticky: a recomputed group met direct stamps in some pass since the
+                                       // last abnn_traversal_workspace_error (which clears it)
     uint32_t ovf;                      // some wave's survivors overflowed the pool this pass (groups recomputed)
-    uint32_t pad;
+    uint32_t init;                     // kRawInit once err has been initialised (the workspace starts as garbage)
     uint64_t g1, g2;                   // the pass's pre-gated and refractory-surviving events (diagnostics)
 };
 static_assert(sizeof(RawHdr) == 64, "workspace header");
@@ -215,8 +217,11 @@ __global__ __launch_bounds__(256) void k_raw_filter(const uint32_t* lastF, const
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // this pass's counters (the gate and the scan set them)
         ws.hdr->chunks = 0u;
         ws.hdr->t0 = 0u;
-        ws.hdr->err = 0u;
         ws.hdr->ovf = 0u;
+        if (ws.hdr->init != kRawInit) {  // first use of this workspace: err is sticky from here on
+            ws.hdr->err = 0u;
+            ws.hdr->init = kRawInit;
+        }
     }
     __syncthreads();
     const uint32_t now = *clock;
@@ -604,8 +609,8 @@ __global__ __launch_bounds__(kRawScanThreads) void k_raw_scan(RawWs ws, uint32_t
         h->gcut = gcut;
         // no group recomputed (nothing overflowed the pool): k_raw_apply reads
         // no lastF, so it stamps the spikes itself; else they wait for
-        // k_raw_stamp, unless the budget is beyond the spike list
-        h->direct = (b0 > ws.spike_cap || h->ovf == 0u) ? 1u : 0u;
+        // k_raw_stamp, unless this pass's spikes (nc <= b0) exceed the list
+        h->direct = (nc > ws.spike_cap || h->ovf == 0u) ? 1u : 0u;
         h->g1 = ws.ng ? s_g[0] : 0ull;
         h->g2 = ws.ng ? s_g[1] : 0ull;
         *budget = b0 - nc;                                               // brain.metal:95-98 (C1: no wrap)
@@ -868,8 +873,13 @@ abnn_status abnn_traversal_workspace_error(const void* workspace, uint32_t* err,
 {
     if (!workspace || !err) return ABNN_ERR_INVALID;
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    const RawHdr* h = static_cast<const RawHdr*>(workspace);
-    if (hipMemcpyAsync(err, &h->err, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return ABNN_ERR_HIP;
+    RawHdr* h = static_cast<RawHdr*>(const_cast<void*>(workspace));
+    RawHdr hh;
+    if (hipMemcpyAsync(&hh, h, sizeof(hh), hipMemcpyDeviceToHost, s) != hipSuccess) return ABNN_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return ABNN_ERR_HIP;
+    *err = hh.init == kRawInit ? hh.err : 0u;  // (never launched on: nothing to report)
+    // sticky until read: cleared here, not by the next launch
+    if (hh.init == kRawInit && hh.err && hipMemsetAsync(&h->err, 0, 4, s) != hipSuccess) return ABNN_ERR_HIP;
     return hipStreamSynchronize(s) == hipSuccess ? ABNN_OK : ABNN_ERR_HIP;
 }
 

@@ -13,8 +13,14 @@ offset in the ordered global spike budget (apply) and the global spike list
 same value ``now``, so this equals the north-star all-reduce(MAX) over
 lastFired exactly, at ~10 KB per rank instead of 40 MB per pass.
 
-``lastVisited`` feeds no decision (brain.metal:44), so it is merged lazily with
-all-reduce(MAX) by :meth:`ShardedBrain.sync_visits`.
+``lastVisited`` feeds no decision (brain.metal:44), so it is merged lazily
+(:func:`merge_visits`): unsharded it holds the LAST value written, so each
+shard contributes only the neurons it visited since the previous merge
+(value + 1, else 0), the contributions are all-reduced with MAX, and a
+non-zero result replaces the value everywhere.  MAX picks the last writer
+because the clock only moves forward between merges: one is forced after
+every renormalisation (:func:`sharded_pass`), and the C-ABI refuses to move
+the clock back over unmerged visits.
 """
 from __future__ import annotations
 
@@ -50,6 +56,15 @@ class Engine(Protocol):
     def apply(self, gathered, world: int, rank: int) -> None: ...
 
     def commit(self, gathered, world: int) -> None: ...
+
+    def tracks_visits(self) -> bool: ...
+
+    def renormalisations(self) -> int: ...
+
+    def visits_delta(self):
+        """int64 tensor of N_NRN merge deltas (abnn_shard_visits_delta)."""
+
+    def visits_merge(self, reduced) -> None: ...
 
 
 class TorchComm:
@@ -88,12 +103,28 @@ class TorchComm:
         self._run(lambda x: self._dist.all_reduce(x, op=self._dist.ReduceOp.SUM, group=self.group), t)
 
 
+def merge_visits(engine: Engine, comm) -> None:
+    """The lastVisited merge (abnn.h abnn_shard_visits_delta / _merge): every
+    rank's deltas, one all-reduce(MAX), the merge.  Collective: every rank
+    calls it at the same point."""
+    if not engine.tracks_visits():
+        return
+    delta = engine.visits_delta()
+    comm.all_reduce_max(delta)
+    engine.visits_merge(delta)
+
+
 def sharded_pass(engine: Engine, comm, xchg, gathered) -> None:
-    """One C1 pass over all shards: gate -> all-gather of the records -> apply -> commit."""
+    """One C1 pass over all shards: gate -> all-gather of the records -> apply
+    -> commit; after a renormalisation (the clock went back) the lastVisited
+    merge, before the next pass stamps values below this epoch's."""
+    renorms = engine.renormalisations()
     engine.gate(xchg)
     comm.all_gather(gathered, xchg)
     engine.apply(gathered, comm.world, comm.rank)
     engine.commit(gathered, comm.world)
+    if engine.renormalisations() != renorms:  # every rank renormalises after the same pass
+        merge_visits(engine, comm)
 
 
 class _GpuEngine:
@@ -109,6 +140,23 @@ class _GpuEngine:
 
     def commit(self, gathered, world) -> None:
         self.brain.shard_commit(gathered.data_ptr(), world, self._stream())
+
+    def tracks_visits(self) -> bool:
+        return bool(self.brain.params.track_visits)
+
+    def renormalisations(self) -> int:
+        return self.brain.renormalisations()
+
+    def visits_delta(self):
+        import torch
+
+        dev = torch.device("cuda", self.brain.device)
+        t = torch.empty(self.brain.n_neuron(), dtype=torch.int64, device=dev)
+        self.brain.shard_visits_delta(t.data_ptr(), self._stream())
+        return t
+
+    def visits_merge(self, reduced) -> None:
+        self.brain.shard_visits_merge(reduced.data_ptr(), self._stream())
 
 
 class NativeComm:
@@ -221,14 +269,13 @@ class ShardedBrain:
         return self.brain.visited_events()
 
     def sync_visits(self) -> None:
-        """Lazy all-reduce(MAX) of lastVisited (never read by a decision)."""
+        """The lazy lastVisited merge (never read by a decision): call on every
+        rank before reading or saving lastVisited."""
         if self.native is not None:
             from ._lib import call
 
-            call("abnn_comm_sync_visits", self.brain._h, self.native.handle, None)
+            call("abnn_comm_sync_visits", self.brain._h, self.native.handle,
+                 int(self._torch.cuda.current_stream(self.xchg.device).cuda_stream))
             return
-        torch = self._torch
-        lv = self.brain.last_visited().view(np.int64)
-        t = torch.from_numpy(lv.copy()).to(self.xchg.device)
-        self.comm.all_reduce_max(t)
-        self.brain.set_last_visited(t.cpu().numpy().view(np.uint64))
+        merge_visits(self.engine, self.comm)
+        self.brain.synchronize()

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define ABNN_ABI_VERSION 8
+#define ABNN_ABI_VERSION 9
 
 typedef enum abnn_status {
     ABNN_OK = 0,
@@ -342,6 +342,29 @@ abnn_status abnn_shard_apply(abnn_brain* b, const void* gathered_dev, uint32_t w
 abnn_status abnn_shard_commit(abnn_brain* b, const void* gathered_dev, uint32_t world,
                               void* stream);
 
+/* The lastVisited merge of a sharded brain with track_visits.
+ * Unsharded, lastVisited[n] holds the last value written: the clock of the
+ * last pass that visited n, or what the host wrote after it.  Each shard
+ * marks the neurons its passes visit; between merges the clock only moves
+ * forward (abnn_set_scalars refuses to move it back over unmerged visits, and
+ * abnn_shard_traverse merges after every renormalisation), so the shard that
+ * visited n last wrote the largest value:
+ *   abnn_shard_visits_delta -> delta_dev[i] = visited since the last merge ?
+ *                              lastVisited[i] + 1 : 0   (u64 x N_NRN, device)
+ *   [all-reduce(MAX) of the deltas over the shards]
+ *   abnn_shard_visits_merge -> lastVisited[i] = reduced[i] - 1 where reduced[i]
+ *                              != 0; every mark clears.
+ * A caller driving the shard phases itself merges whenever
+ * abnn_renormalisations changed after a pass, and before reading lastVisited
+ * (abnn_comm_sync_visits does all three steps over RCCL).  Host writes
+ * (abnn_set_last_visited, abnn_load_flat) must be the same on every shard;
+ * they clear the marks of what they write.  Without track_visits both calls
+ * are no-ops (delta = 0).                                                    */
+abnn_status abnn_shard_visits_delta(abnn_brain* b, void* delta_dev, void* stream);
+abnn_status abnn_shard_visits_merge(abnn_brain* b, const void* reduced_dev, void* stream);
+/* Renormalisations run by this handle (host-side count, no synchronisation). */
+uint64_t abnn_renormalisations(const abnn_brain* b);
+
 /* Spike budget left by the last pass: max_spikes minus the spikes it emitted
  * (the reference's bufBudget_ after a pass, brain.h:58; the host resets it to
  * kMaxSpikes before every pass, brain.cpp:90, here the max_spikes knob; C1 never
@@ -370,10 +393,10 @@ uint64_t abnn_structural_updates(const abnn_brain* b);
  * abnn_traversal_workspace_min_bytes the least accepted (no pool).  Survivors
  * that do not fit the pool are recomputed from the records (slower, same
  * results).  The spikes are stamped after the pass's last lastF read from a
- * list of min(events, 65536) entries; a *budget above that stamps them
- * directly, which is exact unless survivors also overflowed the pool -- then
- * abnn_traversal_workspace_error reports 1 (the host's kMaxSpikes = 2560,
- * brain.cpp:90, never comes near it).  This is the reference's memory
+ * list of min(events, 65536) entries; a pass with more spikes than that
+ * stamps them directly, which is exact unless survivors also overflowed the
+ * pool -- then abnn_traversal_workspace_error reports 1 (the host's
+ * kMaxSpikes = 2560, brain.cpp:90, never comes near it).  This is the reference's memory
  * layout, so it streams 16 B per visited event; the pre-spike test is
  * answered from an LDS filter of lastF, which is gathered only for the ~1 %
  * of events the filter passes (the handle API's layout moves
@@ -401,8 +424,10 @@ typedef struct abnn_traversal_args {
 } abnn_traversal_args;
 uint64_t abnn_traversal_workspace_bytes(uint32_t n_syn, uint32_t events);
 uint64_t abnn_traversal_workspace_min_bytes(uint32_t n_syn, uint32_t events);
-/* synchronises `stream`: 1 if a pass since the last launch's start stamped
- * directly while recomputing overflowed survivors (see above), else 0 */
+/* synchronises `stream`: 1 if any pass on this workspace since the last call
+ * (or since its first launch) stamped directly while recomputing overflowed
+ * survivors (see above), else 0; the flag is sticky until this call reads
+ * and clears it, so one check after many passes sees every pass */
 abnn_status abnn_traversal_workspace_error(const void* workspace, uint32_t* err, void* stream);
 abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream);
 abnn_status abnn_launch_renormalise(uint32_t* last_fired, uint32_t* last_visited, uint32_t* clock,
@@ -419,8 +444,10 @@ abnn_status abnn_launch_renormalise(uint32_t* last_fired, uint32_t* last_visited
  * exchange records (in place, on the stream), abnn_shard_apply,
  * abnn_shard_commit -- with no host round trip except after a structural
  * update (an all-reduce of the shards' visited events for the clock-tick
- * rule, then abnn_set_global_events).  abnn_comm_sync_visits is the lazy
- * all-reduce(MAX) of lastVisited (never read by a decision, brain.metal:44).
+ * rule, then abnn_set_global_events) and, with track_visits, the lastVisited
+ * merge after every renormalisation (above).  abnn_comm_sync_visits is that
+ * merge on demand (lastVisited is never read by a decision, brain.metal:44;
+ * merge before reading or saving it).
  * An error on any rank (a failed launch or collective, a pass error flag)
  * leaves the other ranks inside the pass's collectives: the communicator is
  * then marked unusable (every later abnn_shard_traverse on it returns

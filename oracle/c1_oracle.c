@@ -400,6 +400,7 @@ static void pass_end(oracle_state* s, const uint32_t* fired, uint64_t n_fired,
         uint64_t base = s->clock;
         for (uint64_t i = 0; i < s->n_nrn; ++i) s->last_fired[i] -= base;
         s->clock = 0;
+        s->renorms += 1;
     }
     s->stats.passes += 1;
     s->pass_index += 1;
@@ -428,7 +429,10 @@ void oracle_pass_serial(oracle_state* s)
         const uint64_t e = rec_index(s, t);
         abnn_synapse sy = s->syn[e];               /* MSL:70 */
         uint64_t tg = s->dims.syn_offset + t;
-        if (p->track_visits && sy.dst < s->n_nrn) s->last_visited[sy.dst] = now;  /* README §4 */
+        if (p->track_visits && sy.dst < s->n_nrn) {  /* README §4 */
+            s->last_visited[sy.dst] = now;
+            if (s->visit_mark) s->visit_mark[sy.dst] = 1;
+        }
         if (sy.src >= s->n_nrn) continue;                       /* removed synapse (README §5) */
         if (age32(now, L[sy.src]) > p->window_pre) continue;    /* MSL:73-77 */
         s->stats.pre_gated++;
@@ -498,7 +502,10 @@ static void gate_range(const oracle_state* s, uint64_t t0, uint64_t t1, g2vec* o
         abnn_synapse sy = s->syn[rec_index(s, t)];
         /* lastVisited is never read by a decision: written as visited, with
          * the same value `now` from every thread */
-        if (p->track_visits && sy.dst < s->n_nrn) s->last_visited[sy.dst] = now;
+        if (p->track_visits && sy.dst < s->n_nrn) {
+            s->last_visited[sy.dst] = now;
+            if (s->visit_mark) s->visit_mark[sy.dst] = 1;  /* the shard merge's marks (abnn.h) */
+        }
         if (sy.src >= s->n_nrn) continue;  /* removed synapse */
         if (age32(now, L[sy.src]) > p->window_pre) continue;
         c->g1++;
@@ -623,6 +630,7 @@ void oracle_shard_commit(oracle_state* s, const int32_t* gathered, uint32_t worl
         uint64_t base = s->clock;
         for (uint64_t i = 0; i < s->n_nrn; ++i) s->last_fired[i] -= base;
         s->clock = 0;
+        s->renorms += 1;
     }
     s->stats.passes += 1;
     s->pass_index += 1;

@@ -40,6 +40,10 @@ typedef struct oracle_state {
     abnn_synapse* grown;        /* structural plasticity: compact_every *
                                    max_spikes slots, zeroed by the caller;
                                    a grown synapse has pad bits = 1          */
+    uint8_t* visit_mark;        /* shard with track_visits: n_nrn, 1 = visited
+                                   since the last lastVisited merge (the
+                                   caller merges, abnn.h); NULL = none       */
+    uint64_t renorms;           /* renormalisations run                     */
 } oracle_state;
 
 /* One G2 entry (event that passed both gates) of a shard, in event order. */

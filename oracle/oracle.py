@@ -51,7 +51,8 @@ class State(C.Structure):
                 ("last_fired", C.c_void_p), ("last_visited", C.c_void_p), ("clock", C.c_uint64),
                 ("reward", C.c_float), ("rbar", C.c_float), ("rng", C.c_uint64),
                 ("stim_first", C.c_uint64), ("stim_count", C.c_uint64), ("stats", Stats),
-                ("pass_index", C.c_uint64), ("grown", C.c_void_p)]
+                ("pass_index", C.c_uint64), ("grown", C.c_void_p), ("visit_mark", C.c_void_p),
+                ("renorms", C.c_uint64)]
 
 
 _lib = None
@@ -150,6 +151,8 @@ class OracleBrain:
         self.last_fired = np.zeros(n_nrn, dtype=np.uint64)
         self.last_visited = np.zeros(n_nrn, dtype=np.uint64)
         self._grown = np.zeros(max(1, self.p.compact_every * self.p.max_spikes), dtype=SYN_DTYPE)
+        # a shard that tracks visits marks them for the lastVisited merge (abnn.h)
+        self.visit_mark = np.zeros(n_nrn, dtype=np.uint8) if (global_events and self.p.track_visits) else None
         self.s = State()
         self.s.dims = Dims(n_input, n_output, n_hidden, n_syn, events_per_pass, syn_offset,
                            global_events, cap)
@@ -168,6 +171,7 @@ class OracleBrain:
         self.s.last_fired = self.last_fired.ctypes.data
         self.s.last_visited = self.last_visited.ctypes.data
         self.s.grown = self._grown.ctypes.data
+        self.s.visit_mark = self.visit_mark.ctypes.data if self.visit_mark is not None else None
 
     # state ---------------------------------------------------------------------------------
     def n_neuron(self) -> int:
@@ -198,6 +202,32 @@ class OracleBrain:
 
     def set_timestamps(self, idx: Sequence[int], value: int) -> None:
         self.last_fired[np.asarray(idx, dtype=np.int64)] = np.uint64(value)
+
+    def set_last_visited(self, values, first: int = 0) -> None:
+        """Host write (replicated on every shard): replaces what this shard
+        visited before it (abnn_set_last_visited clears those marks)."""
+        v = np.asarray(values, dtype=np.uint64)
+        self.last_visited[first:first + v.shape[0]] = v
+        if self.visit_mark is not None:
+            self.visit_mark[first:first + v.shape[0]] = 0
+
+    def renormalisations(self) -> int:
+        return int(self.s.renorms)
+
+    def visits_delta(self) -> np.ndarray:
+        """abnn_shard_visits_delta restated: visited ? lastVisited + 1 : 0 (int64 view)."""
+        if self.visit_mark is None:
+            return np.zeros(self.last_visited.shape[0], dtype=np.int64)
+        d = np.where(self.visit_mark != 0, self.last_visited + np.uint64(1), np.uint64(0))
+        return d.view(np.int64)
+
+    def visits_merge(self, reduced: np.ndarray) -> None:
+        """abnn_shard_visits_merge restated."""
+        r = np.asarray(reduced).view(np.uint64)
+        nz = r != 0
+        self.last_visited[nz] = r[nz] - np.uint64(1)
+        if self.visit_mark is not None:
+            self.visit_mark[:] = 0
 
     def set_auto_stimulus(self, first: int, count: int) -> None:
         self.s.stim_first, self.s.stim_count = first, count

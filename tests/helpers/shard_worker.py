@@ -26,21 +26,29 @@ def main():
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl" if native else "gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    sb = ShardedBrain(TorchComm(), 256, 256, 30_000, n_syn, events, device=dev, track_visits=1, native=native)
+    # track_visits with a renormalisation after pass 5 (the clock goes back to
+    # 0) and a host write of lastVisited ahead of the clock before pass 6, the
+    # same on every rank: the lastVisited merge
+    extra = dict(track_visits=1, renorm_thresh=4)
+    sb = ShardedBrain(TorchComm(), 256, 256, 30_000, n_syn, events, device=dev, native=native, **extra)
     sb.brain.build_random_graph(4)
     sb.brain.set_auto_stimulus(0, 256)
-    for k in range(passes):
+
+    def at_pass(b, k):
         if k == 6:
-            sb.brain.set_reward(0.125)
+            b.set_reward(0.125)
+            b.set_last_visited(np.full(8400, b.scalars()["clock"] + 2, np.uint64), 600)
+
+    for k in range(passes):
+        at_pass(sb.brain, k)
         sb.step(1)
     torch.cuda.synchronize()
     sb.sync_visits()
-    ref = abnn_amd.Brain(256, 256, 30_000, n_syn, events, track_visits=1, device=dev)
+    ref = abnn_amd.Brain(256, 256, 30_000, n_syn, events, device=dev, **extra)
     ref.build_random_graph(4)
     ref.set_auto_stimulus(0, 256)
     for k in range(passes):
-        if k == 6:
-            ref.set_reward(0.125)
+        at_pass(ref, k)
         ref.encode_traversal(1)
     mine = sb.brain.download_synapses()
     theirs = ref.download_synapses(sb.lo, sb.hi - sb.lo)
@@ -48,6 +56,7 @@ def main():
     ok &= bool(np.array_equal(sb.brain.last_fired(), ref.last_fired()))
     ok &= bool(np.array_equal(sb.brain.last_visited(), ref.last_visited()))
     ok &= sb.brain.scalars() == ref.scalars()
+    ok &= sb.brain.renormalisations() == ref.renormalisations() == 1
     flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=f"cuda:{dev}" if native else "cpu")
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if sb.native is not None:

@@ -40,3 +40,37 @@ class GpuShards:
             b.shard_apply(g.data_ptr(), self.world, r, self.stream)
         for b in self.brains:
             b.shard_commit(g.data_ptr(), self.world, self.stream)
+
+
+def merge_visits_local(shards) -> None:
+    """The lastVisited merge (abnn.h abnn_shard_visits_delta / _merge) over
+    shards held in one process: every shard's deltas, their elementwise MAX
+    (what the all-reduce does), the merge on every shard.  Works for oracle
+    shards (numpy) and GPU shards (abnn_amd.Brain, torch tensors on the
+    current stream)."""
+    if hasattr(shards[0], "visits_delta"):  # OracleBrain
+        red = np.maximum.reduce([s.visits_delta() for s in shards])
+        for s in shards:
+            s.visits_merge(red)
+        return
+    import torch
+
+    dev = torch.device("cuda", shards[0].device)
+    stream = torch.cuda.current_stream(dev)
+    n = shards[0].n_neuron()
+    deltas = [torch.empty(n, dtype=torch.int64, device=dev) for _ in shards]
+    for s, d in zip(shards, deltas):
+        s.shard_visits_delta(d.data_ptr(), stream)
+    red = torch.stack(deltas).amax(dim=0).contiguous()
+    for s in shards:
+        s.shard_visits_merge(red.data_ptr(), stream)
+    stream.synchronize()
+
+
+def shard_pass_merging(shards, pass_fn) -> None:
+    """One sharded pass (pass_fn), then the merge if it renormalised -- the
+    rule of abnn_amd.shard.sharded_pass, in one process."""
+    before = shards[0].renormalisations()
+    pass_fn()
+    if shards[0].renormalisations() != before:
+        merge_visits_local(shards)

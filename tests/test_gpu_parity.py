@@ -229,6 +229,68 @@ def test_virtual_shards_equal_unsharded_gpu(gpu, monkeypatch, world, fused):
         assert b.scalars() == g.scalars()
 
 
+def _flat_sections(path, n_nrn):
+    raw = open(path, "rb").read()
+    n = int(np.frombuffer(raw[:4], np.uint32)[0])
+    pairs = np.frombuffer(raw[16:16 + 8 * n], np.uint32)
+    w = np.frombuffer(raw[16 + 8 * n:16 + 12 * n], np.uint32)
+    ts = raw[16 + 12 * n:]
+    assert len(ts) == 16 * n_nrn
+    return pairs, w, ts
+
+
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["fused-shard-pass", "two-kernel-shard-pass"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_virtual_shards_visits_merge(gpu, monkeypatch, tmp_path, world, fused):
+    """track_visits on shards: the lastVisited merge (abnn_shard_visits_delta /
+    _merge after every renormalisation and before the read) equals the
+    unsharded brain bit for bit, across two renormalisations and a host write
+    ahead of the clock whose value pass 7's visits write again; so do the
+    shards' flat saves (abnn_save_flat: records, lastFired, lastVisited)."""
+    import torch
+
+    import abnn_amd
+    from abnn_amd.shard import global_events, shard_ranges
+    from shard_helpers import merge_visits_local
+
+    monkeypatch.setenv("ABNN_FUSED", fused)
+    n_syn, passes, nh = 2_000_000, 9, 30_000
+    kw = dict(track_visits=1, renorm_thresh=2)  # clock 0 1 2 3 | 0 1 2 3 | 0
+    ge = global_events(n_syn, n_syn, world)
+    shards = []
+    for lo, hi in shard_ranges(n_syn, world):
+        b = abnn_amd.Brain(256, 256, nh, hi - lo, n_syn, syn_offset=lo, global_events=ge, **kw)
+        b.build_random_graph(4)
+        b.set_auto_stimulus(0, 256)
+        shards.append(b)
+    g, o = _pair(nh, n_syn, n_syn, seed=4, **kw)
+    gs = GpuShards(shards)
+    for k in range(passes):
+        if k == 4:
+            for x in [g, o, *shards]:
+                clk = x.scalars()["clock"]
+                x.set_last_visited(np.full(8400, clk + 3, np.uint64), 600)
+        g.encode_traversal(1)
+        o.pass_serial()
+        before = shards[0].renormalisations()
+        gs.pass_()
+        if shards[0].renormalisations() != before:
+            merge_visits_local(shards)
+    torch.cuda.synchronize()
+    merge_visits_local(shards)
+    assert g.renormalisations() == o.renormalisations() == shards[0].renormalisations() == 2
+    assert np.array_equal(g.last_visited(), o.last_visited)
+    _assert_same(g, o, "unsharded")
+    g.save_flat(tmp_path / "whole.flat")
+    wp, ww, wts = _flat_sections(tmp_path / "whole.flat", g.n_neuron())
+    for r, ((lo, hi), b) in enumerate(zip(shard_ranges(n_syn, world), shards)):
+        assert np.array_equal(b.last_visited(), g.last_visited()), f"rank {r} lastVisited"
+        b.save_flat(tmp_path / f"shard{r}.flat")
+        sp, sw, sts = _flat_sections(tmp_path / f"shard{r}.flat", b.n_neuron())
+        assert np.array_equal(sp, wp[2 * lo:2 * hi]) and np.array_equal(sw, ww[lo:hi]), f"rank {r} records"
+        assert sts == wts, f"rank {r} lastFired / lastVisited bytes"
+
+
 def test_virtual_shards_partial_sweep_vs_oracle_shards(gpu):
     # events < shard size: each shard sweeps only its first `events` (config 4 shape)
     from abnn_amd.shard import global_events, shard_ranges

@@ -167,3 +167,75 @@ def test_structural_update_in_place_patterns(gpu, pattern):
         o.pass_serial()
         _same(g, o, f"{pattern} pass {k}")
     assert g.n_syn() <= n - int(dead.sum())
+
+
+def _hip_copy_d2d(dst: int, src: int, nbytes: int) -> None:
+    """hipMemcpy device -> device through the runtime torch loaded (test-only raw write)."""
+    import ctypes as C
+    import os
+
+    import torch
+
+    hip = C.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert hip.hipMemcpy(dst, src, nbytes, 3) == 0  # hipMemcpyDeviceToDevice
+    assert hip.hipDeviceSynchronize() == 0
+
+
+def test_failed_structural_update_refuses_passes(gpu, tmp_path):
+    """The in-place compaction cannot be rolled back, so a structural update
+    that fails part-way leaves the records invalid: the handle then refuses
+    every pass (ABNN_ERR_INVALID) until they are reloaded.  Both failures:
+    (1) a compaction wait that gives up (the debug knob's spin limit 0 makes
+    every wait give up: a 50k tombstone run makes blocks wait on lower ones);
+    (2) a tombstone tally that disagrees with the records (the last block's
+    tombstones revived behind the handle's back through the device layout).
+    After a reload the passes equal the oracle again."""
+    from abnn_amd import _lib
+
+    kw = dict(w_prune=1e-30, p_new=0.0, compact_every=1)
+    g, o = _pair(0, **kw)
+    syn = g.download_synapses()
+    idx = np.arange(len(syn))
+    dead = (idx >= 10_000) & (idx < 60_000)
+    syn["src"][dead] = 0xFFFFFFFF
+    syn["dst"][dead] = 0xFFFFFFFF
+    g.upload_synapses(syn)
+    o.set_synapses(syn)
+    flat, sc = str(tmp_path / "before.flat"), g.scalars()
+    g.save_flat(flat)
+
+    def refused():
+        with pytest.raises(_lib.AbnnError, match="failed structural update") as e:
+            g.encode_traversal(1)
+        assert e.value.status == 1  # ABNN_ERR_INVALID
+
+    def reload():
+        g.load_flat(flat)
+        g.set_scalars(sc["clock"], sc["reward"], sc["rbar"], sc["pass_index"])
+
+    # (1) the compaction's waits give up
+    _lib.call("abnn_debug_set_compact_spin_limit", g._h, 0)
+    with pytest.raises(_lib.AbnnError, match="wait timed out; the records are not valid"):
+        g.encode_traversal(1)
+    refused()
+    refused()
+    _lib.call("abnn_debug_set_compact_spin_limit", g._h, 1 << 22)
+    reload()
+
+    # (2) records [57344, 60160) (the last tallied block's tombstones, whole
+    # 256-record groups) revived with the codes and {dst, w} of records [0, 2816)
+    lay = g.synapse_layout()["arrays"]
+    a, m = 57344, 2816
+    for name, eb in (("src_code_lo", 2), ("src_code_hi", 1), ("dst_w", 8)):
+        base = lay[name][0]
+        _hip_copy_d2d(base + a * eb, base, m * eb)
+    with pytest.raises(_lib.AbnnError, match="tally and the records disagree; the records are not valid"):
+        g.encode_traversal(1)
+    refused()
+    reload()
+
+    for k in range(3):  # reloaded: the passes run and equal the oracle's
+        g.encode_traversal(1)
+        o.pass_serial()
+        _same(g, o, f"after reload, pass {k}")

@@ -187,17 +187,29 @@ def test_raw_survivor_pool_overflow_recomputes(gpu, pool_chunks):
 
 
 def test_raw_direct_stamps_with_pool_overflow_are_reported(gpu):
-    """A budget above the spike list (min(E, 65536) entries) stamps directly;
-    with survivors recomputed as well, abnn_traversal_workspace_error says
-    so (abnn.h)."""
+    """A pass whose spikes exceed the spike list (min(E, 65536) entries; an
+    unbounded budget) stamps directly; with survivors recomputed as well,
+    abnn_traversal_workspace_error says so (abnn.h).  Config 2's 10M events:
+    the all-gated passes 3-5 emit ~10^5 spikes each."""
     from oracle import oracle as O
 
-    o = O.OracleBrain(256, 256, 99_488, 1_000_000, 1_000_000)
-    o.build_random_graph(1, nthreads=8)
-    r = RawBrain(o.syn.copy(), 100_000, 1_000_000, 10**8, pool_chunks=0)
+    n = 10_000_000
+    o = O.OracleBrain(256, 256, 99_488, n, n)
+    o.build_random_graph(1, nthreads=16)
+    r = RawBrain(o.syn.copy(), 100_000, n, 10**8, pool_chunks=0)
     for _ in range(5):  # passes 3-5: every event gated, candidates far beyond the budget list
         r.one_pass()
-    assert r.workspace_error() == 1
+    assert r.workspace_error() == 1  # sticky: set in passes 3-5, still seen after pass 5
+    assert r.workspace_error() == 0  # ... and cleared by the read
+
+
+def test_raw_budget_above_list_with_pool_overflow_is_exact(gpu):
+    """A budget above the spike list does not by itself stamp directly: only a
+    pass whose spikes exceed the list does.  With E <= 65536 the
+    list holds every spike, so even with every survivor recomputed (no pool)
+    and an unbounded budget the stamps wait for the last lastF read: exact,
+    no error."""
+    _run(9_488, 200_000, 60_000, 8, max_spikes=10**8, pool_chunks=0)
 
 
 def test_raw_config3_bit_exact_vs_threaded_oracle(gpu):

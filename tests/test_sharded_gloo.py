@@ -29,6 +29,18 @@ class CpuShardEngine:
     def commit(self, gathered, world):
         self.ob.shard_commit(gathered.numpy(), world)
 
+    def tracks_visits(self):
+        return bool(self.ob.p.track_visits)
+
+    def renormalisations(self):
+        return self.ob.renormalisations()
+
+    def visits_delta(self):
+        return torch.from_numpy(self.ob.visits_delta().copy())
+
+    def visits_merge(self, reduced):
+        self.ob.visits_merge(reduced.numpy())
+
 
 def _free_port():
     s = socket.socket()
@@ -38,48 +50,64 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, events, track):
+# host write of lastVisited ahead of the clock: (before pass, (first neuron,
+# count), value - pass-start clock) -- the same on every rank, as the neuron
+# state is replicated.  With renorm_thresh 2 the clock runs 0 1 2 3 | 0 1 2 3
+# | 0, so the written value 3 is also what pass 7's visits write
+AHEAD = (4, (600, 8400), 3)
+
+
+def _worker(rank, world, port, events, track, renorm):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
     import torch.distributed as dist
-    from abnn_amd.shard import TorchComm, global_events, shard_ranges, sharded_pass
+    from abnn_amd.shard import TorchComm, global_events, merge_visits, shard_ranges, sharded_pass
     from oracle import oracle as O
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    extra = dict(renorm_thresh=renorm) if renorm else {}
     try:
         comm = TorchComm()
         lo, hi = shard_ranges(N_SYN, world)[rank]
         ge = global_events(N_SYN, events, world)
         ob = O.OracleBrain(256, 256, N_HIDDEN, hi - lo, events, syn_offset=lo, global_events=ge,
-                           track_visits=track)
+                           track_visits=track, **extra)
         ob.build_random_graph(seed=11, nthreads=2)
         ob.set_auto_stimulus(0, 256)
         eng = CpuShardEngine(ob)
         words = ob.exchange_words()
         xchg = torch.zeros(words, dtype=torch.int32)
         gathered = torch.zeros(words * world, dtype=torch.int32)
+
+        def host_write(x):  # abnn_set_last_visited of a contiguous range
+            _, (first, n), ahead = AHEAD
+            x.set_last_visited(np.full(n, x.clock + ahead, np.uint64), first)
+
         for k in range(PASSES):
             if k == 6:
                 ob.set_reward(0.25)
+            if track and k == AHEAD[0]:
+                host_write(ob)
             sharded_pass(eng, comm, xchg, gathered)
-        if track:  # lazy lastVisited merge (all-reduce MAX)
-            t = torch.from_numpy(ob.last_visited.view(np.int64).copy())
-            comm.all_reduce_max(t)
-            ob.last_visited[:] = t.numpy().view(np.uint64)
+        merge_visits(eng, comm)  # the lazy merge before lastVisited is read
 
         # unsharded reference, computed independently on every rank
         ref = O.OracleBrain(256, 256, N_HIDDEN, N_SYN, events if world == 1 else N_SYN,
-                            track_visits=track)
+                            track_visits=track, **extra)
         ref.build_random_graph(seed=11, nthreads=2)
         ref.set_auto_stimulus(0, 256)
         for k in range(PASSES):
             if k == 6:
                 ref.set_reward(0.25)
+            if track and k == AHEAD[0]:
+                host_write(ref)
             ref.pass_serial()
+        if renorm:
+            assert ref.renormalisations() >= 2 and ob.renormalisations() == ref.renormalisations()
         assert np.array_equal(ob.syn.view(np.uint32), ref.syn[lo:hi].view(np.uint32))
         assert np.array_equal(ob.last_fired, ref.last_fired)
         assert ob.clock == ref.clock
@@ -90,11 +118,13 @@ def _worker(rank, world, port, events, track):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,track", [(2, 0), (3, 0), (2, 1)])
-def test_sharded_gloo_equals_unsharded(world, track):
+@pytest.mark.parametrize("world,track,renorm", [(2, 0, 0), (3, 0, 0), (2, 1, 0), (2, 1, 2), (3, 1, 2)])
+def test_sharded_gloo_equals_unsharded(world, track, renorm):
     # events >= every shard's size: each shard sweeps its whole range, so the
-    # rank-ordered union is the unsharded full sweep
-    mp.spawn(_worker, args=(world, _free_port(), N_SYN, track), nprocs=world, join=True)
+    # rank-ordered union is the unsharded full sweep.  track + renorm: the
+    # lastVisited merge across renormalisations (the clock goes back to 0
+    # after passes 3 and 7) and a host write ahead of the clock
+    mp.spawn(_worker, args=(world, _free_port(), N_SYN, track, renorm), nprocs=world, join=True)
 
 
 SP = dict(w_prune=0.105, p_new=0.35, w_init=0.5, compact_every=2)

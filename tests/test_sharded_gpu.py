@@ -69,7 +69,10 @@ def test_native_rccl_shard_traverse_world1(gpu, monkeypatch):
     monkeypatch.setenv("MASTER_PORT", str(_port()))
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
-        extra = dict(w_prune=0.105, p_new=0.35, w_init=0.5, compact_every=4, track_visits=1)
+        # track_visits with renormalisations after passes 5 and 11 (the
+        # library merges lastVisited after each, over RCCL) and a host write
+        # ahead of the clock before pass 7
+        extra = dict(w_prune=0.105, p_new=0.35, w_init=0.5, compact_every=4, track_visits=1, renorm_thresh=4)
         n_syn, events, passes = 1_000_000, 1_000_000, 13
         sb = ShardedBrain(TorchComm(), 256, 256, 30_000, n_syn, events, device=0, capacity_factor=1.05,
                           native=True, **extra)
@@ -78,10 +81,15 @@ def test_native_rccl_shard_traverse_world1(gpu, monkeypatch):
             b.build_random_graph(4)
             b.set_auto_stimulus(0, 256)
             b.set_reward(0.25)
-        sb.step(passes)
-        ref.encode_traversal(passes)
+        sb.step(7)
+        ref.encode_traversal(7)
+        for b in (sb.brain, ref):
+            b.set_last_visited(np.full(8400, b.scalars()["clock"] + 2, np.uint64), 600)
+        sb.step(passes - 7)
+        ref.encode_traversal(passes - 7)
         sb.sync_visits()
         ref.synchronize()
+        assert sb.brain.renormalisations() == ref.renormalisations() == 2
         assert sb.brain.structural_updates() == ref.structural_updates() == 3
         assert np.array_equal(sb.brain.download_synapses().view(np.uint32), ref.download_synapses().view(np.uint32))
         assert np.array_equal(sb.brain.last_fired(), ref.last_fired())
