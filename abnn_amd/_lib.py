@@ -71,7 +71,7 @@ class Scalars(C.Structure):
 
 MODE_SWEEP, MODE_RANDOM = 0, 1  # abnn_params.mode (include/abnn/abnn.h)
 ABI_VERSION = 9
-LAYOUT_VERSION = 3
+LAYOUT_VERSION = 4
 
 
 class Stats(C.Structure):

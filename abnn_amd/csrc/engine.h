@@ -70,20 +70,20 @@ constexpr uint32_t kLbSpinLimit = 1u << 22;  // ~1 s of polls: then error, never
 // i is {src[i], dst[i], w[i]} (SynapsePacked without its never-read pad).
 // src is held in 24 bits (N_NRN < 2^24 - 1, checked at create; the tombstone
 // src is kSrcNone) as two streams, so the sweep's gate reads 3 B per visited
-// event: a u16 word lo[i] and a u8 byte hi[hi_pos(i)], together the *filter
-// code* of src -- a bijection of the 24 bits laid out so that the gate's
-// pre-spike filter test (kernels.hip, filter_t / filter_set) needs no hashing:
+// event: a u16 word lo[i] and a u8 byte hi[i], together the *filter code* of
+// src -- a bijection of the 24 bits laid out so that the gate's pre-spike
+// filter test (kernels.hip, quad_filter / filter_set) needs no hashing:
 // neuron n = 32 j + b sits in filter block g = (j ^ t) mod 8192,
 // t = 0x9E5 (j >> 13), at low bit lb = b and high bit hb = (b + t) mod 32;
 //   lo = g << 3 | hb[2:0]                 (lo & 0xFFF8 = the block's LDS byte address)
 //   hi = lb | x << 5 | hb[4:3] << 6       (x = bit 5 of j >> 13, i.e. n >= 2^23)
-// lo is in natural order, hi permuted within every 256-record group so that
-// the one 4-B hi word a gate lane loads per group holds the four records of
-// its two lo words:
-//   group G = i / 256, r = i % 256, kh = r / 128, lane = (r % 128) / 2, s = r % 2
-//   hi byte at 256 G + 4 lane + 2 kh + s                           (hi_pos)
+// Record layout 4: both streams in natural record order; a gate lane loads
+// 8 consecutive records' lo words (16 B) and hi bytes (8 B) per 512-record
+// block (lane-contiguous events: lane order is event order within a block,
+// kernels.hip k_gate).  Layout 3 permuted hi within 256-record groups for a
+// lane-interleaved gate.
 // Each array holds capacity + kDummyRecords entries (zero padding: the gate's
-// last iteration reads past the sweep; hi rounded up to whole groups).
+// last iteration reads past the sweep; hi rounded up to whole 256-record groups).
 constexpr uint32_t kSrcNone = 0xFFFFFFu;   // 24-bit tombstone src (downloads as 0xFFFFFFFF)
 constexpr uint64_t kMaxNeurons = kSrcNone; // N_NRN < 2^24 - 1
 constexpr uint32_t kCodeFilterWords = 8192; // the filter the code is laid out for (sweep gate shapes)
@@ -115,10 +115,7 @@ struct SynArrays {
 // w of record i inside its {dst, w} pair
 __host__ __device__ inline float* w_ptr(const SynArrays& a, uint64_t i) { return reinterpret_cast<float*>(a.dw + i) + 1; }
 
-__host__ __device__ inline uint64_t hi_pos(uint64_t i)
-{
-    return (i & ~255ull) | ((i >> 1) & 63ull) << 2 | ((i >> 7) & 1ull) << 1 | (i & 1ull);
-}
+__host__ __device__ inline uint64_t hi_pos(uint64_t i) { return i; }  // layout 4: natural order
 
 __host__ __device__ inline uint64_t hi_bytes(uint64_t count) { return (count + 255) & ~255ull; }
 

@@ -224,6 +224,9 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total, uint64_t* 
     return before + inc - v;
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // (the nontemporal builtins take vector types)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ uint64_t range_begin(uint32_t b, uint32_t iters, uint32_t G)
 {
     return (uint64_t)b * iters / G;
@@ -285,6 +288,65 @@ __device__ __forceinline__ void filter_test(const uint2 f, uint32_t v, uint32_t&
         ABNN_SHR_BYTE(HB, hb, f.y, "BYTE_3", "DWORD", "UNUSED_PRESERVE");
     }
 }
+// Lane-contiguous sweep (record layout 4, engine.h): a lane's 8 events of a
+// 512-event block come as four lo dwords (event k's lo in half k & 1 of dword
+// k >> 1) and two hi dwords (event k's hi in byte k & 3 of dword k >> 2).
+// The filter block's LDS byte address of the event in half `half` of lo
+// dword w: lo & 0xFFF8 (SDWA word select for the high half: one VALU).
+__device__ __forceinline__ uint32_t code_addr(uint32_t w, int half)
+{
+    if (half == 0) return w & 0xFFF8u;
+    uint32_t a;
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+        : "=v"(a) : "v"(w), "v"(0xFFF8u));
+    return a;
+}
+
+__device__ __forceinline__ uint2 filter_block_at(const uint2* s_fb, uint32_t addr)
+{
+    return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s_fb) + addr);
+}
+
+// The filter test of four consecutive events of a lane (blocks f[0..3]; lo
+// dwords w0 = events 0, 1 and w1 = events 2, 3; hi dword h): bit 0 of byte m
+// of the result is set iff event m passes.  lb = hi[4:0] is the shift amount
+// straight from hi's byte m (SDWA src0_sel); hb = lo[2:0] | hi[7:6] << 3 for
+// all four at once: one v_perm gathers the lo bytes, one v_bfi inserts
+// hi >> 3 (bits 5..7 of each byte are don't-cares: shifts use [4:0]).  4 VALU
+// per event (the layout-3 gate took 6.25: a v_perm per event to assemble the
+// code, a shift and a v_bfi for hb).
+#define ABNN_SHR_SEL(acc, amt, val, BYTE, KEEP)                                                       \
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:" BYTE " dst_unused:" KEEP " src0_sel:" BYTE           \
+        " src1_sel:DWORD"                                                                             \
+        : "+v"(acc)                                                                                   \
+        : "v"(amt), "v"(val))
+__device__ __forceinline__ uint32_t quad_filter(const uint2* f, uint32_t w0, uint32_t w1, uint32_t h)
+{
+    const uint32_t A = __builtin_amdgcn_perm(w1, w0, 0x06040200u);  // lo[7:0] of events 0..3
+    const uint32_t R = (A & 0x07070707u) | ((h >> 3) & ~0x07070707u);  // byte m: hb of event m
+    uint32_t HA, HB;
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+        : "=v"(HA) : "v"(h), "v"(f[0].x));
+    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+        : "=v"(HB) : "v"(R), "v"(f[0].y));
+    ABNN_SHR_SEL(HA, h, f[1].x, "BYTE_1", "UNUSED_PRESERVE");
+    ABNN_SHR_SEL(HB, R, f[1].y, "BYTE_1", "UNUSED_PRESERVE");
+    ABNN_SHR_SEL(HA, h, f[2].x, "BYTE_2", "UNUSED_PRESERVE");
+    ABNN_SHR_SEL(HB, R, f[2].y, "BYTE_2", "UNUSED_PRESERVE");
+    ABNN_SHR_SEL(HA, h, f[3].x, "BYTE_3", "UNUSED_PRESERVE");
+    ABNN_SHR_SEL(HB, R, f[3].y, "BYTE_3", "UNUSED_PRESERVE");
+    return HA & HB & 0x01010101u;
+}
+#undef ABNN_SHR_SEL
+
+// The stored code (lo | hi << 16) of event k of a lane's block from its lo
+// dword w (= lo dword k >> 1) and hi dword v (= hi dword k >> 2).
+__device__ __forceinline__ uint32_t code_at(uint32_t w, uint32_t v, int k)
+{
+    const uint32_t s = 2u * (uint32_t)(k & 1);
+    return __builtin_amdgcn_perm(v, w, 0x0C000000u | (4u + (uint32_t)(k & 3)) << 16 | (s + 1u) << 8 | s);
+}
+
 __device__ __forceinline__ void filter_set(uint32_t* f, uint32_t j, uint32_t bits, uint32_t FB, uint32_t lg)
 {
     const uint32_t t = filter_t(j, lg), g = (j ^ t) & (FB - 1), r = t & 31u;
@@ -1333,10 +1395,10 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     constexpr int NW = BLOCK / 64;
     constexpr uint32_t IE = 64 * K;
     constexpr int KD = kTrack ? K : 1;                 // dst words in flight (track_visits)
-    constexpr int NG = K / 4;                          // sweep: 256-event groups per iteration
+    constexpr int NB8 = K / 8;                         // sweep: 512-event blocks per iteration
     constexpr uint32_t LG = __builtin_ctz(FW);
     constexpr uint32_t SE = kChunk + 128;              // a chunk + one staging step (<= 128 events)
-    static_assert(K % 4 == 0, "the packed src stream is read in 256-event groups");
+    static_assert(K % 8 == 0, "the packed src stream is read in 512-event blocks (8 events per lane)");
     static_assert(kRandom || FW == kCodeFilterWords, "the sweep tests the stored code (engine.h, src_code)");
     static_assert(IE <= (uint32_t)kDummyRecords, "dummy block / padding must cover one iteration");
     static_assert(!(kFused && kRandom), "the fused pass is sweep-mode only");
@@ -1406,17 +1468,26 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     if (kFused && !d.shard_mode && spec_wgs + 3u + gridDim.x / 4u <= gridDim.x) hw0 = spec_wgs + 3u;
     uint32_t* st_off = s_stage[wid];
     uint32_t* st_src = s_stage[wid] + SE;
-    // Records in flight.  Sweep: the packed src stream (engine.h, SynArrays):
-    // per 256-event group g a lane holds two lo words (events 128 kh + 2 lane
-    // + {0, 1}, kh = 0, 1) and one hi word (the same four events' bits
-    // 16..23), 3 B per event.  Random mode: per event k (t = 64 k + lane) the
-    // u32 src of its picked record (the src32 mirror).
+    // Records in flight.  Sweep (layout 4, engine.h SynArrays): lane-
+    // contiguous -- per 512-event block b of an iteration, lane L holds events
+    // 512 b + 8 L .. 8 L + 7: their eight lo words in one 16-B load and their
+    // eight hi bytes in one 8-B load, 3 B per event, both in natural record
+    // order (a wave-instruction reads 1 KiB / 512 B contiguous).  Random mode:
+    // per event k (t = 64 k + lane) the u32 src of its picked record (the
+    // src32 mirror).
     // kDepth iterations of records in flight per wave (sweep: two, ping-pong
     // buffers A/B; a wave's memory-level parallelism bounds its stream rate)
     constexpr int kDepth = (kRandom || kTrack) ? 1 : 2;
-    struct Recs {
-        uint32_t s[kRandom ? K : 2 * NG], h[NG], dd[KD];
+    struct RecsSweep {
+        u32x4 lo[NB8];
+        u32x2 hi[NB8];
+        uint32_t dd[KD];
     };
+    struct RecsRandom {
+        uint32_t s[K];
+        uint32_t dd[KD];
+    };
+    using Recs = std::conditional_t<kRandom, RecsRandom, RecsSweep>;
     Recs A, B;
     const uint64_t pass = kRandom ? sload(d.pass_index) : 0;
     auto issue = [&](Recs& x, uint64_t it, bool live) __attribute__((always_inline)) {
@@ -1433,24 +1504,26 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             }
         } else {
             // wave-uniform bases; past the range the zero dummy block
-            const uint32_t* bl = live ? reinterpret_cast<const uint32_t*>(d.syn.lo) + it * (IE / 2) : d.dummy;
-            const uint32_t* bh = live ? reinterpret_cast<const uint32_t*>(d.syn.hi) + it * (IE / 4) : d.dummy;
+            const u32x4* bl = live ? reinterpret_cast<const u32x4*>(d.syn.lo) + it * (IE / 8)
+                                   : reinterpret_cast<const u32x4*>(d.dummy);
+            const u32x2* bh = live ? reinterpret_cast<const u32x2*>(d.syn.hi) + it * (IE / 8)
+                                   : reinterpret_cast<const u32x2*>(d.dummy);
 #pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                x.s[2 * g] = __builtin_nontemporal_load(bl + g * 128 + lane);
-                x.s[2 * g + 1] = __builtin_nontemporal_load(bl + g * 128 + 64 + lane);
-                x.h[g] = __builtin_nontemporal_load(bh + g * 64 + lane);
+            for (int b = 0; b < NB8; ++b) {
+                x.lo[b] = __builtin_nontemporal_load(bl + b * 64 + lane);
+                x.hi[b] = __builtin_nontemporal_load(bh + b * 64 + lane);
             }
-            if constexpr (kTrack) {  // dst of the same events: one 16-B {dst, w} pair per (g, kh)
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            if constexpr (kTrack) {  // dst of the same events: 8 {dst, w} pairs per lane and block
                 const u32x4* bd = reinterpret_cast<const u32x4*>(live ? reinterpret_cast<const uint32_t*>(d.syn.dw + (uint64_t)it * IE)
                                                                       : d.dummy);
 #pragma unroll
-                for (int j = 0; j < 2 * NG; ++j) {
-                    const u32x4 v = __builtin_nontemporal_load(bd + j * 64 + lane);
-                    x.dd[2 * j] = v.x;
-                    x.dd[2 * j + 1] = v.z;
-                }
+                for (int b = 0; b < NB8; ++b)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const u32x4 v = __builtin_nontemporal_load(bd + b * 256 + lane * 4 + j);
+                        x.dd[8 * b + 2 * j] = v.x;
+                        x.dd[8 * b + 2 * j + 1] = v.z;
+                    }
             }
         }
     };
@@ -1475,7 +1548,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // would wait for vmcnt(0): the records' whole round trip, and until
         // round 4 the prologue's zeroing stores too, before the stream began.)
         // (kTrack: the {dst, w} pairs of the same events too, one iteration deep)
-        constexpr int kRecLoads = kDepth * (3 * NG + (kTrack ? 2 * NG : 0));
+        constexpr int kRecLoads = kDepth * (kRandom ? K * (kTrack ? 2 : 1) : NB8 * (2 + (kTrack ? 4 : 0)));
         __builtin_amdgcn_sched_barrier(0);
         wait_vm_lgkm0<kRecLoads>();
         __builtin_amdgcn_s_barrier();
@@ -1537,51 +1610,34 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         chunk_t += (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc);
     };
     auto step = [&](Recs& x, uint32_t it) __attribute__((always_inline)) {
-        // src[k] of event idx(k) of this iteration: sweep k = 4 g + 2 kh + s,
-        // idx = 256 g + 128 kh + 2 lane + s (v_perm: lo half s, hi byte 2 kh + s);
-        // random k: idx = 64 k + lane
-        auto idx_of = [&](int k) -> uint32_t {
-            return kRandom ? (uint32_t)(k * 64) + lane : (uint32_t)((k >> 2) * 256 + ((k >> 1) & 1) * 128 + (k & 1)) + 2 * lane;
-        };
-        uint32_t src[K];
-        uint32_t dst[KD];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if constexpr (kRandom) {
-                src[k] = x.s[k];
-            } else {
-                const int g = k >> 2, kh = (k >> 1) & 1, sh = k & 1;
-                const uint32_t sel = 0x0C000000u | (uint32_t)(4 + 2 * kh + sh) << 16 | (uint32_t)(2 * sh + 1) << 8 | (uint32_t)(2 * sh);
-                src[k] = __builtin_amdgcn_perm(x.h[g], x.s[2 * g + kh], sel);
-            }
-        }
         // The SIMD arbiter issues strictly by priority, then age: with a fixed
         // order the last of a SIMD's four waves streams ~15 % slower than the
         // first.  Rotating every wave through the four ranks every four
         // iterations equalises them (tools/ubench_soa.hip, profiles/r01p_*).
         if (((it - it_begin) & 3u) == 0) set_priority((uint32_t)((it - it_begin) >> 2) + wid / 4u);
+        uint32_t dst[KD];
 #pragma unroll
         for (int k = 0; k < KD; ++k) dst[k] = kTrack ? x.dd[k] : 0u;
-        issue(x, it + kDepth, it + kDepth < it_end);  // the buffer's next iteration in flight first
         const uint64_t base = (uint64_t)it * IE;
-        uint32_t vmask = (K == 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);  // events of this lane that exist
-        if (base + IE > d.events) {  // only the sweep's last iteration
-            vmask = 0;
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (base + idx_of(k) < d.events) vmask |= 1u << k;
-        }
-
-        // Pre-spike filter (brain.metal:73-77 pre-selection).  Random mode:
-        // every event's block read back to back; the block index is masked,
-        // so any src (tombstones included) stays in bounds; ubfe takes the bit
-        // offset mod 32: low bit src mod 32, high bit (src + t) mod 32 =
-        // (b + r) mod 32.  Sweep: src[k] is the record's code, tested by
-        // filter_test (every block address is below 64 KiB); the hit of event
-        // k is bit 0 of byte k % 4 of H[k / 4] (fm is not formed).
-        uint32_t fm = 0;
-        uint32_t H[kRandom ? 1 : K / 4];
+        const uint32_t rel = (uint32_t)(base - region);
+        const bool last = base + IE > d.events;  // only the sweep's last iteration (wave-uniform)
         if constexpr (kRandom) {
+            // event k of this lane: idx = 64 k + lane (event order = (k, lane))
+            uint32_t src[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) src[k] = x.s[k];
+            issue(x, it + kDepth, it + kDepth < it_end);  // the buffer's next iteration in flight first
+            uint32_t vmask = (K == 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);  // events of this lane that exist
+            if (last) {
+                vmask = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (base + (uint32_t)(k * 64) + lane < d.events) vmask |= 1u << k;
+            }
+            // Pre-spike filter (brain.metal:73-77 pre-selection): every
+            // event's block read back to back; the block index is masked, so
+            // any src (tombstones included) stays in bounds; ubfe takes the
+            // bit offset mod 32: low bit src mod 32, high bit (src + t) mod 32
             uint2 fb[K];
             uint32_t ft[K];
 #pragma unroll
@@ -1589,93 +1645,149 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 ft[k] = filter_t(src[k] >> 5, LG);
                 fb[k] = s_fb[((src[k] >> 5) ^ ft[k]) & (FW - 1)];
             }
+            uint32_t fm = 0;
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 fm |= (__builtin_amdgcn_ubfe(fb[k].x, src[k], 1) & __builtin_amdgcn_ubfe(fb[k].y, src[k] + ft[k], 1)) << k;
             fm &= vmask;
-        } else {
-            // every block read issued before the first test: the reads are
-            // independent, and each one waited for (the round-3 code let the
-            // compiler reuse one register pair, so the eight 8-B LDS reads of
-            // an iteration ran one after another, each behind its bank
-            // conflicts: SQ_LDS_BANK_CONFLICT is half of SQ_LDS_IDX_ACTIVE).  Measured
-            // equal in time (profiles/r04c_*): the waves' waits became issue
-            // stalls -- the stream loop is issue-bound on its SIMD
-            uint2 fb[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) fb[k] = filter_block(s_fb, src[k]);
-#pragma unroll
-            for (int g = 0; g < K / 4; ++g) {
-                uint32_t HA, HB;
-                filter_test<0>(fb[4 * g], src[4 * g], HA, HB);
-                filter_test<1>(fb[4 * g + 1], src[4 * g + 1], HA, HB);
-                filter_test<2>(fb[4 * g + 2], src[4 * g + 2], HA, HB);
-                filter_test<3>(fb[4 * g + 3], src[4 * g + 3], HA, HB);
-                H[g] = HA & HB & 0x01010101u;
-            }
-            if (base + IE > d.events) {  // only the sweep's last iteration (wave-uniform)
-#pragma unroll
-                for (int g = 0; g < K / 4; ++g) {
-                    const uint32_t m = vmask >> (4 * g);
-                    H[g] &= (m & 1u) | (m & 2u) << 7 | (m & 4u) << 14 | (m & 8u) << 21;
-                }
-            }
-        }
-        auto hit = [&](int k) -> bool {
-            if constexpr (kRandom) return (fm >> k) & 1u;
-            else return (H[k >> 2] >> (8 * (k & 3))) & 1u;
-        };
-
-        if constexpr (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (((vmask >> k) & 1u) && dst[k] < nn) d.last_visited[dst[k]] = now;
-            // a shard handle also marks the neuron visited since the last
-            // lastVisited merge (k_visits_delta)
-            if (d.visit_mark) {
+            if constexpr (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if (((vmask >> k) & 1u) && dst[k] < nn) d.visit_mark[dst[k]] = 1u;
-            }
-        }
-        if constexpr (!kRandom) {
+                    if (((vmask >> k) & 1u) && dst[k] < nn) d.last_visited[dst[k]] = now;
+                // a shard handle also marks the neuron visited since the last
+                // lastVisited merge (k_visits_delta)
+                if (d.visit_mark) {
 #pragma unroll
-            for (int g = 0; g < K / 4; ++g) fm |= H[g];
-        }
-        if (__ballot(fm != 0) == 0) return;
-        const uint32_t rel = (uint32_t)(base - region);
-        if constexpr (kRandom) {  // event order = (k, lane)
+                    for (int k = 0; k < K; ++k)
+                        if (((vmask >> k) & 1u) && dst[k] < nn) d.visit_mark[dst[k]] = 1u;
+                }
+            }
+            if (__ballot(fm != 0) == 0) return;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const bool h = (fm >> k) & 1u;
                 const uint64_t b1 = __ballot(h);
                 if (h) {
                     const uint32_t q = pend + mbcnt64(b1);
-                    st_off[q] = rel + idx_of(k);
+                    st_off[q] = rel + (uint32_t)(k * 64) + lane;
                     st_src[q] = src[k];
                 }
                 pend += (uint32_t)__popcll(b1);
                 if (pend >= kChunk) chunk_out();  // a k-step stages at most 64
             }
-        } else {  // event order = (lane, s) within each (g, kh) step of 128 events
+        } else {
+            // this iteration's words (the buffer is refilled right away)
+            u32x4 lo[NB8];
+            u32x2 hi[NB8];
 #pragma unroll
-            for (int j = 0; j < 2 * NG; ++j) {
-                const bool h0 = hit(2 * j), h1 = hit(2 * j + 1);
-                const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
-                if ((b0 | b1) == 0) continue;  // wave-uniform
-                const uint32_t q = pend + mbcnt64(b0) + mbcnt64(b1);
-                if (h0) {
-                    st_off[q] = rel + idx_of(2 * j);
-                    st_src[q] = src[2 * j];
+            for (int b = 0; b < NB8; ++b) {
+                lo[b] = x.lo[b];
+                hi[b] = x.hi[b];
+            }
+            issue(x, it + kDepth, it + kDepth < it_end);  // the buffer's next iteration in flight first
+            // Pre-spike filter (brain.metal:73-77 pre-selection) on the stored
+            // codes (engine.h, src_code), every block read issued before the
+            // first test (the reads are independent; SQ_LDS_BANK_CONFLICT is
+            // half of SQ_LDS_IDX_ACTIVE, so they queue): 4 VALU per event
+            // (quad_filter), no v_perm to assemble the codes
+            uint2 fb[K];
+#pragma unroll
+            for (int b = 0; b < NB8; ++b) {
+                const uint32_t w[4] = {lo[b].x, lo[b].y, lo[b].z, lo[b].w};
+#pragma unroll
+                for (int k = 0; k < 8; ++k) fb[8 * b + k] = filter_block_at(s_fb, code_addr(w[k >> 1], k & 1));
+            }
+            uint32_t H[2 * NB8];  // bit 0 of byte m of H[2 b + q]: event 8 L + 4 q + m of block b passed
+#pragma unroll
+            for (int b = 0; b < NB8; ++b) {
+                H[2 * b] = quad_filter(fb + 8 * b, lo[b].x, lo[b].y, hi[b].x);
+                H[2 * b + 1] = quad_filter(fb + 8 * b + 4, lo[b].z, lo[b].w, hi[b].y);
+            }
+            if (last) {  // events past the sweep pass nothing
+#pragma unroll
+                for (int b = 0; b < NB8; ++b) {
+                    const uint64_t e0 = base + 512u * b + 8u * lane;
+                    const uint32_t nv = e0 >= d.events ? 0u : (uint32_t)std::min<uint64_t>(8u, d.events - e0);
+                    H[2 * b] &= nv >= 4 ? 0xFFFFFFFFu : (1u << (8 * nv)) - 1u;
+                    H[2 * b + 1] &= nv >= 8 ? 0xFFFFFFFFu : nv <= 4 ? 0u : (1u << (8 * (nv - 4))) - 1u;
                 }
-                if (h1) {
-                    st_off[q + h0] = rel + idx_of(2 * j + 1);
-                    st_src[q + h0] = src[2 * j + 1];
+            }
+            if constexpr (kTrack) {  // README §4: lastVisited[dst] = now (never read by a decision)
+#pragma unroll
+                for (int b = 0; b < NB8; ++b) {
+                    const uint64_t e0 = base + 512u * b + 8u * lane;
+                    const uint32_t nv = !last ? 8u : e0 >= d.events ? 0u : (uint32_t)std::min<uint64_t>(8u, d.events - e0);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if ((uint32_t)k < nv && dst[8 * b + k] < nn) d.last_visited[dst[8 * b + k]] = now;
+                    // a shard handle also marks the neuron visited since the
+                    // last lastVisited merge (k_visits_delta)
+                    if (d.visit_mark) {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            if ((uint32_t)k < nv && dst[8 * b + k] < nn) d.visit_mark[dst[8 * b + k]] = 1u;
+                    }
                 }
-                pend += (uint32_t)(__popcll(b0) + __popcll(b1));
-                if (kFused ? pend >= d.flush_at : pend >= kChunk) {  // a step stages at most 128
-                    if constexpr (kFused) flush_all();
-                    else chunk_out();
+            }
+            // Staging in event order.  Event order within a block is (lane,
+            // k), so a lane's hits go to consecutive slots from the exclusive
+            // prefix of the per-lane hit counts, in k order: round j writes
+            // every lane's j-th hit (ffbl, then cleared).  In the steady state
+            // (~0.7 % of events pass) no lane holds two hits: one mbcnt is the
+            // prefix and one round places them all; else (a lane with 2+
+            // hits: ~8 % of blocks, and the dense input->output stretch) four
+            // bit-plane ballots give the prefix and the rounds repeat.  A
+            // block that would overflow the stage (dense) goes in 128-event
+            // quarters (16 lanes each), the stage flushed between them.
+            // (Runtime loops, not unrolled: the compiler hoisted an unrolled
+            // slow path's per-event work in front of the common case.)
+#pragma unroll
+            for (int b = 0; b < NB8; ++b) {
+                const uint32_t xb = H[2 * b] | (H[2 * b + 1] << 1);  // event 4 q + m at bit 8 m + q
+                const uint64_t bb = __ballot(xb != 0);
+                if (bb == 0) continue;  // wave-uniform
+                const uint32_t relb = rel + 512u * b + 8u * lane;  // this lane's first event of the block
+                const uint32_t cb = __builtin_popcount(xb);
+                uint32_t P, tot;  // exclusive prefix of the counts, their total
+                if (__ballot(cb > 1u) == 0) {
+                    P = mbcnt64(bb);
+                    tot = (uint32_t)__popcll(bb);
+                } else {
+                    P = 0;
+                    tot = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {  // counts <= 8: four bit planes
+                        const uint64_t bi = __ballot((cb >> i) & 1u);
+                        P += mbcnt64(bi) << i;
+                        tot += (uint32_t)__popcll(bi) << i;
+                    }
+                }
+                const bool split = pend + tot > SE;  // wave-uniform (dense)
+                const uint32_t w0 = lo[b].x, w1 = lo[b].y, w2 = lo[b].z, w3 = lo[b].w, v0 = hi[b].x, v1 = hi[b].y;
+#pragma unroll 1
+                for (uint32_t u = 0; u < (split ? 4u : 1u); ++u) {  // wave-uniform
+                    const uint32_t p0 = split ? (uint32_t)__builtin_amdgcn_readlane((int)P, (int)(16u * u)) : 0u;
+                    const uint32_t p1 = !split || u == 3 ? tot
+                                                         : (uint32_t)__builtin_amdgcn_readlane((int)P, (int)(16u * u + 16u));
+                    uint32_t xr = !split || (lane >> 4) == u ? xb : 0u;
+                    uint32_t q = pend + P - p0;
+                    do {  // one round: every lane's next hit (wave-uniform trip count)
+                        if (xr) {
+                            const uint32_t pos = __builtin_ctz(xr), m = pos >> 3;
+                            const bool hs = pos & 1u;  // the block's second quad (events 4..7)
+                            xr &= xr - 1u;
+                            const uint32_t e0 = hs ? w2 : w0, e1 = hs ? w3 : w1;
+                            const uint32_t lo16 = __builtin_amdgcn_perm(e1, e0, 0x0C0C0100u + m * 0x0202u);
+                            st_off[q] = relb + (hs ? 4u : 0u) + m;
+                            st_src[q] = __builtin_amdgcn_perm(hs ? v1 : v0, lo16, 0x0C040100u + (m << 16));
+                            ++q;
+                        }
+                    } while (__ballot(xr != 0) != 0);
+                    pend += p1 - p0;
+                    if (kFused ? pend >= d.flush_at : pend >= kChunk) {  // at most 128 past the threshold
+                        if constexpr (kFused) flush_all();
+                        else chunk_out();
+                    }
                 }
             }
         }

@@ -74,6 +74,8 @@ def parse():
                     help="at one GPU, run the sharded pass (abnn_shard_traverse over the library's RCCL "
                          "communicator, world 1) instead of the fused single-GPU pass: its per-pass "
                          "overhead (DESIGN.md §7)")
+    ap.add_argument("--no-reference-layout", action="store_true",
+                    help="skip the reference_layout sub-object of the default run")
     ap.add_argument("--raw", action="store_true",
                     help="the reference-layout path: abnn_launch_traversal (brain.metal's 14-buffer ABI) over "
                          "caller-owned 16-B SynapsePacked records and u32 lastF at the config's sweep "
@@ -195,8 +197,8 @@ def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, ex
                       f"(cgroup quota {hc['cgroup_quota_cpus']} CPUs)"}
 
 
-def raw_main(args) -> None:
-    """--raw: one step = one pass of abnn_launch_traversal over caller-owned
+def raw_run(config: str, events_arg: int, settle: int, warmup: int, steps: int) -> dict:
+    """One step = one pass of abnn_launch_traversal over caller-owned
     buffers in the reference's layouts (brain.cpp:52-69): the host's two
     writes of encode_traversal / inject_inputs (lastF[inputs] = clock,
     budget = kMaxSpikes; brain.cpp:82,90) as two tiny torch kernels, then
@@ -209,8 +211,8 @@ def raw_main(args) -> None:
 
     from abnn_amd import CONFIGS, Brain, _lib
 
-    wl = CONFIGS[args.config]
-    events = args.events or wl.events
+    wl = CONFIGS[config]
+    events = events_arg or wl.events
     E = min((events + 255) // 256 * 256, wl.n_syn)
     dev = torch.device("cuda", 0)
     lib = _lib.load()
@@ -246,10 +248,10 @@ def raw_main(args) -> None:
                 raise RuntimeError("abnn_launch_traversal failed")
 
     ts = time.perf_counter()
-    step(args.settle)
+    step(settle)
     torch.cuda.synchronize()
     settle_s = time.perf_counter() - ts
-    step(args.warmup)
+    step(warmup)
     torch.cuda.synchronize()
     g = (C.c_uint64 * 2)()
     lib.abnn_debug_raw_gate_timing(1)
@@ -257,7 +259,7 @@ def raw_main(args) -> None:
     g1 = g2 = 0
     t0 = time.perf_counter()
     ev_a.record()
-    step(args.steps)
+    step(steps)
     ev_b.record()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -278,14 +280,14 @@ def raw_main(args) -> None:
     traffic, traffic_note = load_traffic("raw_" + wl.name)
     out = {
         "metric": "traversal events/sec at 1B synapses, 5M neurons; achieved HBM GB/s",
-        "value": E * args.steps / dt, "unit": "events/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+        "value": E * steps / dt, "unit": "events/s", "n_gpus": 1, "steps": steps,
+        "warmup": warmup, "ms_per_step": dt / steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (build_random_graph recipe, portable RNG, generated on GPU)",
         "config": {"workload": f"{wl.name} reference layout: abnn_launch_traversal over caller-owned "
                                f"16-B records ({wl.n_syn:,} x 16 B) and u32 lastF",
                    "n_neuron": n_nrn, "n_syn": wl.n_syn, "visited_events_per_pass": E,
-                   "workspace_bytes": nb, "settle_passes": args.settle, "settle_s": round(settle_s, 3),
+                   "workspace_bytes": nb, "settle_passes": settle, "settle_s": round(settle_s, 3),
                    "last_pass_pre_gated": g1, "last_pass_survivors": g2,
                    "host_writes_per_pass": "lastF[inputs] = clock, budget = kMaxSpikes (2 torch kernels)"},
         "roofline": {
@@ -304,11 +306,33 @@ def raw_main(args) -> None:
             "survey_formula_achieved": round(survey / (avg_gate_ms * 1e-3) / 1e9, 1),
             "survey_formula": "20*E + 4*G1 (SURVEY §8d with u32 lastF: record + lastF[src] per event, "
                               "lastF[dst] per pre-gated; G1 of the last pass)",
-            "pass_ms_events": round(region_ms / args.steps, 4),
+            "pass_ms_events": round(region_ms / steps, 4),
         },
         "cpu_baseline": None,
     }
+    del recs, ws, lastF, lastV
+    torch.cuda.empty_cache()
+    return out
+
+
+def raw_main(args) -> None:
+    """--raw: the reference-layout path (raw_run) as the bench line itself."""
+    out = raw_run(args.config, args.events, args.settle, args.warmup, args.steps)
     print(json.dumps(out), file=_JSON_OUT, flush=True)
+
+
+def reference_layout_summary(config: str, settle: int) -> dict:
+    """The drop-in path over the reference's own buffers (abnn_launch_traversal,
+    16-B records), timed in the same run as the headline line: its pass and
+    gate times and its roofline on 16 B per visited event."""
+    r = raw_run(config, 0, settle, 10, 50)
+    rf = r["roofline"]
+    return {"api": "abnn_launch_traversal (caller-owned 16-B SynapsePacked records, u32 lastF; brain.metal:42-58)",
+            "events_per_s": r["value"], "pass_ms": round(r["ms_per_step"], 4), "steps": r["steps"],
+            "gate_kernel": rf["kernel"], "gate_ms": rf["avg_launch_ms"], "gate_timed_launches": rf["timed_launches"],
+            "bytes_per_pass": rf["algorithmic_bytes_per_launch"], "bytes_formula": rf["bytes_formula"],
+            "achieved_gbs": rf["achieved"], "frac": rf["frac"], "traffic": rf["traffic"],
+            "traffic_source": rf["traffic_source"], "pass_ms_events": rf["pass_ms_events"]}
 
 
 _JSON_OUT = sys.stdout
@@ -476,6 +500,12 @@ def main():
                                if traffic else traffic_note),
             "pass_ms": round(dt / args.steps * 1e3, 4),
         }
+        ref_layout = None
+        if world == 1 and default_run and not args.plasticity and not args.no_reference_layout:
+            brain.close()  # its device memory before the reference-layout buffers (16 GB of records)
+            del step, brain
+            torch.cuda.empty_cache()
+            ref_layout = reference_layout_summary(args.config, args.settle)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             avail = host_cpus()["available"]
@@ -503,7 +533,7 @@ def main():
                 "pre_gated_frac": stats["pre_gated"] / max(1, stats["events"]),
                 "spikes_per_pass": stats["fired"] / max(1, stats["passes"]),
             },
-            "roofline": roofline, "cpu_baseline": cpu,
+            "roofline": roofline, "cpu_baseline": cpu, "reference_layout": ref_layout,
         }
         print(json.dumps(out), file=_JSON_OUT, flush=True)
     if dist is not None:

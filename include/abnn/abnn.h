@@ -219,7 +219,7 @@ typedef struct abnn_state {
  * names the layout (DESIGN.md §4 documents each; ABNN_LAYOUT_VERSION is the
  * one this library writes); arrays[i] = {device pointer, bytes, element
  * bytes, name}.  A caller that does not know `version` must not touch them. */
-#define ABNN_LAYOUT_VERSION 3
+#define ABNN_LAYOUT_VERSION 4
 #define ABNN_LAYOUT_MAX_ARRAYS 4
 typedef struct abnn_array_desc {
     void* ptr;

@@ -160,6 +160,75 @@ def test_c4_eight_virtual_shards_of_the_1b_graph(gpu):
     assert np.float32(o.s.rbar) == np.float32(sf["rbar"]) and o.clock == sf["clock"]
 
 
+def test_c4_random_mode_eight_virtual_shards(gpu):
+    """Config 4's workload in random-edge mode (150M
+    picks per GPU per pass; README §4): the 1B-record graph in 8 shards of
+    125M records, each shard picking 150M records of its own per pass (its own
+    Philox stream, keyed by syn_offset), through the real shard entry points
+    around an in-process all-gather, 6 passes from the fresh graph through
+    the all-gated transient (passes 3-5 gate every pick), reward changed
+    mid-run.  Against the oracle's shard phases on the same 8 shards (run in
+    parallel threads): every shard's checksum over its 125M records, a 10M-
+    record slice of each, lastFired, statistics and scalars."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import abnn_amd
+    from abnn_amd import CONFIGS
+    from abnn_amd.shard import global_events, shard_ranges
+    from oracle import oracle as O
+    from shard_helpers import GpuShards
+
+    wl, world, passes = CONFIGS["c3"], 8, 6
+    kw = dict(mode=1, seed=9)
+    ge = global_events(wl.n_syn, wl.events, world, 1)
+    assert ge == world * wl.events
+    shards, obs = [], []
+    for lo, hi in shard_ranges(wl.n_syn, world):
+        b = abnn_amd.Brain(wl.n_input, wl.n_output, wl.n_hidden, hi - lo, wl.events, syn_offset=lo,
+                           global_events=ge, **kw)
+        b.build_random_graph(1)
+        b.set_auto_stimulus(0, wl.n_input)
+        assert b.visited_events() == wl.events
+        shards.append(b)
+    pool = ThreadPoolExecutor(world)
+
+    def make(r):
+        lo, hi = shard_ranges(wl.n_syn, world)[r]
+        ob = O.OracleBrain(wl.n_input, wl.n_output, wl.n_hidden, hi - lo, wl.events, syn_offset=lo,
+                           global_events=ge, **kw)
+        ob.build_random_graph(1, nthreads=2)
+        ob.set_auto_stimulus(0, wl.n_input)
+        return ob
+
+    obs = list(pool.map(make, range(world)))
+    vs = GpuShards(shards)
+    words = obs[0].exchange_words()
+    gathered = np.zeros(world * words, dtype=np.int32)
+    for k in range(passes):
+        if k == 4:
+            for x in (*shards, *obs):
+                x.set_reward(0.5)
+        vs.pass_()
+        # the oracle's shard phases, the gates (150M picks each) in parallel
+        list(pool.map(lambda r: obs[r].shard_gate(gathered[r * words:(r + 1) * words]), range(world)))
+        list(pool.map(lambda r: obs[r].shard_apply(gathered, world, r), range(world)))
+        for ob in obs:
+            ob.shard_commit(gathered, world)
+    for r, (b, ob) in enumerate(zip(shards, obs)):
+        sg, so = b.scalars(), ob.scalars()
+        assert sg["clock"] == so["clock"] == passes and sg["pass_index"] == so["pass_index"], r
+        assert np.float32(sg["rbar"]) == np.float32(so["rbar"]), r
+        assert b.stats() == ob.stats(), r
+        assert np.array_equal(b.last_fired(), ob.last_fired), r
+        assert b.checksum() == ob.checksum(), r
+        n = 10_000_000
+        first = b.n_syn() - n if r % 2 else 0
+        assert np.array_equal(b.download_synapses(first, n).view(np.uint32),
+                              ob.syn[first:first + n].view(np.uint32)), r
+    st = [b.stats() for b in shards]
+    assert sum(x["fired"] for x in st) >= 2560 * 3 and sum(x["updated"] for x in st) > sum(x["fired"] for x in st)
+
+
 def test_c5_4b_records_plasticity(gpu):
     """Config 5's size on one GPU: 4e9 records (44 GB of packed records; the
     structural update compacts in place), sweep mode, reward 0.25, pruning

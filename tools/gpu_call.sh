@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU call of this round, from named steps (each under its own time limit,
+# the call stops at the first failure; tools/gpu_step.sh):
+#   tests=<pytest selection>  parity tests (-m gpu)
+#   ab=<rounds>               interleaved pass times: in-tree library vs tools/exp/*.so
+#   sq=<name>                 SQ counters of the in-tree library -> gpurun_out/<name>
+#   bench=<name>[:args]       bench.py -> gpurun_out/<name>.json
+#   wc=<file>                 per-wave timelines of 8 fused passes (tools/wc_multi.py)
+#   cal=<file>                FETCH_SIZE calibration (tools/ubench_fetch_cal.hip, prebuilt)
+#   smoke
+# usage: tools/gpu_call.sh step [step ...]
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+(while sleep 50; do date +%s >> gpurun_out/heartbeat.txt; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+for st in "$@"; do
+  key=${st%%=*}; val=${st#*=}
+  case $key in
+    tests) bash tools/gpu_step.sh 900 tests.log python -u -m pytest $val -m gpu -x -v --timeout 600 --timeout-method thread || exit 1
+           grep -q " passed" gpurun_out/tests.log && ! grep -q " failed" gpurun_out/tests.log || { echo "TESTS FAILED"; exit 1; } ;;
+    ab) bash tools/gpu_step.sh 900 ab.txt bash tools/ab_times.sh "$val" || exit 1; cat gpurun_out/ab.txt ;;
+    sq) bash tools/gpu_step.sh 400 "$val.log" bash tools/sq_profile.sh "gpurun_out/$val" || exit 1 ;;
+    bench) name=${val%%:*}; args=""; [ "$name" != "$val" ] && args=${val#*:}
+           timeout -k 10 400 python -u bench.py $args > "gpurun_out/$name.json" 2> "gpurun_out/$name.err" || { echo "bench $name failed"; tail -5 "gpurun_out/$name.err"; exit 1; }
+           python3 tools/bench_line.py "gpurun_out/$name.json" "$name" ;;
+    wc) bash tools/gpu_step.sh 300 "$val" python -u tools/wc_multi.py || exit 1; cat "gpurun_out/$val" ;;
+    cal) bash tools/gpu_step.sh 300 fetch_cal.log timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -T --kernel-trace --output-format csv -d gpurun_out/fcal -o run -- ./tools/ubench_fetch_cal || exit 1
+         python3 tools/fetch_cal.py gpurun_out/fcal | tee "gpurun_out/$val" ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
+           tail -1 gpurun_out/smoke.log ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
