@@ -166,11 +166,6 @@ __device__ __forceinline__ T wave_sum(T v)
     return v;
 }
 
-__device__ __forceinline__ uint32_t wave_total(uint32_t x)
-{
-    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(x), 63);
-}
-
 // Workgroup barrier for LDS communication only: unlike __syncthreads() it does
 // not wait for the wave's outstanding global stores and atomics (a
 // workgroup-scope release fence on global memory waits for vmcnt(0)).
@@ -227,11 +222,6 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total, uint64_t* 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // (the nontemporal builtins take vector types)
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint64_t range_begin(uint32_t b, uint32_t iters, uint32_t G)
-{
-    return (uint64_t)b * iters / G;
-}
-
 // ---------------------------------------------------------------------------
 // Pre-spike filter: a blocked Bloom filter of the exact
 // recent-spike bitmap, FB 64-bit blocks {low, high} (2 FB u32 words, one LDS
@@ -246,48 +236,6 @@ __device__ __forceinline__ uint64_t range_begin(uint32_t b, uint32_t iters, uint
 // refractory stage.
 __device__ __forceinline__ uint32_t filter_t(uint32_t j, uint32_t lg) { return __umul24(j >> lg, 0x9E5u); }
 
-// The sweep's filter test on the stored code v = lo | hi << 16 of one record
-// (engine.h, src_code): the LDS block at v & 0xFFF8, its low half shifted by
-// lb = v[20:16] (SDWA: the shift amount is bits [4:0] of v's high word), its
-// high half by hb = v[2:0] | v[23:22] << 3 (a shift and a bit-field insert);
-// SDWA puts each shift's low byte (bit 0 = the test) into byte DB of the
-// accumulators HA (low halves) and HB (high halves), keeping their other
-// bytes (DB == 0 starts them): the record passes iff bit 0 of byte DB is set
-// in both.  6 VALU per record (the hashed form took 11-12: a multiply, four
-// shifts, an xor and the bit extracts).
-#define ABNN_SHR_BYTE(acc, amt, val, DST, SRC, KEEP)                                              \
-    asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:" DST " dst_unused:" KEEP " src0_sel:" SRC        \
-        " src1_sel:DWORD"                                                                         \
-        : "+v"(acc)                                                                               \
-        : "v"(amt), "v"(val))
-
-// The filter block of code v (one 8-B LDS read).
-__device__ __forceinline__ uint2 filter_block(const uint2* s_fb, uint32_t v)
-{
-    return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s_fb) + (v & 0xFFF8u));
-}
-
-template <int DB>
-__device__ __forceinline__ void filter_test(const uint2 f, uint32_t v, uint32_t& HA, uint32_t& HB)
-{
-    uint32_t hb;  // v's bits 0..2 over (v >> 19)'s: bits 3..4 = v[23:22]
-    asm("v_bfi_b32 %0, 7, %1, %2" : "=v"(hb) : "v"(v), "v"(v >> 19));
-    if constexpr (DB == 0) {
-        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
-            : "=v"(HA) : "v"(v), "v"(f.x));
-        asm("v_lshrrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD"
-            : "=v"(HB) : "v"(hb), "v"(f.y));
-    } else if constexpr (DB == 1) {
-        ABNN_SHR_BYTE(HA, v, f.x, "BYTE_1", "WORD_1", "UNUSED_PRESERVE");
-        ABNN_SHR_BYTE(HB, hb, f.y, "BYTE_1", "DWORD", "UNUSED_PRESERVE");
-    } else if constexpr (DB == 2) {
-        ABNN_SHR_BYTE(HA, v, f.x, "BYTE_2", "WORD_1", "UNUSED_PRESERVE");
-        ABNN_SHR_BYTE(HB, hb, f.y, "BYTE_2", "DWORD", "UNUSED_PRESERVE");
-    } else {
-        ABNN_SHR_BYTE(HA, v, f.x, "BYTE_3", "WORD_1", "UNUSED_PRESERVE");
-        ABNN_SHR_BYTE(HB, hb, f.y, "BYTE_3", "DWORD", "UNUSED_PRESERVE");
-    }
-}
 // Lane-contiguous sweep (record layout 4, engine.h): a lane's 8 events of a
 // 512-event block come as four lo dwords (event k's lo in half k & 1 of dword
 // k >> 1) and two hi dwords (event k's hi in byte k & 3 of dword k >> 2).
@@ -338,14 +286,6 @@ __device__ __forceinline__ uint32_t quad_filter(const uint2* f, uint32_t w0, uin
     return HA & HB & 0x01010101u;
 }
 #undef ABNN_SHR_SEL
-
-// The stored code (lo | hi << 16) of event k of a lane's block from its lo
-// dword w (= lo dword k >> 1) and hi dword v (= hi dword k >> 2).
-__device__ __forceinline__ uint32_t code_at(uint32_t w, uint32_t v, int k)
-{
-    const uint32_t s = 2u * (uint32_t)(k & 1);
-    return __builtin_amdgcn_perm(v, w, 0x0C000000u | (4u + (uint32_t)(k & 3)) << 16 | (s + 1u) << 8 | s);
-}
 
 __device__ __forceinline__ void filter_set(uint32_t* f, uint32_t j, uint32_t bits, uint32_t FB, uint32_t lg)
 {
@@ -578,10 +518,12 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
         uint64_t ld[R];
         uint2 dw[R];
         bool f2[R];
-        // one dependent round trip for both: the exact bitmap word of src
-        // and, for the events the second-level filter passes (LDS: the
-        // recent ones and ~a tenth of the blocked filter's false positives),
-        // the record's {dst, w}
+        // one dependent round trip for both, only for the events the
+        // second-level filter passes (LDS: the recent ones and ~a tenth of the
+        // blocked filter's false positives; it holds every recent neuron, so
+        // it has no false negatives): the exact bitmap word of src and the
+        // record's {dst, w}.  (Round 4 read the bitmap word for every staged
+        // event: each random read costs the CU's vector-memory path)
         if constexpr (!kTail) {
 #pragma unroll
             for (int j = 0; j < R; ++j) {
@@ -590,8 +532,12 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
                 rel[j] = e.x;
                 // the sweep stages the record's code (engine.h, src_code), random mode its src
                 src[j] = kRandom || q >= n ? e.y : code_src(e.y & 0xFFFFu, e.y >> 16);
-                bw[j] = src[j] < nn ? d.bitmap[src[j] >> 5] : 0u;
                 f2[j] = src[j] < nn && f2_test(s_f2, src[j]);
+#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 5  // experiment: no bitmap gather
+                bw[j] = f2[j] ? ~0u : 0u;
+#else
+                bw[j] = f2[j] ? d.bitmap[src[j] >> 5] : 0u;
+#endif
                 dw[j] = f2[j] ? d.syn.dw[record_of(rel[j])] : make_uint2(0xFFFFFFFFu, 0u);  // one access for both
             }
         } else {
@@ -618,17 +564,18 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
             for (int j = 0; j < R; ++j) {
                 const uint32_t sn = src[j] < nn ? src[j] : 0u;
                 f2[j] = src[j] < nn && ((fa[j] >> (f2_hash1(sn) & 31u)) & (fb[j] >> (f2_hash2(sn) & 31u)) & 1u);
-                bw[j] = d.bitmap[sn >> 5];
+#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 5
+                bw[j] = f2[j] ? ~0u : 0u;
+#else
+                bw[j] = d.bitmap[f2[j] ? sn >> 5 : 0u];
+#endif
                 dw[j] = d.syn.dw[f2[j] ? record_of(rel[j]) : 0];
             }
         }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const bool g1 = src[j] < nn && ((bw[j] >> (src[j] & 31u)) & 1u);  // brain.metal:73-77, exact
+            const bool g1 = f2[j] && src[j] < nn && ((bw[j] >> (src[j] & 31u)) & 1u);  // brain.metal:73-77, exact
             bw[j] = g1;
-            // never taken while the second-level filter holds every recent
-            // neuron (it is built beside the bitmap: filter_set)
-            if (__ballot(g1 && !f2[j]) != 0 && g1 && !f2[j]) dw[j] = d.syn.dw[record_of(rel[j])];
             if (!g1) dw[j] = make_uint2(0xFFFFFFFFu, 0u);
             dst[j] = dw[j].x;  // tombstones (dst = 0xFFFFFFFF) never pass
             w[j] = __uint_as_float(dw[j].y);
@@ -638,10 +585,20 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
         if constexpr (!kTail) {
 #pragma unroll
             for (int j = 0; j < R; ++j)
+#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 4  // experiment: no lastFired gather
+                ld[j] = 0ull;
+#else
                 ld[j] = dst[j] - d.stim_first < d.stim_count ? now : (dst[j] < nn ? d.last_fired[dst[j]] : 0ull);
+#endif
         } else {
 #pragma unroll
-            for (int j = 0; j < R; ++j) ld[j] = d.last_fired[dst[j] < nn ? dst[j] : 0u];
+            for (int j = 0; j < R; ++j) {
+#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 4
+                ld[j] = 0ull;
+#else
+                ld[j] = d.last_fired[dst[j] < nn ? dst[j] : 0u];
+#endif
+            }
 #pragma unroll
             for (int j = 0; j < R; ++j)
                 ld[j] = dst[j] - d.stim_first < d.stim_count ? now : (dst[j] < nn ? ld[j] : 0ull);
@@ -1362,14 +1319,15 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
 // k_gate: the streaming kernel (see file header).  Every wave owns one
 // contiguous range of events.  The pre-spike gate needs only the src of each
 // record, held as a 3-B filter code in two streams (engine.h, SynArrays): per
-// 256-event group a lane loads two lo words and one hi word (wave-uniform
-// bases, non-temporal, two iterations in flight), assembles each record's
-// code with one v_perm and tests it against ONE 8-B block of the LDS filter
-// (filter_test: 6 VALU per event, no global load).  The arrays are padded by
+// 512-event block a lane loads its 8 consecutive events' lo words (16 B) and
+// hi bytes (8 B) from wave-uniform bases, non-temporal, kDepth iterations in
+// flight, and tests each against ONE 8-B block of the LDS filter
+// (quad_filter: 4 VALU per event, no global load).  The arrays are padded by
 // kDummyRecords, so the sweep's last iteration reads past its end instead of
 // masking lanes, and the prefetch after a range's last iteration reads the
 // zero dummy block.  Events that pass the filter (under 1 % at config 3 in
-// steady state; the exact bitmap decides) are staged in LDS as {offset, code}; every
+// steady state; the exact bitmap decides) are staged in LDS as {offset,
+// code} in event order (lane order is event order within a block); every
 // chunk of them goes through the refractory stage in the wave itself (a full
 // one at once, the last one -- the range's tail -- after the stream).
 // Instruction-issue priority (s_setprio takes an immediate).
@@ -1477,7 +1435,10 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // src32 mirror).
     // kDepth iterations of records in flight per wave (sweep: two, ping-pong
     // buffers A/B; a wave's memory-level parallelism bounds its stream rate)
-    constexpr int kDepth = (kRandom || kTrack) ? 1 : 2;
+#ifndef ABNN_DEPTH
+#define ABNN_DEPTH 2
+#endif
+    constexpr int kDepth = (kRandom || kTrack) ? 1 : ABNN_DEPTH;
     struct RecsSweep {
         u32x4 lo[NB8];
         u32x2 hi[NB8];
@@ -1488,7 +1449,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         uint32_t dd[KD];
     };
     using Recs = std::conditional_t<kRandom, RecsRandom, RecsSweep>;
-    Recs A, B;
+    Recs bufs[kDepth];
     const uint64_t pass = kRandom ? sload(d.pass_index) : 0;
     auto issue = [&](Recs& x, uint64_t it, bool live) __attribute__((always_inline)) {
         if constexpr (kRandom) {  // random-edge mode: a per-lane random record per event
@@ -1528,8 +1489,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         }
     };
     __builtin_amdgcn_sched_barrier(0);  // the LDS-DMAs above stay older than the records (see the wait below)
-    issue(A, it_begin, it_begin < it_end);
-    if constexpr (kDepth == 2) issue(B, it_begin + 1, it_begin + 1 < it_end);
+#pragma unroll
+    for (int j = 0; j < kDepth; ++j) issue(bufs[j], it_begin + j, it_begin + j < it_end);
     if constexpr (!kFused) {
         // the bitmap and images of the pass after next are zeroed here (the
         // next pass builds them: k_apply or k_bitmap), a slice per workgroup;
@@ -1600,6 +1561,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // are staged (survivors go right after the range's earlier ones)
     auto flush_all = [&]() {
         const uint64_t tc = __builtin_amdgcn_s_memrealtime();
+#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 3  // experiment: staged events dropped
+        if (pend != 0xFFFFFFFFu) { pend = 0; return; }
+#endif
         const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, false>(d, kp, region, region + tot.y, pend, now, pass, Rw,
                                                                    rbw, spec, r, tot.z, s_f2, stage_at);
         tot.x += c.x;
@@ -1690,6 +1654,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             // first test (the reads are independent; SQ_LDS_BANK_CONFLICT is
             // half of SQ_LDS_IDX_ACTIVE, so they queue): 4 VALU per event
             // (quad_filter), no v_perm to assemble the codes
+#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 1  // 1: no filter test either, the records consumed
+#pragma unroll
+            for (int b = 0; b < NB8; ++b) asm volatile("" ::"v"(lo[b].x), "v"(lo[b].y), "v"(lo[b].z), "v"(lo[b].w), "v"(hi[b].x), "v"(hi[b].y));
+            if (rel != 0xFFFFFFFFu) return;
+#endif
             uint2 fb[K];
 #pragma unroll
             for (int b = 0; b < NB8; ++b) {
@@ -1703,6 +1672,13 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 H[2 * b] = quad_filter(fb + 8 * b, lo[b].x, lo[b].y, hi[b].x);
                 H[2 * b + 1] = quad_filter(fb + 8 * b + 4, lo[b].z, lo[b].w, hi[b].y);
             }
+#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER <= 2  // experiment builds only (tools/build_variant.sh): nothing is staged
+#pragma unroll
+            for (int i = 0; i < 2 * NB8; ++i) {
+                asm volatile("" ::"v"(H[i]));  // 2: the filter test runs, its result is dropped
+                H[i] = 0u;
+            }
+#endif
             if (last) {  // events past the sweep pass nothing
 #pragma unroll
                 for (int b = 0; b < NB8; ++b) {
@@ -1732,7 +1708,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             // Staging in event order.  Event order within a block is (lane,
             // k), so a lane's hits go to consecutive slots from the exclusive
             // prefix of the per-lane hit counts, in k order: round j writes
-            // every lane's j-th hit (ffbl, then cleared).  In the steady state
+            // every lane's j-th hit (ffbl of the first quad's hits, then the
+            // second's, each cleared when taken).  In the steady state
             // (~0.7 % of events pass) no lane holds two hits: one mbcnt is the
             // prefix and one round places them all; else (a lane with 2+
             // hits: ~8 % of blocks, and the dense input->output stretch) four
@@ -1743,11 +1720,11 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             // slow path's per-event work in front of the common case.)
 #pragma unroll
             for (int b = 0; b < NB8; ++b) {
-                const uint32_t xb = H[2 * b] | (H[2 * b + 1] << 1);  // event 4 q + m at bit 8 m + q
-                const uint64_t bb = __ballot(xb != 0);
+                // event 4 q + m: bit 8 m of H[2 b + q]
+                const uint64_t bb = __ballot((H[2 * b] | H[2 * b + 1]) != 0);
                 if (bb == 0) continue;  // wave-uniform
                 const uint32_t relb = rel + 512u * b + 8u * lane;  // this lane's first event of the block
-                const uint32_t cb = __builtin_popcount(xb);
+                const uint32_t cb = __builtin_popcount(H[2 * b]) + __builtin_popcount(H[2 * b + 1]);
                 uint32_t P, tot;  // exclusive prefix of the counts, their total
                 if (__ballot(cb > 1u) == 0) {
                     P = mbcnt64(bb);
@@ -1769,20 +1746,23 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                     const uint32_t p0 = split ? (uint32_t)__builtin_amdgcn_readlane((int)P, (int)(16u * u)) : 0u;
                     const uint32_t p1 = !split || u == 3 ? tot
                                                          : (uint32_t)__builtin_amdgcn_readlane((int)P, (int)(16u * u + 16u));
-                    uint32_t xr = !split || (lane >> 4) == u ? xb : 0u;
+                    const bool mine = !split || (lane >> 4) == u;
+                    uint32_t x0 = mine ? H[2 * b] : 0u, x1 = mine ? H[2 * b + 1] : 0u;
                     uint32_t q = pend + P - p0;
                     do {  // one round: every lane's next hit (wave-uniform trip count)
-                        if (xr) {
-                            const uint32_t pos = __builtin_ctz(xr), m = pos >> 3;
-                            const bool hs = pos & 1u;  // the block's second quad (events 4..7)
-                            xr &= xr - 1u;
+                        if ((x0 | x1) != 0u) {
+                            const bool hs = x0 == 0u;  // the block's second quad (events 4..7)
+                            const uint32_t xx = hs ? x1 : x0, m = (uint32_t)__builtin_ctz(xx) >> 3;
+                            const uint32_t xn = xx & (xx - 1u);
+                            x0 = hs ? x0 : xn;
+                            x1 = hs ? xn : x1;
                             const uint32_t e0 = hs ? w2 : w0, e1 = hs ? w3 : w1;
                             const uint32_t lo16 = __builtin_amdgcn_perm(e1, e0, 0x0C0C0100u + m * 0x0202u);
                             st_off[q] = relb + (hs ? 4u : 0u) + m;
                             st_src[q] = __builtin_amdgcn_perm(hs ? v1 : v0, lo16, 0x0C040100u + (m << 16));
                             ++q;
                         }
-                    } while (__ballot(xr != 0) != 0);
+                    } while (__ballot((x0 | x1) != 0u) != 0);
                     pend += p1 - p0;
                     if (kFused ? pend >= d.flush_at : pend >= kChunk) {  // at most 128 past the threshold
                         if constexpr (kFused) flush_all();
@@ -1793,9 +1773,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         }
     };
     for (uint32_t it = it_begin; it < it_end; it += kDepth) {  // wave-uniform
-        step(A, it);
-        if constexpr (kDepth == 2)
-            if (it + 1 < it_end) step(B, it + 1);
+#pragma unroll
+        for (int j = 0; j < kDepth; ++j)
+            if (j == 0 || it + j < it_end) step(bufs[j], it + j);
     }
     const uint64_t t_stream = __builtin_amdgcn_s_memrealtime();
     if (!kFused && lane == 0) {  // diagnostics (tools/wave_clock.py; the fused pass stores them in fused_end)
@@ -1823,6 +1803,9 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         const bool lds_ok = kShard ? false : (kLean || (!d.shard_mode && !d.g2src));
         if (lds_ok && pend <= 256u) tail_lds = reinterpret_cast<uint4*>(s_stage[wid]);
     }
+#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 3  // experiment: staged events dropped
+    pend = 0;
+#endif
     const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, true>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
                                                                r, tot.z, s_f2, stage_at, tail_lds);
     const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;

@@ -1,6 +1,8 @@
 #!/bin/bash
 # Build the HIP library from the working tree into tools/exp/<name>.so (an A/B
 # variant for tools/ab_variants.sh); the in-tree product library is untouched.
+# VARIANT_FLAGS adds compiler flags (e.g. -DABNN_ABLATE_FILTER=1 for an
+# experiment compiled only into the variant).
 set -e
 name=${1:?usage: tools/build_variant.sh NAME}
 cd "$(dirname "$0")/.."
@@ -9,6 +11,7 @@ python3 - "$name" <<'PY'
 import os, subprocess, sys
 from abnn_amd import build as b
 out = os.path.join("tools", "exp", sys.argv[1] + ".so")
-subprocess.check_call([b.HIPCC, *b.HIP_FLAGS, "-o", out, *b.HIP_SOURCES])
+extra = os.environ.get("VARIANT_FLAGS", "").split()
+subprocess.check_call([b.HIPCC, *b.HIP_FLAGS, *extra, "-o", out, *b.HIP_SOURCES])
 print(out)
 PY

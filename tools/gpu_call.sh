@@ -6,7 +6,9 @@
 #   sq=<name>                 SQ counters of the in-tree library -> gpurun_out/<name>
 #   bench=<name>[:args]       bench.py -> gpurun_out/<name>.json
 #   wc=<file>                 per-wave timelines of 8 fused passes (tools/wc_multi.py)
+#   wcbase=<file> / benchbase=<name>[:args]   the same with tools/exp/base.so
 #   cal=<file>                FETCH_SIZE calibration (tools/ubench_fetch_cal.hip, prebuilt)
+#   absweep=<rounds>          full-sweep bench (1e9 events) per library, interleaved
 #   smoke
 # usage: tools/gpu_call.sh step [step ...]
 set -o pipefail
@@ -26,8 +28,17 @@ for st in "$@"; do
            timeout -k 10 400 python -u bench.py $args > "gpurun_out/$name.json" 2> "gpurun_out/$name.err" || { echo "bench $name failed"; tail -5 "gpurun_out/$name.err"; exit 1; }
            python3 tools/bench_line.py "gpurun_out/$name.json" "$name" ;;
     wc) bash tools/gpu_step.sh 300 "$val" python -u tools/wc_multi.py || exit 1; cat "gpurun_out/$val" ;;
+    wcsweep) EVENTS=1000000000 bash tools/gpu_step.sh 300 "$val" python -u tools/wc_multi.py 40 || exit 1; cat "gpurun_out/$val" ;;
+    wcbase) ABNN_LIB=$PWD/tools/exp/base.so bash tools/gpu_step.sh 300 "$val" python -u tools/wc_multi.py || exit 1; cat "gpurun_out/$val" ;;
+    benchbase) name=${val%%:*}; args=""; [ "$name" != "$val" ] && args=${val#*:}
+           ABNN_LIB=$PWD/tools/exp/base.so timeout -k 10 400 python -u bench.py $args > "gpurun_out/$name.json" 2> "gpurun_out/$name.err" || { echo "bench $name failed"; tail -5 "gpurun_out/$name.err"; exit 1; }
+           python3 tools/bench_line.py "gpurun_out/$name.json" "$name(base)" ;;
     cal) bash tools/gpu_step.sh 300 fetch_cal.log timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -T --kernel-trace --output-format csv -d gpurun_out/fcal -o run -- ./tools/ubench_fetch_cal || exit 1
          python3 tools/fetch_cal.py gpurun_out/fcal | tee "gpurun_out/$val" ;;
+    absweep) for r in $(seq 1 "$val"); do for lib in abnn_amd/libabnn_hip.so tools/exp/*.so; do
+               ABNN_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --events 1000000000 --steps 30 --no-cpu-baseline > gpurun_out/abs.json 2> gpurun_out/abs.err || { echo "sweep $lib failed"; tail -5 gpurun_out/abs.err; exit 1; }
+               python3 tools/bench_line.py gpurun_out/abs.json "$(basename $lib .so) r$r"
+             done; done | tee gpurun_out/absweep.txt ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
            tail -1 gpurun_out/smoke.log ;;
     *) echo "unknown step $st"; exit 2 ;;

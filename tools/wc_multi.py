@@ -15,7 +15,8 @@ from abnn_amd import CONFIGS, Brain  # noqa: E402
 
 wl = CONFIGS[os.environ.get("CFG", "c3")]
 passes = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-b = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, device=0)
+events = int(os.environ.get("EVENTS", wl.events))  # EVENTS=1000000000: the full sweep
+b = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, events, device=0)
 b.build_random_graph(1)
 b.set_auto_stimulus(0, wl.n_input)
 b.encode_traversal(74)
@@ -53,6 +54,12 @@ for k in range(7, -1, -1):
     np.save(os.path.join(os.environ.get("OUT", "gpurun_out"), f"wcm_p{k}.npy"), w)
     rw = us(14)
     if k == 0:
+        ct, nc, st = w[:, 6] * 1e-2, w[:, 7], us(1) - us(0)
+        print("   last pass: per wave stream (start->stream end) pcts 50/90/max", np.round(np.percentile(st, [50, 90, 100]), 1),
+              " mid-stream chunks", np.round(np.percentile(nc, [50, 90, 100]), 1),
+              " chunk time us", np.round(np.percentile(ct, [50, 90, 100]), 1),
+              " tail us", np.round(np.percentile(en - se, [50, 90, 100]), 1),
+              " survivors", np.round(np.percentile(w[:, 8], [50, 90, 100]), 0))
         m = w[:, 14] > 0
         print("   last pass: range_walk dur pcts 50/90/99/max", np.round(np.percentile((rw - lb)[m], [50, 90, 99, 100]), 1),
               " lds walk+items dur", np.round(np.percentile((wk - rw)[m], [50, 90, 99, 100]), 1))
