@@ -222,6 +222,9 @@ DEBUG_SIGNATURES = [
     ("abnn_debug_raw_stats", C.c_int, [_VP, C.POINTER(C.c_uint64), _VP]),
     ("abnn_debug_raw_gate_timing", C.c_int, [C.c_int]),
     ("abnn_debug_raw_gate_time", C.c_int, [C.POINTER(C.c_double), _PU32]),
+    ("abnn_debug_raw_fused", C.c_int, [C.c_int]),
+    ("abnn_debug_raw_fused_active", C.c_int, []),
+    ("abnn_debug_raw_wave_clock", C.c_int, [_VP, C.c_uint64, _U32, _U32, C.POINTER(C.c_uint64), C.c_uint64, _VP]),
     ("abnn_debug_set_compact_spin_limit", C.c_int, [_VP, _U32]),
 ]
 

@@ -17,6 +17,15 @@
 //                  filter as the handle API's; each filter block
 //                  built by one workgroup from its ~20 bitmap words: no
 //                  atomics, no zeroing); resets the pass's workspace counters.
+//   k_raw_pass   : (round 5, the default) the rest of the pass in ONE
+//                  persistent launch -- see its comment below: one
+//                  adaptive contiguous range per workgroup, groups claimed by
+//                  its waves, the gates in one round trip per ~192 staged
+//                  hits, survivors in a bounded pool, a decoupled look-back
+//                  for the ordered budget, the walks, the stamps, the pass end.
+//
+// The round-4 pass (ABNN_RAW_FUSED=0, or where 256 workgroups of ~158 KB LDS
+// cannot be resident at once) keeps five launches after the filter:
 //   k_raw_gate   : persistent, one 1024-thread workgroup per CU; every wave
 //                  sweeps groups of 1024 events (interleaved over the CUs):
 //                  16-B records four iterations ahead, the filter test per
@@ -45,6 +54,7 @@
 // the clock read by every thread, k_raw_zero_clock zeroes it afterwards (the
 // reference zeroes it inside the same kernel, racing with the readers).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -72,6 +82,21 @@ constexpr uint32_t kRawFLg = 13;
 constexpr uint32_t kRawSpikeCap = 65536;             // spike list entries (deferred stamps)
 constexpr uint32_t kRawScanThreads = 1024;
 constexpr uint32_t kRawScanBlock = 4 * kRawScanThreads;  // groups per k_raw_scan_local workgroup
+constexpr uint32_t kRfNR = kRawGateWGs;              // fused pass: one contiguous range per workgroup
+constexpr uint32_t kRfMaxG = 2048;                   // fused pass: groups per workgroup range (LDS tallies)
+#ifndef ABNN_RF_D
+#define ABNN_RF_D 3
+#endif
+constexpr uint32_t kRfD = ABNN_RF_D;                 // fused pass: iterations in flight per wave
+#ifndef ABNN_RF_G
+#define ABNN_RF_G 2
+#endif
+constexpr uint32_t kRfG = ABNN_RF_G;                 // fused pass: the least group (iterations, a power of two)
+constexpr uint32_t kRfCt = 16;                       // fused pass: chunk ids of a wave's sequence kept in LDS
+constexpr uint32_t kRfWB = 4;                        // fused pass: chunks a walk loads at once
+constexpr uint32_t kRfLink = kRawChunk - 1;          // fused pass: a pool chunk holds 255 survivors + the next chunk's id
+constexpr uint32_t kRfClk = 8;  // fused pass, diagnostics words per gate wave: entry, stream start / end, look-back,
+                                // walk, end (100 MHz), iterations, survivors
 static_assert(kRawWaves % kRawScanThreads == 0, "k_raw_scan sums the gate waves' statistics in whole rounds");
 constexpr uint32_t kRawApplyWGs = 1024;              // x 4 waves, grid-stride over the groups below the cut
 constexpr uint32_t kRawNone = 0xFFFFFFFFu;
@@ -93,8 +118,14 @@ struct RawHdr {
     uint32_t ovf;                      // some wave's survivors overflowed the pool this pass (groups recomputed)
     uint32_t init;                     // kRawInit once err has been initialised (the workspace starts as garbage)
     uint64_t g1, g2;                   // the pass's pre-gated and refractory-surviving events (diagnostics)
+    // the fused pass (k_raw_pass): its state across passes, on the device
+    uint32_t pass;                     // fused passes run on this workspace (rotates bounds / costs, tags the look-back)
+    uint32_t pvalid;                   // kRawInit: bounds[pass % 3] hold a partition of pE events; costs of pass - 1 valid
+    uint32_t pE;                       // events the partition was made for
+    uint32_t wdone;                    // workgroups whose walk is done (this pass; pool-overflow passes wait for it)
+    uint32_t pad2[12];
 };
-static_assert(sizeof(RawHdr) == 64, "workspace header");
+static_assert(sizeof(RawHdr) == 128, "workspace header");
 
 struct RawWs {
     RawHdr* hdr;
@@ -108,6 +139,10 @@ struct RawWs {
     uint2* wstat;      // per wave: {pre-gated, survivors} of its groups (k_raw_scan sums them)
     uint32_t* ctab;    // per wave: pool chunk of every 256 entries of its sequence
     uint32_t* spikes;  // dst per budget position (deferred stamps)
+    unsigned long long* lb;  // fused pass: per gate workgroup its look-back word (epoch-tagged, never reset)
+    uint32_t* bounds;  // fused pass: 3 x (kRfNR + 1) range bounds (iterations), rotated by pass % 3
+    uint32_t* cost;    // fused pass: 2 x kRfNR range costs (40-ns units), by pass % 2
+    uint64_t* clk;     // fused pass, diagnostics: kRfClk words per gate wave (abnn_debug_raw_wave_clock)
     uint4* pool;       // survivors {event, age bits | candidate << 31, w bits, dst}
     uint32_t ng, maxc, spike_cap, pool_chunks;
 };
@@ -124,9 +159,10 @@ inline uint64_t raw_fixed_bytes(uint64_t E)
 {
     const uint64_t ng = raw_groups(E);
     const uint64_t L = std::min<uint64_t>(E, kRawSpikeCap);
-    return 64 + kRawFB * 8 + al16(4 * ng) * 2 + al16(4 * ((ng + kRawScanBlock - 1) / kRawScanBlock)) + al16(16 * ng) +
+    return 128 + kRawFB * 8 + al16(4 * ng) * 2 + al16(4 * ((ng + kRawScanBlock - 1) / kRawScanBlock)) + al16(16 * ng) +
            al16(4ull * kRawWaves) + al16(8ull * kRawWaves) +
-           al16(4ull * kRawWaves * raw_maxc(ng)) + al16(4 * L);
+           al16(4ull * kRawWaves * raw_maxc(ng)) + al16(4 * L) +
+           8ull * kRawGateWGs + al16(4ull * 3 * (kRfNR + 1)) + 4ull * 2 * kRfNR + 8ull * kRfClk * kRawWaves;
 }
 
 // Recommended pool: a partial chunk per wave plus 1/64 of the events (config
@@ -150,7 +186,7 @@ inline RawWs raw_ws(void* base, uint64_t E, uint64_t bytes)
     w.maxc = raw_maxc(ng);
     w.spike_cap = (uint32_t)std::min<uint64_t>(E, kRawSpikeCap);
     w.hdr = reinterpret_cast<RawHdr*>(p);
-    p += 64;
+    p += 128;
     w.filter = reinterpret_cast<uint2*>(p);
     p += kRawFB * 8;
     w.gcand = reinterpret_cast<uint32_t*>(p);
@@ -169,6 +205,14 @@ inline RawWs raw_ws(void* base, uint64_t E, uint64_t bytes)
     p += al16(4ull * kRawWaves * w.maxc);
     w.spikes = reinterpret_cast<uint32_t*>(p);
     p += al16(4ull * w.spike_cap);
+    w.lb = reinterpret_cast<unsigned long long*>(p);
+    p += 8ull * kRawGateWGs;
+    w.bounds = reinterpret_cast<uint32_t*>(p);
+    p += al16(4ull * 3 * (kRfNR + 1));
+    w.cost = reinterpret_cast<uint32_t*>(p);
+    p += 4ull * 2 * kRfNR;
+    w.clk = reinterpret_cast<uint64_t*>(p);
+    p += 8ull * kRfClk * kRawWaves;
     w.pool = reinterpret_cast<uint4*>(p);
     const uint64_t fixed = (uint64_t)(p - static_cast<char*>(base));
     w.pool_chunks = (uint32_t)std::min<uint64_t>((bytes - fixed) / (kRawChunk * 16), 0xFFFFFFFEu);
@@ -218,9 +262,15 @@ __global__ __launch_bounds__(256) void k_raw_filter(const uint32_t* lastF, const
         ws.hdr->chunks = 0u;
         ws.hdr->t0 = 0u;
         ws.hdr->ovf = 0u;
-        if (ws.hdr->init != kRawInit) {  // first use of this workspace: err is sticky from here on
-            ws.hdr->err = 0u;
+        ws.hdr->wdone = 0u;
+        ws.hdr->g1 = 0ull;
+        ws.hdr->g2 = 0ull;
+        if (ws.hdr->init != kRawInit) {  // first use of this workspace: err is sticky from here on, and the
+            ws.hdr->err = 0u;            // fused pass's state starts over
             ws.hdr->init = kRawInit;
+            ws.hdr->pass = 0u;
+            ws.hdr->pvalid = 0u;
+            for (uint32_t i = 0; i < kRawGateWGs; ++i) ws.lb[i] = 0ull;
         }
     }
     __syncthreads();
@@ -781,6 +831,596 @@ __global__ __launch_bounds__(1024) void k_raw_stamp(uint32_t* lastF, RawWs ws)
     for (uint32_t i = threadIdx.x; i < n; i += 1024) lastF[ws.spikes[i]] = now;  // brain.metal:125-126
 }
 
+// ---------------------------------------------------------------------------
+// k_raw_pass: the fused reference-layout pass (round 5).  After k_raw_filter,
+// ONE launch does the rest of the pass with the handle path's design
+// (kernels.hip k_gate<..., kFused>): persistent workgroups (one per CU), one
+// contiguous range of 256-event iterations per WORKGROUP -- an adaptive
+// partition kept in the workspace (each pass moves the next pass's bounds
+// towards equal measured costs; the dense input->output stretch gets a short
+// range) -- split into up to kRfMaxG groups that the workgroup's 16 waves
+// claim in order from an LDS counter.  Per-wave ranges (the first version)
+// left 80 us between a workgroup's first and last wave: the CU's oldest waves
+// issue first, so the waves of one workgroup stream at rates 0.39-0.50
+// iterations/us by age, which no cost-driven partition kept up with; claimed
+// groups even that out.  Each wave streams its groups kRawD iterations ahead;
+// the LDS filter test per event; hits staged in LDS in event order and,
+// every ~192, through the gates in ONE round trip (lastF[src] and
+// lastF[dst]: both come with the record); the survivors appended to the
+// wave's sequence in the bounded pool (chunks of 255 entries + the next
+// chunk's id), each group's candidates and {first place, wave candidates
+// before it} tallied in LDS.  Then the workgroup's decoupled look-back
+// (epoch-tagged words in the workspace, never reset) and an LDS scan over its
+// groups give every survivor its budget position, every wave walks its own
+// sequence (the weight update into the record's w, brain.metal:101-122;
+// spikes into the workgroup's list), and once every look-back word is
+// published -- every lastF read of the pass done -- the spikes are stamped
+// (brain.metal:125-126) and workgroup 0 ends the pass (*budget, rBar, clock;
+// brain.metal:95-98, 110-113, 129).  Round 4 ran five launches (gate, two
+// scans, apply, stamp) with 71 us per pass outside the gate.
+constexpr uint32_t kRfSpkLds = 2560;     // spikes of a workgroup kept in LDS (budgets up to kMaxSpikes, brain.h:18)
+constexpr uint32_t kRfSpinLimit = 1u << 22;
+
+struct RfLds {
+    uint32_t next;   // the next group to claim
+    uint32_t tmax;   // the workgroup's longest stream (40-ns units)
+    uint32_t g1, g2; // the workgroup's pre-gated and surviving events
+    uint32_t done;   // waves through their tail
+    uint32_t excl;   // candidates of every lower workgroup (capped)
+    uint32_t cwg;    // the workgroup's candidates
+    uint32_t tot;    // the pass's candidates (capped; stamping workgroups)
+};
+
+// One wave polls the look-back words of workgroups [0, n) (64 per lane-round,
+// up to 4 rounds: 256 workgroups) until all carry `tag` or, with
+// stop_at_budget, the published ones reach the budget; their capped sum.
+__device__ uint32_t rf_poll(const RawWs& ws, uint32_t n, uint32_t tag, uint32_t budget, bool stop_at_budget,
+                            uint64_t pub)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t spins = 0;; ++spins) {  // wave-uniform
+        uint64_t raw[kRawGateWGs / 64];
+#pragma unroll
+        for (uint32_t i = 0; i < kRawGateWGs / 64; ++i) {
+            const uint32_t q = i * 64 + lane;
+            raw[i] = q < n ? __hip_atomic_load(ws.lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
+        if (pub && spins == 0 && lane == 0)  // this workgroup's word, behind the first sweep's loads
+            __hip_atomic_store(ws.lb + blockIdx.x, (unsigned long long)pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t sum = 0;
+        bool ok = true;
+#pragma unroll
+        for (uint32_t i = 0; i < kRawGateWGs / 64; ++i) {
+            const uint32_t q = i * 64 + lane;
+            if (q < n) {
+                const bool mine = (uint32_t)(raw[i] >> 32) == tag;
+                sum += mine ? (raw[i] & 0x3FFFFFFFull) : 0ull;
+                ok = ok && mine;
+            }
+        }
+        uint64_t tot = sum;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if (__ballot(!ok) == 0 || (stop_at_budget && tot >= budget)) return (uint32_t)(tot < budget ? tot : budget);
+        if (spins >= kRfSpinLimit) {  // never hang the GPU: report (abnn_traversal_workspace_error) and go on
+            if (lane == 0) ws.hdr->err = 2u;  // (every workgroup is resident: never expected)
+            return budget;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// The next pass's bound k from this pass's bound `from`, the previous pass's
+// costs (exclusive prefix cc over its bounds rb, NR ranges, total T): a
+// quarter of the way (or, gain 4, all of it) to where the cost curve reaches
+// k / NR of the total (kernels.hip adapted_bound).
+__device__ __forceinline__ uint32_t rf_bound(const uint32_t* cc, const uint32_t* rb, uint32_t NR, uint32_t k,
+                                             uint32_t total, uint32_t from, uint32_t gain)
+{
+    if (k == 0 || k >= NR || total == 0) return from;
+    const uint32_t T = (uint32_t)((uint64_t)k * total / NR);
+    uint32_t lo = 0, hi = NR;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cc[mid] <= T) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t cr = cc[lo + 1] - cc[lo];
+    const uint64_t tfp = (uint64_t)rb[lo] * 256u + (cr ? (uint64_t)(T - cc[lo]) * (rb[lo + 1] - rb[lo]) * 256u / cr : 0u);
+    return (uint32_t)(((uint64_t)from * 256u * (4u - gain) + tfp * gain + 512u) >> 10);
+}
+
+__global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn, uint32_t* lastF, uint32_t* clock,
+                                                        uint32_t* budget_p, const float* reward, float* rbar,
+                                                        uint32_t n_nrn, uint32_t E, KernelParams kp, RawWs ws)
+{
+    constexpr uint32_t NW = kRawBlock / 64, NR = kRfNR, RR = kRawStage / 64, MG = kRfMaxG;
+    __shared__ uint2 s_fb[kRawFB];
+    __shared__ uint4 s_st[NW][kRawStage];          // staged hits {event, src, dst, w}
+    __shared__ alignas(16) uint32_t s_cc[NR + 4];  // the previous pass's workgroup costs, scanned in place
+    __shared__ uint32_t s_spk[kRfSpkLds];          // the workgroup's spikes, budget order
+    __shared__ uint32_t s_gc[MG];                  // per group: its candidates, then their exclusive prefix
+    __shared__ uint32_t s_gk[MG];                  // per group: the sweeping wave's candidates before its first
+                                                   // survivor (the least over its survivors)
+    __shared__ uint8_t s_gw[MG];                   // per group: the wave that swept it
+    __shared__ uint32_t s_ct[NW][kRfCt];           // per wave: its sequence's first chunks' pool ids
+    __shared__ RfLds L;
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = wave_uniform(tid >> 6);
+    // the filter global -> LDS (LDS-DMA) before the first records are requested
+#pragma unroll
+    for (uint32_t c = 0; c < kRawFB / 2 / kRawBlock; ++c)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(ws.filter) + c * kRawBlock + tid,
+                                         reinterpret_cast<uint4*>(s_fb) + c * kRawBlock + (tid & ~63u), 16, 0, 0);
+    // the pass's state and scalars (C1: pass-start values; nothing this launch
+    // writes them before every workgroup has read them)
+    const uint32_t pass = sload(&ws.hdr->pass), pvalid = sload(&ws.hdr->pvalid), pE = sload(&ws.hdr->pE);
+    const uint32_t now = sload(clock), b0 = sload(budget_p);
+    const float R = sload(reward), rb = sload(rbar);
+    const uint32_t tag = pass + 1u;
+    const uint32_t NI = (E + kRawIt - 1) / kRawIt;  // iterations of the sweep
+    // bounds[pass % 3] partition these events; the previous pass wrote its
+    // bounds into bounds[(pass + 2) % 3] and its costs over them
+    const bool valid = pvalid == kRawInit && pE == E;
+    uint32_t* bcur = ws.bounds + (pass % 3u) * (NR + 1);
+    uint32_t* bnext = ws.bounds + ((pass + 1u) % 3u) * (NR + 1);
+    const uint32_t* bprev = ws.bounds + ((pass + 2u) % 3u) * (NR + 1);
+    const uint32_t* cost_in = ws.cost + ((pass + 1u) % 2u) * NR;
+    uint32_t* cost_out = ws.cost + (pass % 2u) * NR;
+    if (valid && tid < NR / 4)  // the previous pass's costs to LDS (the next partition's input)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(cost_in) + tid,
+                                         reinterpret_cast<uint4*>(s_cc) + (tid & ~63u), 16, 0, 0);
+    const uint32_t ib = valid ? sload(bcur + blockIdx.x) : (uint32_t)((uint64_t)blockIdx.x * NI / NR);
+    const uint32_t ie = valid ? sload(bcur + blockIdx.x + 1) : (uint32_t)((uint64_t)(blockIdx.x + 1) * NI / NR);
+    const uint32_t nit = ie - ib;  // the workgroup's iterations
+    // groups of gsz = 2^gsh iterations (at least kRfG), at most MG of them
+    uint32_t gsh = 31 - __builtin_clz(kRfG);
+    while (((uint64_t)MG << gsh) < nit) ++gsh;
+    const uint32_t gsz = 1u << gsh;
+    const uint32_t ngrp = (nit + gsz - 1) / gsz;
+    for (uint32_t i = tid; i < ngrp; i += kRawBlock) {
+        s_gc[i] = 0u;
+        s_gk[i] = ~0u;
+    }
+    uint4* st = s_st[wid];
+    uint4 Rc[kRfD][kRawK];
+    // iteration it (of the workgroup's range): events (ib + it) * 256 + k * 64
+    // + lane; past the range or E a tombstone-like record that never passes
+    auto issue = [&](uint32_t d, uint32_t it) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t k = 0; k < kRawK; ++k) {
+            const uint64_t t = (uint64_t)(ib + it) * kRawIt + k * 64 + lane;
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 x = {kRawNone, kRawNone, 0u, 0u};
+            if (it < nit && t < E) x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(syn) + t);
+            Rc[d][k] = make_uint4(x.x, x.y, x.z, x.w);
+        }
+    };
+    // the wave's iterations: its groups' in order, kRfD in flight (buffer d
+    // holds itb[d]).  Wave w starts with the m0 groups [w m0, w m0 + m0) --
+    // enough for the kRfD iterations fetched before the barrier, so no claim
+    // comes before the counter is set --, then the fetch cursor {fg, fi}
+    // claims the next group from the workgroup's counter whenever it needs one
+    const uint32_t m0 = (kRfD + gsz - 1) / gsz;
+    uint32_t fg = wid * m0 < ngrp ? wid * m0 : kRawNone, fi = 0, fstat = m0 - 1;
+    if (fg != kRawNone && lane == 0) s_gw[fg] = (uint8_t)wid;
+    auto next_fetch = [&]() -> uint32_t {  // wave-uniform: the next iteration of the wave, kRawNone past its last
+        if (fg == kRawNone) return kRawNone;
+        if (fi == gsz || fg * gsz + fi >= nit) {  // past the group: the next one
+            uint32_t g = fg + 1;
+            if (fstat) --fstat;
+            else {
+                if (lane == 0) g = atomicAdd(&L.next, 1u);
+                g = wave_uniform(g);
+            }
+            fg = g < ngrp ? g : kRawNone;
+            fi = 0;
+            if (fg == kRawNone) return kRawNone;
+            if (lane == 0) s_gw[fg] = (uint8_t)wid;
+        }
+        return fg * gsz + fi++;
+    };
+    uint32_t itb[kRfD];
+#pragma unroll
+    for (uint32_t d = 0; d < kRfD; ++d) {
+        itb[d] = next_fetch();
+        if (itb[d] != kRawNone) issue(d, itb[d]);
+    }
+    if (tid == 0) {
+        L.next = NW * m0;
+        L.tmax = 0u;
+        L.g1 = 0u;
+        L.g2 = 0u;
+        L.done = 0u;
+    }
+    __syncthreads();  // the filter, the costs and the tallies' zeros in LDS
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    const uint32_t window = kp.window_pre, refr = kp.refractory;
+    uint32_t pend = 0, n_g1 = 0, S = 0, Kw = 0, n_it = 0;
+    // the survivor sequence: chunk ids of its first and current chunk, entries
+    // stored (kRawNone: all so far), the first unstored survivor's event and
+    // the wave's candidates before it
+    uint32_t first_id = kRawNone, cur_id = kRawNone, lim = kRawNone, resume = kRawNone, kres = 0;
+    auto new_chunk = [&]() -> uint32_t {  // wave-uniform; kRawNone when the pool is spent
+        uint32_t id = 0;
+        if (lane == 0) id = atomicAdd(&ws.hdr->chunks, 1u);
+        id = wave_uniform(id);
+        return id < ws.pool_chunks ? id : kRawNone;
+    };
+    // every staged hit through the gates (one round trip), the survivors
+    // appended to the sequence in event order and tallied to their groups
+    auto flush = [&]() {
+        // the gathers first, from the stage's {src, dst} alone (the records in
+        // flight keep most registers: the entries are re-read from LDS below)
+        uint32_t a[RR], bl[RR];
+#pragma unroll
+        for (uint32_t j = 0; j < RR; ++j) {
+            const uint32_t q = j * 64 + lane;
+            const uint32_t src = q < pend ? st[q].y : kRawNone, dst = q < pend ? st[q].z : kRawNone;
+            const bool ok = src < n_nrn && dst < n_nrn;
+            a[j] = ok ? lastF[src] : now;   // brain.metal:73 (exact, for the filter's hits)
+            bl[j] = ok ? lastF[dst] : now;  // brain.metal:79, in the same round trip
+        }
+        // the gates; each entry rewritten in place as its pool entry; places
+        // and tallies: survivor x of the sequence, K(x) = the wave's
+        // candidates before it
+        uint64_t m2[RR], mc[RR];
+        uint32_t n = 0, nc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < RR; ++j) {
+            const uint32_t q = j * 64 + lane;
+            uint4 e = q < pend ? st[q] : make_uint4(0u, kRawNone, kRawNone, 0u);
+            const bool ok = e.y < n_nrn && e.z < n_nrn;
+            const bool g1 = ok && now - a[j] <= window;    // brain.metal:73-77 (u32 ages)
+            const bool g2 = g1 && now - bl[j] > refr;      // brain.metal:79-83
+            const bool cand = g2 && spike_candidate(kp, __uint_as_float(e.w), e.x, now);  // brain.metal:91-92
+            m2[j] = __ballot(g2);
+            mc[j] = __ballot(cand);
+            n_g1 += (uint32_t)__popcll(__ballot(g1));
+            if (g2 && e.x == 0u) {  // event 0 reached the budget test (brain.metal:110): drained before
+                                    // this workgroup's look-back word is published
+                __hip_atomic_store(&ws.hdr->t0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            st[q] = make_uint4(e.x, __float_as_uint((float)(now - bl[j])) | (cand ? 0x80000000u : 0u), e.w, e.z);
+            if (g2) {
+                const uint32_t gl = ((e.x >> 8) - ib) >> gsh;
+                atomicMin(&s_gk[gl], Kw + nc + mbcnt64(mc[j]));  // K never decreases along the sequence
+                if (cand) atomicAdd(&s_gc[gl], 1u);
+            }
+            n += (uint32_t)__popcll(m2[j]);
+            nc += (uint32_t)__popcll(mc[j]);
+        }
+        if (n && lim == kRawNone) {
+            // chunks for entries [S, S + n): the current one and up to two more
+            // (n <= 256, 255 per chunk); a new chunk's id goes into its
+            // predecessor's link slot
+            uint32_t ids[3] = {cur_id, kRawNone, kRawNone};
+            const uint32_t c0 = S / kRfLink, c1 = (S + n - 1) / kRfLink;
+            if (S % kRfLink == 0) {  // S starts a new chunk
+                ids[0] = new_chunk();
+                if (ids[0] != kRawNone) {
+                    if (first_id == kRawNone) first_id = ids[0];
+                    else if (lane == 0) ws.pool[(uint64_t)cur_id * kRawChunk + kRfLink].x = ids[0];
+                    if (lane == 0 && c0 < kRfCt) s_ct[wid][c0] = ids[0];
+                }
+            }
+            for (uint32_t c = 1; c <= c1 - c0 && ids[c - 1] != kRawNone; ++c) {  // wave-uniform
+                ids[c] = new_chunk();
+                if (ids[c] != kRawNone && lane == 0) {
+                    ws.pool[(uint64_t)ids[c - 1] * kRawChunk + kRfLink].x = ids[c];
+                    if (c0 + c < kRfCt) s_ct[wid][c0 + c] = ids[c];
+                }
+            }
+            uint32_t stored = n;  // the first chunk that could not be had ends the stored entries
+            for (uint32_t c = 0; c <= c1 - c0; ++c)
+                if (ids[c] == kRawNone) {
+                    stored = (c0 + c) * kRfLink > S ? (c0 + c) * kRfLink - S : 0u;
+                    break;
+                }
+            uint32_t o = 0, oc = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < RR; ++j) {
+                const uint32_t x = o + mbcnt64(m2[j]);  // this survivor's place among the flush's
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 e = reinterpret_cast<const u32x4*>(st)[j * 64 + lane];
+                if (((m2[j] >> lane) & 1u) && x < stored) {
+                    const uint32_t xs = S + x, c = xs / kRfLink - c0;
+                    const uint32_t id = c == 0 ? ids[0] : (c == 1 ? ids[1] : ids[2]);
+                    reinterpret_cast<u32x4*>(ws.pool)[(uint64_t)id * kRawChunk + xs % kRfLink] = e;
+                }
+                if (stored < n && o <= stored && stored < o + (uint32_t)__popcll(m2[j])) {  // wave-uniform
+                    // the survivor at place `stored` is the first one not stored
+                    const uint64_t mm = m2[j];
+                    const uint32_t want = stored - o;  // its rank among this round's survivors
+                    const bool me = ((mm >> lane) & 1u) && mbcnt64(mm) == want;
+                    const int src_lane = (int)__builtin_ctzll(__ballot(me));
+                    resume = (uint32_t)__builtin_amdgcn_readlane((int)e.x, src_lane);
+                    kres = (uint32_t)__builtin_amdgcn_readlane((int)(Kw + oc + mbcnt64(mc[j])), src_lane);
+                }
+                o += (uint32_t)__popcll(m2[j]);
+                oc += (uint32_t)__popcll(mc[j]);
+            }
+            cur_id = ids[c1 - c0] != kRawNone ? ids[c1 - c0] : cur_id;
+            if (stored < n) {
+                lim = S + stored;
+                if (lane == 0) ws.hdr->ovf = 1u;  // the walk recomputes the rest: the stamps wait for every walk
+            }
+        }
+        S += n;
+        Kw += nc;
+        pend = 0;
+    };
+    for (bool more = itb[0] != kRawNone; more;) {  // wave-uniform: kRfD iterations per step
+#pragma unroll
+        for (uint32_t d = 0; d < kRfD; ++d) {
+            const uint32_t it = itb[d];
+            if (it == kRawNone) {  // (fetch order: so is every later buffer)
+                more = false;
+                break;
+            }
+            uint4 rc[kRawK];
+#pragma unroll
+            for (uint32_t k = 0; k < kRawK; ++k) rc[k] = Rc[d][k];
+            itb[d] = next_fetch();  // this buffer's next iteration in flight first
+            if (itb[d] != kRawNone) issue(d, itb[d]);
+            ++n_it;
+            const uint32_t rel = (ib + it) * kRawIt;
+#pragma unroll
+            for (uint32_t k = 0; k < kRawK; ++k) {
+                const bool h = raw_filter_pass(s_fb, rc[k].x);
+                const uint64_t bm = __ballot(h);
+                if (bm == 0) continue;  // wave-uniform
+                if (h) st[pend + mbcnt64(bm)] = make_uint4(rel + k * 64 + lane, rc[k].x, rc[k].y, rc[k].z);
+                pend += (uint32_t)__popcll(bm);
+                if (pend > kRawStage - 64) flush();
+            }
+        }
+    }
+    if (pend) flush();  // the wave's tail
+    // ---- the workgroup: next partition, look-back, walks, stamps, pass end ----
+    const uint64_t t_tail = __builtin_amdgcn_s_memrealtime();
+    uint32_t order = 0;
+    if (lane == 0) {
+        atomicAdd(&L.g1, n_g1);
+        atomicAdd(&L.g2, S);
+        const uint64_t gt = (t_tail - t_start) >> 2;  // 40-ns units
+        atomicMax(&L.tmax, (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)));  // (+ the walk, below)
+        order = atomicAdd(&L.done, 1u);
+    }
+    if (wave_uniform(order) == 0) {
+        // the first wave through its tail: the next pass's bound of this
+        // workgroup's range (off the critical path)
+        const uint32_t k = blockIdx.x + lane;
+        const bool mine = lane == 0 || (lane == 1 && k == NR);
+        if (valid) {
+            // the previous pass's costs (LDS) scanned in place into an
+            // exclusive prefix; a range above 4x the mean moves every bound the
+            // whole way (kernels.hip fused_next_bounds)
+            uint32_t run = 0, cmax = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < NR / 64; ++u) {
+                const uint32_t v = s_cc[u * 64 + lane];
+                cmax = v > cmax ? v : cmax;
+                const uint32_t inc = wave_incl_scan(v);
+                s_cc[u * 64 + lane] = run + inc - v;
+                run += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            }
+            if (lane == 0) s_cc[NR] = run;
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint32_t x = (uint32_t)__shfl_xor((int)cmax, o, 64);
+                cmax = x > cmax ? x : cmax;
+            }
+            const uint32_t gain = (uint64_t)cmax * NR > 4ull * run ? 4u : 1u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            if (mine) bnext[k] = k == NR ? NI : rf_bound(s_cc, bprev, NR, k, run, bcur[k], gain);
+        } else if (mine) {
+            // no costs to adapt from: the bounds stay (the first pass writes
+            // its uniform ones as this pass's, so the next one has both)
+            const uint32_t cur = k == NR ? NI : (uint32_t)((uint64_t)k * NI / NR);
+            bnext[k] = cur;
+            bcur[k] = cur;
+        }
+    }
+    __syncthreads();  // every wave of the workgroup through its tail: the tallies complete
+    if (wid == 0) {
+        // the groups' candidates -> their exclusive prefix in the workgroup
+        // (each lane a run of consecutive groups)
+        const uint32_t per = (ngrp + 63) / 64, g0 = lane * per;
+        uint32_t sum = 0;
+        for (uint32_t i = 0; i < per; ++i)
+            if (g0 + i < ngrp) sum += s_gc[g0 + i];
+        const uint32_t inc = wave_incl_scan(sum);
+        uint32_t run = inc - sum;
+        for (uint32_t i = 0; i < per; ++i)
+            if (g0 + i < ngrp) {
+                const uint32_t c = s_gc[g0 + i];
+                s_gc[g0 + i] = run;
+                run += c;
+            }
+        const uint32_t c_wg = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        if (lane == 0) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&ws.hdr->g1), (unsigned long long)L.g1);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&ws.hdr->g2), (unsigned long long)L.g2);
+            L.cwg = c_wg;
+        }
+        const uint32_t cv = c_wg < b0 ? c_wg : b0;
+        const uint64_t word = (uint64_t)tag << 32 | (cv < 0x3FFFFFFFu ? cv : 0x3FFFFFFFu);
+        const uint32_t e = rf_poll(ws, blockIdx.x, tag, b0, true, word);
+        if (lane == 0) L.excl = e;
+    }
+    __syncthreads();
+    const uint64_t t_lb = __builtin_amdgcn_s_memrealtime();
+    const uint32_t excl = L.excl, c_wg = L.cwg;
+    // the workgroup's spikes: budget positions [s0, s1)
+    const uint32_t s0 = excl, s1 = (uint32_t)(excl + (uint64_t)c_wg < b0 ? excl + c_wg : b0);
+    const bool spk_lds = b0 <= kRfSpkLds;
+    auto spike = [&](uint32_t pre, uint32_t dst) {  // the spike at budget position pre < b0
+        if (spk_lds) s_spk[pre - s0] = dst;
+        else if (pre < ws.spike_cap) ws.spikes[pre] = dst;
+        else {  // beyond the list (a budget above 65536 and more spikes than that): stamped now,
+                // which may race with another workgroup's refractory reads -- reported
+            lastF[dst] = now;
+            ws.hdr->err = 1u;
+        }
+    };
+    // budget position of the survivor of group gl with K wave candidates
+    // before it: every candidate of lower workgroups, of lower groups, and of
+    // its group before it (its group's survivors are consecutive in the
+    // wave's sequence, from the tallied first place on)
+    auto base_of = [&](uint32_t gl) -> uint32_t { return excl + s_gc[gl] - s_gk[gl]; };
+    // the walk of this wave's survivors in event order (brain.metal:85-122):
+    // the weight update into the record's w, the spikes; budget positions
+    // never decrease along the sequence
+    if (excl < b0 && S > 0) {
+        const uint32_t ns = lim == kRawNone ? S : lim;  // stored survivors
+        uint32_t id = first_id, K = 0;  // (id: the next chunk past the LDS table)
+        bool more = true;
+        for (uint32_t x0 = 0; x0 < ns && more;) {  // wave-uniform: up to kRfWB chunks in flight
+            const uint32_t c = x0 / kRfLink, left = (ns - x0 + kRfLink - 1) / kRfLink;
+            uint32_t nb = 1;
+            if (c + 1 < kRfCt) nb = left < kRfWB ? left : kRfWB;
+            if (c < kRfCt && c + nb > kRfCt) nb = kRfCt - c;
+            uint32_t cid[kRfWB];
+#pragma unroll
+            for (uint32_t b = 0; b < kRfWB; ++b) cid[b] = b < nb ? (c + b < kRfCt ? s_ct[wid][c + b] : id) : 0u;
+            uint4 ex[kRfWB][4];
+#pragma unroll
+            for (uint32_t b = 0; b < kRfWB; ++b)
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t x = x0 + b * kRfLink + j * 64 + lane;
+                    ex[b][j] = b < nb && j * 64 + lane < kRfLink && x < ns ? ws.pool[(uint64_t)cid[b] * kRawChunk + j * 64 + lane]
+                                                                          : make_uint4(0u, 0u, 0u, 0u);
+                }
+            const uint32_t xl = x0 + nb * kRfLink;  // the sequence past this batch
+            if (xl < ns && c + nb >= kRfCt) {      // past the table: the last chunk's link
+                uint32_t last = cid[0];
+#pragma unroll
+                for (uint32_t b = 1; b < kRfWB; ++b) last = b + 1 == nb ? cid[b] : last;
+                id = ws.pool[(uint64_t)last * kRawChunk + kRfLink].x;
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < kRfWB; ++b) {
+                if (b >= nb || !more) break;  // wave-uniform
+                const uint32_t xb = x0 + b * kRfLink, nc = ns - xb < kRfLink ? ns - xb : kRfLink;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    if (j * 64 >= nc) break;  // wave-uniform
+                    const bool v = j * 64 + lane < nc, cand = v && (ex[b][j].y >> 31);
+                    const uint64_t bc = __ballot(cand);
+                    const uint32_t pre = v ? base_of(((ex[b][j].x >> 8) - ib) >> gsh) + K + mbcnt64(bc) : kRawNone;
+                    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)pre) >= b0) {  // lane 0: the round's first
+                        more = false;
+                        break;
+                    }
+                    if (v && pre < b0) {
+                        const float w = updated_weight(kp, __uint_as_float(ex[b][j].z), cand, R, rb,
+                                                       __uint_as_float(ex[b][j].y & 0x7FFFFFFFu));
+                        reinterpret_cast<float*>(syn + ex[b][j].x)[2] = w;  // brain.metal:122 (src, dst, pad unchanged)
+                        if (cand) spike(pre, ex[b][j].w);
+                    }
+                    K += (uint32_t)__popcll(bc);
+                }
+            }
+            x0 = xl;
+        }
+        if (lim != kRawNone && more) {
+            // the pool ran out: the rest recomputed from the records of this
+            // wave's groups from the first unstored survivor's event on, with
+            // the pass-start lastF (every stamp of this pass waits for every
+            // walk: hdr->ovf)
+            K = kres;
+            for (uint32_t gl = 0; gl < ngrp && more; ++gl) {  // wave-uniform
+                if (s_gw[gl] != wid) continue;
+                const uint32_t ge_it = gl * gsz + gsz < nit ? gl * gsz + gsz : nit;
+                const uint32_t gs = (ib + gl * gsz) * kRawIt, ge = (ib + ge_it) * kRawIt < E ? (ib + ge_it) * kRawIt : E;
+                if (ge <= resume) continue;
+                const uint32_t base = base_of(gl);  // (a group with no survivor never gets here with one)
+                for (uint32_t t0 = gs > resume ? gs : resume; t0 < ge; t0 += 64) {  // wave-uniform
+                    const uint32_t t = t0 + lane;
+                    const uint4 rc = t < ge ? syn[t] : make_uint4(kRawNone, kRawNone, 0u, 0u);
+                    const bool ok = rc.x < n_nrn && rc.y < n_nrn;
+                    const uint32_t la = ok ? lastF[rc.x] : now, lb2 = ok ? lastF[rc.y] : now;
+                    const bool g2 = ok && now - la <= window && now - lb2 > refr;
+                    const bool cand = g2 && spike_candidate(kp, __uint_as_float(rc.z), t, now);
+                    const uint64_t bc = __ballot(cand);
+                    const uint64_t b2 = __ballot(g2);
+                    if (b2) {
+                        // the round's first survivor already past the budget: so is the rest
+                        const uint32_t pre0 = base + K + mbcnt64(bc & ((1ull << __builtin_ctzll(b2)) - 1ull));
+                        if (base + K >= b0 || pre0 >= b0) {
+                            more = false;
+                            break;
+                        }
+                    }
+                    const uint32_t pre = base + K + mbcnt64(bc);
+                    if (g2 && pre < b0) {
+                        const float w = updated_weight(kp, __uint_as_float(rc.z), cand, R, rb, (float)(now - lb2));
+                        reinterpret_cast<float*>(syn + t)[2] = w;
+                        if (cand) spike(pre, rc.y);
+                    }
+                    K += (uint32_t)__popcll(bc);
+                }
+            }
+        }
+    }
+    __syncthreads();  // the workgroup's walks (and its LDS spike list) done
+    const uint64_t t_walk = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+        __hip_atomic_fetch_add(&ws.hdr->wdone, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        // the workgroup's cost: its longest stream and its walk (the dense
+        // input stretch's walk is long: its range shrinks for it)
+        const uint32_t c = L.tmax + (uint32_t)((t_walk - t_lb) >> 2);
+        cost_out[blockIdx.x] = nit == 0 ? 0u : (c > 0xFFFFu ? 0xFFFFu : c);
+    }
+    uint64_t* clk = ws.clk + (uint64_t)kRfClk * (blockIdx.x * NW + wid);  // diagnostics (abnn_debug_raw_wave_clock)
+    if (lane < kRfClk) {
+        const uint64_t vals[kRfClk] = {t_entry, t_start, t_tail, t_lb, t_walk, t_walk, n_it, S};
+        uint64_t x = vals[0];
+#pragma unroll
+        for (uint32_t j = 1; j < kRfClk; ++j) x = lane == j ? vals[j] : x;
+        clk[lane] = x;
+    }
+    const bool first = blockIdx.x == 0;
+    if (!(s1 > s0 || first)) return;
+    // every look-back word published = every refractory stage (lastF read) of
+    // the pass done; with a pool overflow, every walk too (recomputes read lastF)
+    if (wid == 0) {
+        const uint32_t tot = rf_poll(ws, gridDim.x, tag, b0, false, 0ull);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (__hip_atomic_load(&ws.hdr->ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            for (uint32_t spins = 0; spins < kRfSpinLimit; ++spins) {
+                if (__hip_atomic_load(&ws.hdr->wdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gridDim.x) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        if (lane == 0) L.tot = tot;
+    }
+    __syncthreads();
+    const uint32_t lim_list = spk_lds ? s1 : (s1 < ws.spike_cap ? s1 : ws.spike_cap);
+    for (uint32_t i = s0 + tid; i < lim_list; i += kRawBlock)
+        lastF[spk_lds ? s_spk[i - s0] : ws.spikes[i]] = now;  // brain.metal:125-126
+    if (first && tid == 0) {  // the pass's end: every workgroup has read the pass-start scalars
+        const uint32_t tot = L.tot;
+        RawHdr* h = ws.hdr;
+        const uint32_t t0 = __hip_atomic_load(&h->t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h->now = now;
+        h->budget0 = b0;
+        h->ncand = tot;
+        *budget_p = b0 - tot;                                   // brain.metal:95-98 (C1: no wrap)
+        if (t0 && b0 > 0) *rbar = rb + kp.alpha_rbar * (R - rb);  // brain.metal:110-113
+        *clock = now + kp.clock_inc;                             // brain.metal:129 (E > 0)
+        h->pass = pass + 1u;
+        h->pvalid = kRawInit;
+        h->pE = E;
+    }
+    if (lane == 0) clk[5] = __builtin_amdgcn_s_memrealtime();
+}
+
 __global__ __launch_bounds__(256) void k_raw_renorm(uint32_t* lastF, const uint32_t* clock, uint32_t n)
 {
     const uint32_t base = *clock;
@@ -800,6 +1440,32 @@ RawTiming& raw_timing()
 {
     static RawTiming t;
     return t;
+}
+
+// The fused pass needs every one of its kRawGateWGs workgroups resident at
+// once (the look-back): one per CU.  ABNN_RAW_FUSED=0 (or
+// abnn_debug_raw_fused(0)) selects the five-launch pass of round 4 (A/B, and
+// the fallback where 256 workgroups of 158 KB LDS do not fit at once).
+int g_raw_fused = -1;  // abnn_debug_raw_fused: -1 the environment, 0 off, 1 on
+
+bool raw_fused_ok()
+{
+    if (g_raw_fused == 0) return false;
+    static const bool fits = [] {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return false;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_raw_pass, kRawBlock, 0) != hipSuccess) return false;
+        return (uint64_t)cus * (uint64_t)per >= kRawGateWGs;
+    }();
+    if (!fits) return false;
+    if (g_raw_fused == 1) return true;
+    static const bool env_on = [] {
+        const char* env = std::getenv("ABNN_RAW_FUSED");
+        return !env || std::atoi(env) != 0;
+    }();
+    return env_on;
 }
 
 KernelParams raw_params(const abnn_traversal_args& a)
@@ -844,6 +1510,19 @@ abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream)
     uint4* syn = reinterpret_cast<uint4*>(a->syn);
     hipLaunchKernelGGL(k_raw_filter, dim3(kRawFB / kRawFilterBlocks), dim3(256), 0, s, a->last_fired, a->clock,
                        a->n_nrn, kp, ws);
+    if (ws.ng && raw_fused_ok()) {  // the fused pass: the rest in one launch
+        RawTiming& tm = raw_timing();
+        std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+        if (tm.on && hipEventCreate(&ev.first) == hipSuccess && hipEventCreate(&ev.second) == hipSuccess)
+            (void)hipEventRecord(ev.first, s);
+        hipLaunchKernelGGL(k_raw_pass, dim3(kRawGateWGs), dim3(kRawBlock), 0, s, syn, a->last_fired, a->clock, a->budget,
+                           a->reward, a->rbar, a->n_nrn, (uint32_t)E, kp, ws);
+        if (ev.second) {
+            (void)hipEventRecord(ev.second, s);
+            tm.ev.push_back(ev);
+        }
+        return hipGetLastError() == hipSuccess ? ABNN_OK : ABNN_ERR_HIP;
+    }
     if (ws.ng) {
         RawTiming& tm = raw_timing();
         std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
@@ -920,6 +1599,27 @@ abnn_status abnn_debug_raw_gate_time(double* total_ms, uint32_t* launches)
     *total_ms = ms;
     *launches = (uint32_t)t.ev.size();
     return ABNN_OK;
+}
+
+abnn_status abnn_debug_raw_fused(int mode)
+{
+    if (mode < -1 || mode > 1) return ABNN_ERR_INVALID;
+    g_raw_fused = mode;
+    return ABNN_OK;
+}
+
+int abnn_debug_raw_fused_active(void) { return raw_fused_ok() ? 1 : 0; }
+
+abnn_status abnn_debug_raw_wave_clock(const void* workspace, uint64_t workspace_bytes, uint32_t n_syn, uint32_t events,
+                                      uint64_t* out, uint64_t n, void* stream)
+{
+    const uint64_t E = raw_events(n_syn, events);
+    if (!workspace || !out || workspace_bytes < raw_fixed_bytes(E)) return ABNN_ERR_INVALID;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const RawWs ws = raw_ws(const_cast<void*>(workspace), E, workspace_bytes);
+    const uint64_t words = std::min<uint64_t>(n, (uint64_t)kRfClk * kRawWaves);
+    if (hipMemcpyAsync(out, ws.clk, words * 8, hipMemcpyDeviceToHost, s) != hipSuccess) return ABNN_ERR_HIP;
+    return hipStreamSynchronize(s) == hipSuccess ? ABNN_OK : ABNN_ERR_HIP;
 }
 
 abnn_status abnn_launch_renormalise(uint32_t* last_fired, uint32_t* last_visited, uint32_t* clock, uint32_t n_nrn,

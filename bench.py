@@ -197,7 +197,7 @@ def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, ex
                       f"(cgroup quota {hc['cgroup_quota_cpus']} CPUs)"}
 
 
-def raw_run(config: str, events_arg: int, settle: int, warmup: int, steps: int) -> dict:
+def raw_run(config: str, events_arg: int, settle: int, warmup: int, steps: int, clock_passes: int = 0) -> dict:
     """One step = one pass of abnn_launch_traversal over caller-owned
     buffers in the reference's layouts (brain.cpp:52-69): the host's two
     writes of encode_traversal / inject_inputs (lastF[inputs] = clock,
@@ -265,6 +265,13 @@ def raw_run(config: str, events_arg: int, settle: int, warmup: int, steps: int) 
     dt = time.perf_counter() - t0
     lib.abnn_debug_raw_stats(ws.data_ptr(), g, None)  # the last pass's
     g1, g2 = int(g[0]), int(g[1])
+    clk = []
+    for _ in range(clock_passes):  # untimed passes, each one's per-wave timeline (tools/raw_clock.py)
+        step(1)
+        c = np.zeros(8 * 4096, dtype=np.uint64)
+        lib.abnn_debug_raw_wave_clock(ws.data_ptr(), nb, wl.n_syn, events,
+                                      c.ctypes.data_as(C.POINTER(C.c_uint64)), c.size, None)
+        clk.append(c.reshape(4096, 8))
     gate_ms, n_gate = C.c_double(), C.c_uint32()
     lib.abnn_debug_raw_gate_time(C.byref(gate_ms), C.byref(n_gate))
     lib.abnn_debug_raw_gate_timing(0)
@@ -277,6 +284,9 @@ def raw_run(config: str, events_arg: int, settle: int, warmup: int, steps: int) 
     # pre-gated event (+ 16 B per update and 4 B per spike, not counted: the
     # update/stamp kernels, < 0.1 % of the bytes at config 3)
     survey = 20 * E + 4 * g1
+    # the fused pass (k_raw_pass: the gate, the budget, the walk and the
+    # stamps in one launch after k_raw_filter) or round 4's five launches
+    kname = "k_raw_pass" if lib.abnn_debug_raw_fused_active() else "k_raw_gate"
     traffic, traffic_note = load_traffic("raw_" + wl.name)
     out = {
         "metric": "traversal events/sec at 1B synapses, 5M neurons; achieved HBM GB/s",
@@ -294,12 +304,12 @@ def raw_run(config: str, events_arg: int, settle: int, warmup: int, steps: int) 
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
-            "traffic_source": ("profiles/traffic_raw_%s.json (rocprofv3 PMC of k_raw_gate, FETCH_SIZE x2 + "
+            "traffic_source": ("profiles/traffic_raw_%s.json (rocprofv3 PMC of the gate kernel, FETCH_SIZE x2 + "
                                "WRITE_SIZE; tag %s, kernel sources %s)" % (wl.name, traffic.get("tag"),
                                                                            traffic.get("source_sha"))
                                if traffic else traffic_note),
-            "kernel": "k_raw_gate", "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": n_gate.value,
-            "launch_ms_source": "HIP event pair around every k_raw_gate launch (abnn_debug_raw_gate_timing)",
+            "kernel": kname, "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": n_gate.value,
+            "launch_ms_source": "HIP event pair around every %s launch (abnn_debug_raw_gate_timing)" % kname,
             "algorithmic_bytes_per_launch": stream_bytes,
             "bytes_formula": "16*E (the caller's 16-B SynapsePacked record per visited event; DESIGN.md §5)",
             "survey_formula_bytes_per_launch": survey,
@@ -310,6 +320,8 @@ def raw_run(config: str, events_arg: int, settle: int, warmup: int, steps: int) 
         },
         "cpu_baseline": None,
     }
+    if clk:
+        out["_wave_clocks"] = np.stack(clk)
     del recs, ws, lastF, lastV
     torch.cuda.empty_cache()
     return out

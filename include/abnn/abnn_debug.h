@@ -36,6 +36,18 @@ abnn_status abnn_debug_range_bounds(abnn_brain* b, uint32_t* out, uint64_t n);
 abnn_status abnn_debug_raw_stats(const void* workspace, uint64_t* out2, void* stream);
 abnn_status abnn_debug_raw_gate_timing(int enable);
 abnn_status abnn_debug_raw_gate_time(double* total_ms, uint32_t* launches);
+/* The buffer-index pass in one launch after the filter (k_raw_pass) or the
+ * five-launch pass of round 4: mode 1 / 0, or -1 = the ABNN_RAW_FUSED
+ * environment variable (default: the fused pass when its 256 workgroups fit
+ * the device at once). */
+abnn_status abnn_debug_raw_fused(int mode);
+/* 1 when the next abnn_launch_traversal runs the fused pass, else 0. */
+int abnn_debug_raw_fused_active(void);
+/* The last fused buffer-index pass's per-range timeline from its workspace:
+ * 8 u64 per range (100-MHz ticks: entry, stream start, stream done, look-back
+ * done, walk done, end; then iterations, survivors). */
+abnn_status abnn_debug_raw_wave_clock(const void* workspace, uint64_t workspace_bytes, uint32_t n_syn,
+                                      uint32_t events, uint64_t* out, uint64_t n, void* stream);
 
 /* The sharded pass's exchange alone: `count` in-place all-gathers of
  * `bytes` per rank on the library's RCCL communicator (enqueued on `stream`;

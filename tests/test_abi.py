@@ -162,12 +162,16 @@ def _raw_ws_bytes(n_syn: int, events: int) -> tuple[int, int]:
     {candidates, prefix, survivors + sequence start}, per 4096 groups a scan
     total, per gate wave (4096) its
     stored limit, statistics and chunk table, the spike list (min(E, 65536)) -- and the
-    recommended pool of 4-KiB survivor chunks: one per wave + E/64 entries + 64."""
+    recommended pool of 4-KiB survivor chunks: one per wave + E/64 entries + 64.
+    The fused pass adds a look-back word per gate workgroup (256), three sets of
+    257 workgroup range bounds, two of 256 range costs and 8 u64 per gate wave
+    of diagnostics."""
     al = lambda x: (x + 15) & ~15
     E = min((events + 255) // 256 * 256, n_syn)
     g, W = (E + 1023) // 1024, 4096
     maxc = (g + W - 1) // W * 4 + 1
-    fixed = 64 + 8192 * 8 + 2 * al(4 * g) + al(4 * ((g + 4095) // 4096)) + al(16 * g) + al(4 * W) + al(8 * W) + al(4 * W * maxc) + al(4 * min(E, 65536))
+    fixed = 128 + 8192 * 8 + 2 * al(4 * g) + al(4 * ((g + 4095) // 4096)) + al(16 * g) + al(4 * W) + al(8 * W) + \
+        al(4 * W * maxc) + al(4 * min(E, 65536)) + 8 * 256 + al(4 * 3 * 257) + 4 * 2 * 256 + 8 * 8 * W
     pool = (W + (E // 64 + 255) // 256 + 64) * 4096 if E else 0
     return fixed, fixed + pool
 

@@ -15,6 +15,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=[0, 1], ids=["five_launches", "fused"])
+def raw_pass_kind(request):
+    """Every test runs both buffer-index passes: the five-launch one and the
+    single k_raw_pass launch after the filter (abnn_debug_raw_fused)."""
+    from abnn_amd import _lib
+
+    lib = _lib.load()
+    assert lib.abnn_debug_raw_fused(request.param) == 0
+    yield request.param
+    lib.abnn_debug_raw_fused(-1)
+
+
 class RawBrain:
     """Caller-owned buffers, as Brain::build_buffers allocates them (brain.cpp:52-69)."""
 

@@ -9,6 +9,9 @@
 #   wcbase=<file> / benchbase=<name>[:args]   the same with tools/exp/base.so
 #   cal=<file>                FETCH_SIZE calibration (tools/ubench_fetch_cal.hip, prebuilt)
 #   absweep=<rounds>          full-sweep bench (1e9 events) per library, interleaved
+#   rawab=<rounds>            buffer-index bench, fused pass vs five launches, interleaved
+#   rawvar=<rounds>           fused buffer-index bench per library (in-tree, tools/exp/*.so), interleaved
+#   rawclk=<file>             per-range timeline of the fused buffer-index pass (tools/raw_clock.py)
 #   smoke
 # usage: tools/gpu_call.sh step [step ...]
 set -o pipefail
@@ -39,6 +42,15 @@ for st in "$@"; do
                ABNN_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --events 1000000000 --steps 30 --no-cpu-baseline > gpurun_out/abs.json 2> gpurun_out/abs.err || { echo "sweep $lib failed"; tail -5 gpurun_out/abs.err; exit 1; }
                python3 tools/bench_line.py gpurun_out/abs.json "$(basename $lib .so) r$r"
              done; done | tee gpurun_out/absweep.txt ;;
+    rawab) for r in $(seq 1 "$val"); do for f in 1 0; do
+             ABNN_RAW_FUSED=$f timeout -k 10 300 python -u bench.py --raw --steps 50 > gpurun_out/rab.json 2> gpurun_out/rab.err || { echo "raw bench failed"; tail -5 gpurun_out/rab.err; exit 1; }
+             python3 tools/bench_line.py gpurun_out/rab.json "raw fused=$f r$r"
+           done; done | tee gpurun_out/rawab.txt ;;
+    rawvar) for r in $(seq 1 "$val"); do for lib in abnn_amd/libabnn_hip.so tools/exp/*.so; do
+             ABNN_LIB=$PWD/$lib ABNN_RAW_FUSED=1 timeout -k 10 300 python -u bench.py --raw --steps 50 > gpurun_out/rv.json 2> gpurun_out/rv.err || { echo "raw bench failed"; tail -5 gpurun_out/rv.err; exit 1; }
+             python3 tools/bench_line.py gpurun_out/rv.json "raw $(basename $lib .so) r$r"
+           done; done | tee gpurun_out/rawvar.txt ;;
+    rawclk) bash tools/gpu_step.sh 300 "$val" python -u tools/raw_clock.py || exit 1; cat "gpurun_out/$val" ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
            tail -1 gpurun_out/smoke.log ;;
     *) echo "unknown step $st"; exit 2 ;;
