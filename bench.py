@@ -288,6 +288,9 @@ def raw_run(config: str, events_arg: int, settle: int, warmup: int, steps: int, 
     # stamps in one launch after k_raw_filter) or round 4's five launches
     kname = "k_raw_pass" if lib.abnn_debug_raw_fused_active() else "k_raw_gate"
     traffic, traffic_note = load_traffic("raw_" + wl.name)
+    if traffic and traffic.get("kernel") != kname:
+        traffic, traffic_note = None, "profiles/traffic_raw_%s.json is of %s, this run's kernel is %s" % (
+            wl.name, traffic.get("kernel"), kname)
     out = {
         "metric": "traversal events/sec at 1B synapses, 5M neurons; achieved HBM GB/s",
         "value": E * steps / dt, "unit": "events/s", "n_gpus": 1, "steps": steps,
@@ -304,9 +307,12 @@ def raw_run(config: str, events_arg: int, settle: int, warmup: int, steps: int, 
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
-            "traffic_source": ("profiles/traffic_raw_%s.json (rocprofv3 PMC of the gate kernel, FETCH_SIZE x2 + "
-                               "WRITE_SIZE; tag %s, kernel sources %s)" % (wl.name, traffic.get("tag"),
-                                                                           traffic.get("source_sha"))
+            "traffic_stream_bytes": traffic.get("stream_bytes") if traffic else None,
+            "traffic_other_fetch_bytes": traffic.get("other_fetch_bytes") if traffic else None,
+            "traffic_source": ("profiles/traffic_raw_%s.json (rocprofv3 PMC of %s: the record stream from "
+                               "FETCH_SIZE x2, the rest of FETCH_SIZE x1, + WRITE_SIZE, calibrated by "
+                               "profiles/r05_fetch_calibration.txt; tag %s, kernel sources %s)"
+                               % (wl.name, kname, traffic.get("tag"), traffic.get("source_sha"))
                                if traffic else traffic_note),
             "kernel": kname, "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": n_gate.value,
             "launch_ms_source": "HIP event pair around every %s launch (abnn_debug_raw_gate_timing)" % kname,
@@ -487,6 +493,8 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
+            "traffic_stream_bytes": traffic.get("stream_bytes") if traffic else None,
+            "traffic_other_fetch_bytes": traffic.get("other_fetch_bytes") if traffic else None,
             "kernel": "k_gate", "avg_launch_ms": round(avg_gate_ms, 4), "timed_launches": args.steps,
             "launch_ms_source": "HIP event pair around the timed passes / steps (launch + dispatch gap)",
             "sampled_launches": launches,
@@ -507,8 +515,10 @@ def main():
             "survey_formula_achieved": round(survey_per_launch / (avg_gate_ms * 1e-3) / 1e9, 1),
             "survey_formula": "24*E + 8*G1 (SURVEY §8d; G1 pre-gated) -- counts an 8-B lastFired[src] "
                               "gather per event that this design answers from LDS/L2",
-            "traffic_source": ("profiles/traffic_%s.json (rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE; tag %s, "
-                               "kernel sources %s)" % (args.config, traffic.get("tag"), traffic.get("source_sha"))
+            "traffic_source": ("profiles/traffic_%s.json (rocprofv3 PMC of k_gate: the 3-B/event stream from "
+                               "FETCH_SIZE x2, the rest of FETCH_SIZE x1, + WRITE_SIZE, calibrated by "
+                               "profiles/r05_fetch_calibration.txt; tag %s, kernel sources %s)"
+                               % (args.config, traffic.get("tag"), traffic.get("source_sha"))
                                if traffic else traffic_note),
             "pass_ms": round(dt / args.steps * 1e3, 4),
         }

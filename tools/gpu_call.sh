@@ -11,6 +11,7 @@
 #   absweep=<rounds>          full-sweep bench (1e9 events) per library, interleaved
 #   rawab=<rounds>            buffer-index bench, fused pass vs five launches, interleaved
 #   rawvar=<rounds>           fused buffer-index bench per library (in-tree, tools/exp/*.so), interleaved
+#   prof=<tag> / profraw=<tag>  rocprofv3 kernel trace + FETCH/WRITE passes (tools/profile.sh, profile_raw.sh)
 #   rawclk=<file>             per-range timeline of the fused buffer-index pass (tools/raw_clock.py)
 #   smoke
 # usage: tools/gpu_call.sh step [step ...]
@@ -50,6 +51,8 @@ for st in "$@"; do
              ABNN_LIB=$PWD/$lib ABNN_RAW_FUSED=1 timeout -k 10 300 python -u bench.py --raw --steps 50 > gpurun_out/rv.json 2> gpurun_out/rv.err || { echo "raw bench failed"; tail -5 gpurun_out/rv.err; exit 1; }
              python3 tools/bench_line.py gpurun_out/rv.json "raw $(basename $lib .so) r$r"
            done; done | tee gpurun_out/rawvar.txt ;;
+    prof) bash tools/gpu_step.sh 1300 "prof_$val.log" bash tools/profile.sh "$val" c3 || exit 1 ;;
+    profraw) bash tools/gpu_step.sh 1300 "profraw_$val.log" bash tools/profile_raw.sh "$val" || exit 1 ;;
     rawclk) bash tools/gpu_step.sh 300 "$val" python -u tools/raw_clock.py || exit 1; cat "gpurun_out/$val" ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
            tail -1 gpurun_out/smoke.log ;;

@@ -4,11 +4,17 @@ usage: tools/pmc_summary.py OUTDIR TAG CONFIG [KERNEL]   (KERNEL: k_gate)
 
 * profiles/<tag>_kernel_stats.csv  : rocprofv3 --stats output (whole run)
 * profiles/<tag>_steady_state.txt  : per-kernel medians over the last 30 passes
-* profiles/traffic_<cfg>.json      : k_gate HBM bytes per launch from the PMC
-  passes.  MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
-  FETCH_SIZE reads exactly half the bytes of a wide (16 B/lane) coalesced
-  streaming read, which is what k_gate's record stream is, so the read side is
-  doubled; WRITE_SIZE is used as is.
+* profiles/traffic_<cfg>.json      : the kernel's HBM bytes per launch from the
+  PMC passes, calibrated (round 5, profiles/r05_fetch_calibration.txt from
+  tools/ubench_fetch_cal.hip under `rocprofv3 --pmc FETCH_SIZE`, step `cal=`
+  of tools/gpu_call.sh): FETCH_SIZE/WRITE_SIZE are in KiB; non-temporal
+  coalesced streams of 16-B and of 8-B lanes report exactly 0.500 of the
+  bytes they move, random 8-B reads from an 8-GiB table report 64 B each (one
+  64-B burst per read: counted as is).  So the record stream (its algorithmic
+  bytes known: 3 B per event for k_gate, 16 B for the reference-layout pass)
+  is taken at 2 x its reported half, and the rest of FETCH_SIZE -- the
+  gathers, the filter / bitmap / look-back traffic -- at 1x.  Round 4 doubled
+  the whole FETCH_SIZE, which double-counted the gathers.
 """
 import csv
 import glob
@@ -101,16 +107,38 @@ def main():
            "commit": os.environ.get("ABNN_COMMIT", "")}
     if fetch and write:
         f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+        E = 0
+        try:
+            bj = [x for x in open(os.path.join(out, "bench_fetch.json")) if x.startswith("{")][-1]
+            c = json.loads(bj)["config"]
+            E = int(c.get("visited_events_per_pass") or c.get("visited_events_per_pass_per_gpu"))
+        except (OSError, IndexError, KeyError, ValueError, TypeError):
+            pass
+        per_event = 3 if KERNEL == "k_gate" else 16
+        stream = per_event * E
+        reported = f_kib * 1024
+        rest = max(0.0, reported - 0.5 * stream)
         res.update({
             "fetch_size_kib_raw": f_kib, "write_size_kib": w_kib,
-            "fetch_bytes_corrected": f_kib * 1024 * 2,
+            "visited_events": E,
+            "stream_bytes": stream,
+            "stream_bytes_formula": f"{per_event}*E (the record stream; reported by FETCH_SIZE at 0.500)",
+            "other_fetch_bytes": rest,
+            "other_fetch_note": "FETCH_SIZE minus the stream's reported half: the gathers (lastF / {dst, w} / "
+                                "bitmap words), filter and look-back traffic, counted 1x (random 8-B reads "
+                                "report one 64-B burst each)",
             "write_bytes": w_kib * 1024,
-            "bytes_per_launch": f_kib * 1024 * 2 + w_kib * 1024,
-            "correction": "FETCH_SIZE x2 (gfx950 stream undercount; calibrated for 4-B nt streams in profiles/r01l_fetch_calibration_dword.txt), KiB -> bytes",
+            "bytes_per_launch": stream + rest + w_kib * 1024,
+            "bytes_per_launch_round4_rule": reported * 2 + w_kib * 1024,
+            "correction": "calibrated: profiles/r05_fetch_calibration.txt (tools/ubench_fetch_cal.hip; "
+                          "tools/gpu_call.sh cal=...): nt streams x2, the rest x1; KiB -> bytes",
+            "command": "tools/profile.sh TAG c3" if KERNEL == "k_gate" else "tools/profile_raw.sh TAG",
             "launches_used": min(len(fetch), len(write)),
         })
-        lines.append(f"{KERNEL} PMC per launch: FETCH_SIZE {f_kib:.0f} KiB (x2 -> {f_kib*2048/1e9:.3f} GB), "
-                     f"WRITE_SIZE {w_kib:.0f} KiB ({w_kib*1024/1e9:.4f} GB)")
+        lines.append(f"{KERNEL} PMC per launch: FETCH_SIZE {f_kib:.0f} KiB = stream {stream/1e9:.3f} GB "
+                     f"(reported at half) + other {rest/1e9:.4f} GB; WRITE_SIZE {w_kib:.0f} KiB "
+                     f"({w_kib*1024/1e9:.4f} GB); total {(stream + rest + w_kib*1024)/1e9:.3f} GB "
+                     f"(round-4 rule, FETCH x2: {(reported*2 + w_kib*1024)/1e9:.3f} GB)")
         with open(f"profiles/traffic_{cfg}.json", "w") as f:
             json.dump(res, f, indent=1)
     for name in ("bench_trace.json", "bench_fetch.json", "bench_write.json"):
