@@ -386,17 +386,20 @@ uint64_t abnn_structural_updates(const abnn_brain* b);
  * clock tick.  The knobs the reference compiles in (#define BASE_SCALE ...,
  * brain.metal:22-31) come from `knobs` (NULL = the reference defaults; only
  * the #define fields are read -- aLTP..wMax are the buffer arguments).
- * Scratch: `workspace` of device memory (any contents; reused every pass),
+ * Scratch: `workspace` of device memory (any contents on first use; reused
+ * every pass: it carries the pass's adaptive partition and look-back epoch),
  * 16-B aligned: abnn_traversal_workspace_bytes(n_syn, events) is the
- * recommended size (~60 MB at config 3: a bounded pool of refractory
+ * recommended size (~61 MB at config 3: a bounded pool of refractory
  * survivors, 1/64 of the visited events, plus per-1024-event counters),
  * abnn_traversal_workspace_min_bytes the least accepted (no pool).  Survivors
  * that do not fit the pool are recomputed from the records (slower, same
  * results).  The spikes are stamped after the pass's last lastF read from a
  * list of min(events, 65536) entries; a pass with more spikes than that
- * stamps them directly, which is exact unless survivors also overflowed the
- * pool -- then abnn_traversal_workspace_error reports 1 (the host's
- * kMaxSpikes = 2560, brain.cpp:90, never comes near it).  This is the reference's memory
+ * stamps the rest directly, which may land before another workgroup's lastF
+ * reads (the fused pass), or (the five-launch pass) before a recomputed
+ * group's when survivors also overflowed the pool -- such a pass is reported
+ * by abnn_traversal_workspace_error (1); the host's kMaxSpikes = 2560,
+ * brain.cpp:90, never comes near it.  This is the reference's memory
  * layout, so it streams 16 B per visited event; the pre-spike test is
  * answered from an LDS filter of lastF, which is gathered only for the ~1 %
  * of events the filter passes (the handle API's layout moves
@@ -425,9 +428,11 @@ typedef struct abnn_traversal_args {
 uint64_t abnn_traversal_workspace_bytes(uint32_t n_syn, uint32_t events);
 uint64_t abnn_traversal_workspace_min_bytes(uint32_t n_syn, uint32_t events);
 /* synchronises `stream`: 1 if any pass on this workspace since the last call
- * (or since its first launch) stamped directly while recomputing overflowed
- * survivors (see above), else 0; the flag is sticky until this call reads
- * and clears it, so one check after many passes sees every pass */
+ * (or since its first launch) stamped directly where that may race (see
+ * above), 2 if a pass's look-back wait gave up (never expected:
+ * every workgroup of the pass is resident), else 0; the flag is sticky until
+ * this call reads and clears it, so one check after many passes sees every
+ * pass */
 abnn_status abnn_traversal_workspace_error(const void* workspace, uint32_t* err, void* stream);
 abnn_status abnn_launch_traversal(const abnn_traversal_args* a, void* stream);
 abnn_status abnn_launch_renormalise(uint32_t* last_fired, uint32_t* last_visited, uint32_t* clock,
