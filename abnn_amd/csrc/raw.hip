@@ -985,14 +985,17 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn,
     uint4* st = s_st[wid];
     uint4 Rc[kRfD][kRawK];
     // iteration it (of the workgroup's range): events (ib + it) * 256 + k * 64
-    // + lane; past the range or E a tombstone-like record that never passes
+    // + lane.  Lanes past the range or E load record 0 (every call issues
+    // exactly kRawK loads, which the prologue's wait counts; an iteration past
+    // the range is never swept, and the sweep's lanes past E are masked where
+    // the records are consumed, so no use of a load follows it here)
     auto issue = [&](uint32_t d, uint32_t it) __attribute__((always_inline)) {
 #pragma unroll
         for (uint32_t k = 0; k < kRawK; ++k) {
             const uint64_t t = (uint64_t)(ib + it) * kRawIt + k * 64 + lane;
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 x = {kRawNone, kRawNone, 0u, 0u};
-            if (it < nit && t < E) x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(syn) + t);
+            const bool live = it < nit && t < E;
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(syn) + (live ? t : 0ull));
             Rc[d][k] = make_uint4(x.x, x.y, x.z, x.w);
         }
     };
@@ -1020,12 +1023,6 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn,
         }
         return fg * gsz + fi++;
     };
-    uint32_t itb[kRfD];
-#pragma unroll
-    for (uint32_t d = 0; d < kRfD; ++d) {
-        itb[d] = next_fetch();
-        if (itb[d] != kRawNone) issue(d, itb[d]);
-    }
     if (tid == 0) {
         L.next = NW * m0;
         L.tmax = 0u;
@@ -1033,7 +1030,29 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn,
         L.g2 = 0u;
         L.done = 0u;
     }
-    __syncthreads();  // the filter, the costs and the tallies' zeros in LDS
+    uint32_t itb[kRfD];
+    __builtin_amdgcn_sched_barrier(0);  // the LDS-DMAs above stay older than the records
+#pragma unroll
+    for (uint32_t d = 0; d < kRfD; ++d) {
+        itb[d] = next_fetch();
+        issue(d, itb[d]);  // (kRawNone: past the range, loads counted all the same)
+    }
+    // the filter, the costs and the tallies' zeros in LDS for every wave, the
+    // first records still in flight: this wave's LDS-DMAs are older than its
+    // kRfD * kRawK record loads and vmcnt retires in order (a __syncthreads
+    // would wait for the records' whole round trip, ~5 us at config 3).  The
+    // builtin wait, not inline asm: the compiler's own count then knows the
+    // DMAs are done (kernels.hip wait_vm_lgkm0)
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        constexpr int N = kRfD * kRawK;
+        static_assert(N < 64, "vmcnt is 6 bits");
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+        asm volatile("" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const uint32_t window = kp.window_pre, refr = kp.refractory;
     uint32_t pend = 0, n_g1 = 0, S = 0, Kw = 0, n_it = 0;
@@ -1166,6 +1185,11 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn,
             if (itb[d] != kRawNone) issue(d, itb[d]);
             ++n_it;
             const uint32_t rel = (ib + it) * kRawIt;
+            if (rel + kRawIt > E) {  // wave-uniform: the sweep's last iteration, lanes past E
+#pragma unroll
+                for (uint32_t k = 0; k < kRawK; ++k)
+                    if (rel + k * 64 + lane >= E) rc[k] = make_uint4(kRawNone, kRawNone, 0u, 0u);
+            }
 #pragma unroll
             for (uint32_t k = 0; k < kRawK; ++k) {
                 const bool h = raw_filter_pass(s_fb, rc[k].x);
