@@ -12,6 +12,7 @@
 #   rawab=<rounds>            buffer-index bench, fused pass vs five launches, interleaved
 #   rawvar=<rounds>           fused buffer-index bench per library (in-tree, tools/exp/*.so), interleaved
 #   prof=<tag> / profraw=<tag>  rocprofv3 kernel trace + FETCH/WRITE passes (tools/profile.sh, profile_raw.sh)
+#   shardvar=<rounds>         sharded-path bench at world 1 per library (in-tree, tools/exp/*.so), interleaved
 #   rawclk=<file>             per-range timeline of the fused buffer-index pass (tools/raw_clock.py)
 #   smoke
 # usage: tools/gpu_call.sh step [step ...]
@@ -53,6 +54,10 @@ for st in "$@"; do
            done; done | tee gpurun_out/rawvar.txt ;;
     prof) bash tools/gpu_step.sh 1300 "prof_$val.log" bash tools/profile.sh "$val" c3 || exit 1 ;;
     profraw) bash tools/gpu_step.sh 1300 "profraw_$val.log" bash tools/profile_raw.sh "$val" || exit 1 ;;
+    shardvar) for r in $(seq 1 "$val"); do for lib in abnn_amd/libabnn_hip.so tools/exp/*.so; do
+             ABNN_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --shard-path --steps 200 --no-cpu-baseline > gpurun_out/sv.json 2> gpurun_out/sv.err || { echo "shard bench failed"; tail -5 gpurun_out/sv.err; exit 1; }
+             python3 tools/bench_line.py gpurun_out/sv.json "shard $(basename $lib .so) r$r"
+           done; done | tee gpurun_out/shardvar.txt ;;
     rawclk) bash tools/gpu_step.sh 300 "$val" python -u tools/raw_clock.py || exit 1; cat "gpurun_out/$val" ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
            tail -1 gpurun_out/smoke.log ;;
