@@ -2638,9 +2638,14 @@ __global__ __launch_bounds__(kScanThreads) void k_append_grown(SynArrays a, uint
                                                                const uint32_t* err)
 {
     __shared__ uint64_t s_wave[kScanThreads / 64];
+    __shared__ uint32_t s_err;
     // a failed removal (err: a compaction wait gave up, or the tally and the
-    // records disagree) leaves n - D meaningless: append nothing
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
+    // records disagree) leaves n - D meaningless: append nothing.  err is the
+    // host-mapped error word: ONE read per workgroup (a read per thread
+    // crossed PCIe 1024 times per workgroup, 360 us per update)
+    if (threadIdx.x == 0) s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (s_err != 0u) return;
     const uint64_t live = n - sp[2];
     uint64_t below = 0;  // used slots in the lower blocks
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kScanThreads) below += cnt[b];
