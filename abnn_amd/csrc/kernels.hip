@@ -533,11 +533,7 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
                 // the sweep stages the record's code (engine.h, src_code), random mode its src
                 src[j] = kRandom || q >= n ? e.y : code_src(e.y & 0xFFFFu, e.y >> 16);
                 f2[j] = src[j] < nn && f2_test(s_f2, src[j]);
-#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 5  // experiment: no bitmap gather
-                bw[j] = f2[j] ? ~0u : 0u;
-#else
                 bw[j] = f2[j] ? d.bitmap[src[j] >> 5] : 0u;
-#endif
                 dw[j] = f2[j] ? d.syn.dw[record_of(rel[j])] : make_uint2(0xFFFFFFFFu, 0u);  // one access for both
             }
         } else {
@@ -564,11 +560,7 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
             for (int j = 0; j < R; ++j) {
                 const uint32_t sn = src[j] < nn ? src[j] : 0u;
                 f2[j] = src[j] < nn && ((fa[j] >> (f2_hash1(sn) & 31u)) & (fb[j] >> (f2_hash2(sn) & 31u)) & 1u);
-#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 5
-                bw[j] = f2[j] ? ~0u : 0u;
-#else
                 bw[j] = d.bitmap[f2[j] ? sn >> 5 : 0u];
-#endif
                 dw[j] = d.syn.dw[f2[j] ? record_of(rel[j]) : 0];
             }
         }
@@ -585,19 +577,11 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
         if constexpr (!kTail) {
 #pragma unroll
             for (int j = 0; j < R; ++j)
-#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 4  // experiment: no lastFired gather
-                ld[j] = 0ull;
-#else
                 ld[j] = dst[j] - d.stim_first < d.stim_count ? now : (dst[j] < nn ? d.last_fired[dst[j]] : 0ull);
-#endif
         } else {
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 4
-                ld[j] = 0ull;
-#else
                 ld[j] = d.last_fired[dst[j] < nn ? dst[j] : 0u];
-#endif
             }
 #pragma unroll
             for (int j = 0; j < R; ++j)
@@ -1561,9 +1545,6 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // are staged (survivors go right after the range's earlier ones)
     auto flush_all = [&]() {
         const uint64_t tc = __builtin_amdgcn_s_memrealtime();
-#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 3  // experiment: staged events dropped
-        if (pend != 0xFFFFFFFFu) { pend = 0; return; }
-#endif
         const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, false>(d, kp, region, region + tot.y, pend, now, pass, Rw,
                                                                    rbw, spec, r, tot.z, s_f2, stage_at);
         tot.x += c.x;
@@ -1654,11 +1635,6 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             // first test (the reads are independent; SQ_LDS_BANK_CONFLICT is
             // half of SQ_LDS_IDX_ACTIVE, so they queue): 4 VALU per event
             // (quad_filter), no v_perm to assemble the codes
-#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 1  // 1: no filter test either, the records consumed
-#pragma unroll
-            for (int b = 0; b < NB8; ++b) asm volatile("" ::"v"(lo[b].x), "v"(lo[b].y), "v"(lo[b].z), "v"(lo[b].w), "v"(hi[b].x), "v"(hi[b].y));
-            if (rel != 0xFFFFFFFFu) return;
-#endif
             uint2 fb[K];
 #pragma unroll
             for (int b = 0; b < NB8; ++b) {
@@ -1672,13 +1648,6 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
                 H[2 * b] = quad_filter(fb + 8 * b, lo[b].x, lo[b].y, hi[b].x);
                 H[2 * b + 1] = quad_filter(fb + 8 * b + 4, lo[b].z, lo[b].w, hi[b].y);
             }
-#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER <= 2  // experiment builds only (tools/build_variant.sh): nothing is staged
-#pragma unroll
-            for (int i = 0; i < 2 * NB8; ++i) {
-                asm volatile("" ::"v"(H[i]));  // 2: the filter test runs, its result is dropped
-                H[i] = 0u;
-            }
-#endif
             if (last) {  // events past the sweep pass nothing
 #pragma unroll
                 for (int b = 0; b < NB8; ++b) {
@@ -1803,9 +1772,6 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         const bool lds_ok = kShard ? false : (kLean || (!d.shard_mode && !d.g2src));
         if (lds_ok && pend <= 256u) tail_lds = reinterpret_cast<uint4*>(s_stage[wid]);
     }
-#if defined(ABNN_ABLATE_FILTER) && ABNN_ABLATE_FILTER == 3  // experiment: staged events dropped
-    pend = 0;
-#endif
     const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, true>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
                                                                r, tot.z, s_f2, stage_at, tail_lds);
     const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
