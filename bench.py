@@ -452,8 +452,16 @@ def main():
     ev_a.record()
     step(args.steps)
     ev_b.record()
-    sync()
+    # the contract's closing bracket: a device-wide synchronize (it covers the
+    # brain's stream, torch's default one) and, across ranks, the barrier.
+    # brain.synchronize() -- the same wait once more, plus its error check --
+    # runs after the clock stops: a second host wake-up was ~1 us per pass of
+    # a 20-pass driver run
+    torch.cuda.synchronize(device)
+    if dist is not None:
+        dist.barrier()
     dt = time.perf_counter() - t0
+    brain.synchronize()
     region_ms = float(ev_a.elapsed_time(ev_b))
     stats = brain.stats()
     # then, untimed: an event pair around a sample of single launches (every
