@@ -1,6 +1,7 @@
 """GPU parity of structural plasticity (README §5; contract in include/abnn/abnn.h):
 pruning to tombstones in k_apply, synaptogenesis into per-pass budget slots,
-and the structural update (stable compaction + ordered append) -- HIP path vs
+and the structural update (the tombstones' span closed up, its hole filled
+from the array's end, then the ordered append; abnn.h) -- HIP path vs
 the CPU oracle, bit-exact, pass by pass, record count included.  No reference
 code exists for this; the oracle is cross-checked against an independent
 Python restatement in tests/test_oracle.py."""

@@ -365,6 +365,27 @@ def test_structural_update_removal_contract(tombs, expect):
     assert ob.syn["dst"].tolist() == expect
 
 
+def test_structural_update_is_not_the_stable_compaction():
+    """Deliberate change from round 4 (structural update): the
+    stable compaction of the whole array is a non-goal.  Where the two orders
+    differ, the records a sweep's visited window [0, events) holds after the
+    update differ too: here the window of 5 takes records 18, 19 (the hole's
+    fill), where the stable order would have given 5, 6."""
+    ob = O.OracleBrain(256, 256, 100, 20, 5, compact_every=1, w_prune=0.1, syn_capacity=20)
+    syn = np.zeros(20, dtype=O.SYN_DTYPE)
+    syn["src"] = 256 + np.arange(20)
+    syn["dst"] = np.arange(20)
+    syn["w"] = 0.5
+    syn["src"][[2, 4]] = 0xFFFFFFFF
+    syn["dst"][[2, 4]] = 0xFFFFFFFF
+    ob.set_synapses(syn)
+    ob.pass_serial()
+    got = ob.syn["dst"].tolist()
+    stable = [i for i in range(20) if i not in (2, 4)]
+    assert sorted(got) == stable and got != stable
+    assert got[:5] == [0, 1, 3, 18, 19] and stable[:5] == [0, 1, 3, 5, 6]
+
+
 def test_structural_update_semantics():
     ob = _sp_brain(0)
     n_nrn = ob.n_neuron()
