@@ -96,8 +96,8 @@ struct abnn_brain {
     int cus = 256, per_cu = 1;     // gate partition inputs (configure)
     uint64_t pass_host = 0;        // mirror of pass_index (structural-update schedule)
     uint64_t rot = 0;              // passes run by this handle: the bitmap buffers' rotation (never reset)
-    // structural updates (compact_every > 0): the second record buffer the
-    // compaction writes into (swapped with d.syn), and its scan scratch
+    // structural updates (compact_every > 0, in place: kernels.hip
+    // launch_structural_update): the span blocks' live-record offsets (k_span_offsets)
     uint64_t* compact_offsets = nullptr;
     uint32_t* compact_flags = nullptr;  // the in-place compaction's per-block read flags (epoch-tagged)
     unsigned long long* span_words = nullptr;  // the update's device words (kernels.hip k_span_init)
@@ -291,7 +291,8 @@ abnn_status validate_records(const abnn_brain* b, const abnn_synapse* s, uint64_
 }
 
 // Host-written records may hold tombstones (a saved pruned brain): recount the
-// structural update's per-block tally over them (pruning on only).
+// structural update's per-block tally over them (structural updates on only:
+// d.dead exists when compact_every > 0).
 abnn_status retally(abnn_brain* b, uint64_t first, uint64_t n)
 {
     if (!b->d.dead || n == 0) return ABNN_OK;
@@ -903,9 +904,9 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.dummy = dummy;
     if ((s = dalloc(&d.wg_stats, kWalkBlocks)) != ABNN_OK) return fail(s);
     if (p.mode == ABNN_MODE_RANDOM && (s = dalloc(&d.claim, cap)) != ABNN_OK) return fail(s);
-    if (p.compact_every > 0) {  // structural updates: the compaction's second buffer + scratch
+    if (p.compact_every > 0) {  // structural updates (in place): the span's offsets, read flags, words
         const uint64_t nb = (cap + kCompactChunk - 1) / kCompactChunk;
-        if ((s = dalloc(&b->compact_offsets, nb + 4)) != ABNN_OK) return fail(s);  // + the span's 3 words
+        if ((s = dalloc(&b->compact_offsets, nb + 4)) != ABNN_OK) return fail(s);  // <= nb used (+ slack)
         if ((s = dalloc(&b->compact_flags, nb)) != ABNN_OK) return fail(s);
         if ((s = dalloc(&b->span_words, 8)) != ABNN_OK) return fail(s);
         // the tombstone tally: pruning's, and an upload's (a saved pruned brain)
