@@ -70,7 +70,7 @@ class Scalars(C.Structure):
 
 
 MODE_SWEEP, MODE_RANDOM = 0, 1  # abnn_params.mode (include/abnn/abnn.h)
-ABI_VERSION = 9
+ABI_VERSION = 10
 LAYOUT_VERSION = 4
 
 
@@ -186,6 +186,9 @@ SIGNATURES = [
     ("abnn_comm_destroy", C.c_int, [_VP]),
     ("abnn_shard_traverse", C.c_int, [_VP, _VP, _U32, _VP]),
     ("abnn_comm_sync_visits", C.c_int, [_VP, _VP, _VP]),
+    ("abnn_comm_group_create", C.c_int, [_U32, C.POINTER(_VP)]),
+    ("abnn_comm_group_destroy", C.c_int, [_VP]),
+    ("abnn_comm_create_local", C.c_int, [_VP, _U32, C.c_int, C.POINTER(_VP)]),
     ("abnn_get_stats", C.c_int, [_VP, C.POINTER(Stats)]),
     ("abnn_reset_stats", C.c_int, [_VP]),
     ("abnn_enable_timing", C.c_int, [_VP, C.c_int]),
@@ -196,6 +199,9 @@ SIGNATURES = [
     ("abnn_save_flat", C.c_int, [_VP, C.c_char_p]),
     ("abnn_load_flat", C.c_int, [_VP, C.c_char_p]),
 ]
+
+# entry points new in ABI 10: an older A/B variant build (ABNN_LIB, timing only) may lack them
+ABI10_ADDITIONS = ("abnn_comm_group_create", "abnn_comm_group_destroy", "abnn_comm_create_local")
 
 _lib = None
 
@@ -225,7 +231,6 @@ DEBUG_SIGNATURES = [
     ("abnn_debug_raw_fused", C.c_int, [C.c_int]),
     ("abnn_debug_raw_fused_active", C.c_int, []),
     ("abnn_debug_raw_wave_clock", C.c_int, [_VP, C.c_uint64, _U32, _U32, C.POINTER(C.c_uint64), C.c_uint64, _VP]),
-    ("abnn_debug_set_compact_spin_limit", C.c_int, [_VP, _U32]),
 ]
 
 
@@ -241,8 +246,9 @@ def load() -> C.CDLL:
     _share_hip_runtime_with_torch()
     lib = C.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES + DEBUG_SIGNATURES:
-        if (name, res, args) in DEBUG_SIGNATURES and not hasattr(lib, name):
-            continue  # an older variant build (A/B timing) without this diagnostic
+        if not hasattr(lib, name) and ((name, res, args) in DEBUG_SIGNATURES or
+                                       (os.environ.get("ABNN_LIB") and name in ABI10_ADDITIONS)):
+            continue  # an older variant build (A/B timing) without this diagnostic / entry point
         fn = getattr(lib, name)  # AttributeError = the ABI is not exported
         fn.restype = res
         fn.argtypes = args

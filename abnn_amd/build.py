@@ -60,12 +60,34 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
-def build_hip(force: bool = False) -> str:
-    if force or _stale(LIB, HIP_DEPS):
-        tmp = LIB + ".tmp"
-        _run([HIPCC, *HIP_FLAGS, "-o", tmp, *HIP_SOURCES])
-        os.replace(tmp, LIB)
-    return LIB
+def build_hip(force: bool = False, out: str | None = None, defines: list[str] | None = None) -> str:
+    """The three translation units compiled in parallel (each ~20-60 s), then
+    linked.  out / defines: an experiment build (tools/build_variant.sh)."""
+    target = out or LIB
+    if force or out or _stale(target, HIP_DEPS):
+        comp = [f for f in HIP_FLAGS if f not in ("-shared", "-ldl")]
+        objs, procs = [], []
+        for src in HIP_SOURCES:
+            obj = f"{target}.{os.path.basename(src)}.o"
+            objs.append(obj)
+            cmd = [HIPCC, *comp, *(defines or []), "-c", "-o", obj, src]
+            procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+        errs = []
+        for cmd, p in procs:
+            o, e = p.communicate()
+            if p.returncode != 0:
+                errs.append(f"build failed ({p.returncode}): {' '.join(cmd)}\n{o}\n{e}")
+        if errs:
+            for obj in objs:
+                if os.path.exists(obj):
+                    os.remove(obj)
+            raise RuntimeError("\n".join(errs))
+        tmp = target + ".tmp"
+        _run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs, "-ldl"])
+        for obj in objs:
+            os.remove(obj)
+        os.replace(tmp, target)
+    return target
 
 
 def build_oracle(force: bool = False) -> str:

@@ -33,11 +33,13 @@ CONFIGS = {
                    "N_NRN=100k, N_SYN=10M, 10M events/pass"),
     # configs[2]: constants.h defaults -- the headline single-GPU workload
     "c3": Workload("c3", 256, 256, 5_000_000, 1_000_000_000, 150_000_000,
-                   "N_NRN=5,000,512, N_SYN=1B (16 GB as SynapsePacked; 12 GB src/dst/w arrays in HBM), 150M events/pass"),
+                   "N_NRN=5,000,512, N_SYN=1B (16 GB as SynapsePacked; 11 GB as the packed src/dst/w streams in HBM), 150M events/pass"),
     # configs[3]: the same graph sharded across GPUs (150M events/pass/GPU, capped by shard)
     "c4": Workload("c4", 256, 256, 5_000_000, 1_000_000_000, 150_000_000,
-                   "N_SYN=1B sharded N ways, 150M events/pass/GPU"),
-    # configs[4]: HBM-filling graph (64 GB of records; 8 GB per GPU at 8 ways)
+                   "N_NRN=5,000,512, N_SYN=1B split into one contiguous shard per GPU, 150M events/pass/GPU"),
+    # configs[4]: HBM-filling graph (64 GB as SynapsePacked, 44 GB packed; 5.5 GB per GPU at 8 ways).
+    # One GPU holds it whole (bench.py --config c5 runs it there); the label
+    # follows the shard count the run actually uses (bench.py workload_label)
     "c5": Workload("c5", 256, 256, 5_000_000, 4_000_000_000, 150_000_000,
-                   "N_SYN=4B sharded 8 ways"),
+                   "N_NRN=5,000,512, N_SYN=4B (HBM-filling), 150M events/pass/GPU"),
 }

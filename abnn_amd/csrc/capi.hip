@@ -6,9 +6,12 @@
 #include <rccl/rccl.h>  // types only: the entry points are resolved at run time (rccl_api)
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -97,12 +100,13 @@ struct abnn_brain {
     uint64_t pass_host = 0;        // mirror of pass_index (structural-update schedule)
     uint64_t rot = 0;              // passes run by this handle: the bitmap buffers' rotation (never reset)
     // structural updates (compact_every > 0, in place: kernels.hip
-    // launch_structural_update): the span blocks' live-record offsets (k_span_offsets)
+    // launch_structural_update): the hole blocks' ranks (k_swap_scan2), the
+    // scan's per-slice sums, the tail blocks' live prefix (k_swap_tail)
     uint64_t* compact_offsets = nullptr;
-    uint32_t* compact_flags = nullptr;  // the in-place compaction's per-block read flags (epoch-tagged)
+    uint64_t* swap_part = nullptr;
+    uint64_t* swap_toff = nullptr;
     unsigned long long* span_words = nullptr;  // the update's device words (kernels.hip k_span_init)
     uint32_t* grown_cnt = nullptr;             // used grown slots per 1024-slot block (k_grown_counts)
-    uint32_t compact_epoch = 0;
     uint64_t structural_updates = 0;  // run so far (abnn_structural_updates)
     uint64_t last_pass = ~0ull;       // pass_index of the last pass (its spike list: abnn_get_budget)
     // host-mapped error word: a fused pass whose look-back wait gave up sets it
@@ -121,7 +125,6 @@ struct abnn_brain {
     // reloaded (abnn_load_bnn / abnn_load_flat / abnn_generate_synapses / an
     // upload of every record)
     bool records_invalid = false;
-    uint32_t compact_spin_limit = kLbSpinLimit;  // abnn_debug_set_compact_spin_limit
 };
 
 namespace {
@@ -161,7 +164,7 @@ void free_all(abnn_brain* b)
                     b->d.range_info,    b->d.range_g1,  b->d.g2x,
                     b->d.chunk_cnt,
                     b->d.wg_stats, b->d.claim,  b->d.g2src,      b->d.grown,
-                    b->d.dead,      b->compact_offsets, b->compact_flags, b->span_words, b->grown_cnt,
+                    b->d.dead,      b->compact_offsets, b->swap_part, b->swap_toff, b->span_words, b->grown_cnt,
                     b->d.work,      b->idx_scratch,
                     b->u64_scratch,  b->d.wave_clock,  b->d.apply_clock, b->d.fired_ring, b->d.n_fired_ring, b->d.range_bounds,  b->d.range_bounds_next, b->d.range_bounds_prev,
                     const_cast<uint32_t*>(b->d.dummy)};
@@ -395,12 +398,10 @@ abnn_status structural_update(abnn_brain* b)
     // the whole update on the device (kernels.hip launch_structural_update):
     // the tally's span, its offsets, the in-place compaction, the hole, the
     // grown records; one synchronisation reads D and the records appended
-    b->compact_epoch += 1;
     *b->err_host = 0;
     unsigned long long* sp = b->span_words;
-    hipError_t e = launch_structural_update(d.syn, n, cap, d.dead, nb, b->compact_offsets, sp, b->compact_flags,
-                                            b->compact_epoch, d.err_word, b->compact_spin_limit, (uint32_t)b->cus, d.grown,
-                                            slots, b->grown_cnt,
+    hipError_t e = launch_structural_update(d.syn, n, cap, d.dead, nb, b->compact_offsets, b->swap_part, b->swap_toff,
+                                            sp, d.err_word, (uint32_t)b->cus, d.grown, slots, b->grown_cnt,
                                             reinterpret_cast<unsigned long long*>(&d.work->stats.grown), nullptr);
     unsigned long long w[5] = {0, 0, 0, 0, 0};
     if (e == hipSuccess) e = hipMemcpy(w, sp, sizeof(w), hipMemcpyDeviceToHost);
@@ -416,10 +417,8 @@ abnn_status structural_update(abnn_brain* b)
         // be rolled back: passes are refused until the records are reloaded
         *b->err_host = 0;
         b->records_invalid = true;
-        set_err(err == 2 ? "structural update: the tombstone tally and the records disagree; "
-                           "the records are not valid, reload them (abnn_load_bnn / abnn_load_flat)"
-                         : "structural update: the in-place compaction's wait timed out; "
-                           "the records are not valid, reload them (abnn_load_bnn / abnn_load_flat)");
+        set_err("structural update: the tombstone tally and the records disagree; "
+                "the records are not valid, reload them (abnn_load_bnn / abnn_load_flat)");
         return ABNN_ERR_HIP;
     }
     b->dims.n_syn = n - w[2] + w[4];
@@ -879,7 +878,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     }
     for (int i = 0; i < 2; ++i)
         if ((s = dalloc(&b->cost_buf[i], max_ranges)) != ABNN_OK) return fail(s);
-    if ((s = dalloc(&d.lb_status, kMaxGateBlocks)) != ABNN_OK) return fail(s);
+    // look-back words, then the lazy workgroups' second words (kLbLazy)
+    if ((s = dalloc(&d.lb_status, 2 * kMaxGateBlocks)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.cand_list, (uint64_t)kFusedMaxRanges * kCandCap)) != ABNN_OK) return fail(s);
     if (const char* env = std::getenv("ABNN_FUSED")) b->use_fused = std::atoi(env) != 0;
     d.spec_mode = 1;
@@ -891,6 +891,13 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.lean = 1;
     if (const char* env = std::getenv("ABNN_LEAN")) d.lean = std::atoi(env) != 0;
     if (const char* env = std::getenv("ABNN_SPEC")) d.spec_mode = (uint32_t)std::min(2, std::max(0, std::atoi(env)));
+    // the lazy isi (kernels.hip refrac_chunk): a dst the filter rules out is
+    // older than window_pre, so it passes the refractory gate unread only if
+    // refractory <= window_pre
+    d.lazy_isi = p.refractory <= p.window_pre ? 1u : 0u;
+    if (const char* env = std::getenv("ABNN_LAZY")) d.lazy_isi = d.lazy_isi && std::atoi(env) != 0 ? 1u : 0u;
+    d.lazy_margin = 3;
+    if (const char* env = std::getenv("ABNN_LAZY_MARGIN")) d.lazy_margin = (uint32_t)std::max(0, std::atoi(env));
     d.bitmap = b->bitmap_buf[0];
     d.filter = b->filter_buf[0];
     if ((s = dalloc(&d.range_info, max_ranges)) != ABNN_OK) return fail(s);
@@ -907,7 +914,8 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     if (p.compact_every > 0) {  // structural updates (in place): the span's offsets, read flags, words
         const uint64_t nb = (cap + kCompactChunk - 1) / kCompactChunk;
         if ((s = dalloc(&b->compact_offsets, nb + 4)) != ABNN_OK) return fail(s);  // <= nb used (+ slack)
-        if ((s = dalloc(&b->compact_flags, nb)) != ABNN_OK) return fail(s);
+        if ((s = dalloc(&b->swap_part, (nb + kScanThreads - 1) / kScanThreads + 1)) != ABNN_OK) return fail(s);
+        if ((s = dalloc(&b->swap_toff, nb + 4)) != ABNN_OK) return fail(s);  // tail blocks + 1 <= nb + 2
         if ((s = dalloc(&b->span_words, 8)) != ABNN_OK) return fail(s);
         // the tombstone tally: pruning's, and an upload's (a saved pruned brain)
         if ((s = dalloc(&d.dead, nb)) != ABNN_OK) return fail(s);
@@ -1103,6 +1111,9 @@ abnn_status abnn_set_last_visited(abnn_brain* b, uint64_t first, const uint64_t*
     // a host write is replicated on every shard (the neuron state is): it
     // replaces whatever this shard visited before it
     if (b->d.visit_mark && n) HIP_TRY(hipMemset(b->d.visit_mark + first, 0, n));
+    // a write of the whole array leaves no unmerged mark (as abnn_load_flat):
+    // a single-rank restore may then move the clock back (abnn_set_scalars)
+    if (first == 0 && n == b->n_nrn) b->marks_dirty = false;
     return ABNN_OK;
 }
 
@@ -1321,19 +1332,11 @@ abnn_status abnn_shard_visits_merge(abnn_brain* b, const void* reduced_dev, void
     return ABNN_OK;
 }
 
-// Diagnostics (abnn_debug.h): the in-place compaction's poll limit (0 = every
-// wait gives up at once: the structural update's error path).
-abnn_status abnn_debug_set_compact_spin_limit(abnn_brain* b, uint32_t limit)
-{
-    REQUIRE(b, "null argument");
-    b->compact_spin_limit = limit;
-    return ABNN_OK;
-}
-
 // ---- sharded passes over RCCL ------------------------------------------------
 
 struct abnn_comm {
     ncclComm_t comm = nullptr;
+    abnn_comm_group* local = nullptr;  // in-process group (abnn_comm_create_local): no RCCL
     uint32_t world = 1, rank = 0;
     int device = 0;
     char* gathered = nullptr;   // world exchange records, rank order
@@ -1342,7 +1345,171 @@ struct abnn_comm {
     uint64_t* visits = nullptr;   // the lastVisited merge's deltas (n_nrn words, sized on first use)
     uint64_t visits_n = 0;
     bool broken = false;          // an earlier pass failed on this rank (abnn.h: abort on every rank)
+    // in-process group: this rank's events (its stream reached the collective /
+    // its reads of the peers' buffers are enqueued) and the all-reduce's
+    // accumulator and peer staging buffer (sized on first use)
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+    uint64_t* red_acc = nullptr;
+    uint64_t* red_in = nullptr;
+    uint64_t red_n = 0;
 };
+
+// ---- in-process communicator group (abnn.h abnn_comm_group) -----------------
+// `world` ranks in ONE process, one host thread per rank (SURVEY §4 item 4's
+// fake communicator behind the same comm interface): the collectives
+// abnn_shard_traverse / abnn_comm_sync_visits need -- the in-place all-gather
+// of the exchange records and the all-reduce(MAX / SUM) of u64 words -- are
+// device copies and a reduction kernel on each rank's own stream, between two
+// host barriers:
+//   1. every rank records ev_ready on its stream (its inputs are enqueued),
+//      barrier;
+//   2. every rank's stream waits for the peers' ev_ready, copies / reduces the
+//      peers' buffers into its own (rank order), records ev_done, barrier;
+//   3. every rank's stream waits for the peers' ev_done (no rank overwrites a
+//      buffer a peer still reads).
+// No GPU work ever waits for the host, so a rank blocked in a host
+// synchronisation never holds up a peer.  Ranks on one device must pass one
+// stream (a pass keeps one workgroup per CU resident for its look-back: two
+// passes must not run at once); ranks on different devices copy over
+// xGMI/PCIe (hipMemcpyDefault).  A barrier that waits longer than
+// kGroupTimeout, or a rank that fails (abnn_shard_traverse error), breaks the
+// group: every later collective on it fails at once.
+struct abnn_comm_group {
+    uint32_t world = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    uint64_t gen = 0;       // barrier generation
+    uint32_t arrived = 0;
+    bool broken = false;
+    std::string why;
+    std::vector<abnn_comm*> ranks;     // registered communicators (null: free slot)
+    std::vector<const char*> buf;      // this collective's buffer of every rank
+    std::vector<hipStream_t> streams;  // ... and its stream
+};
+
+namespace {
+
+constexpr auto kGroupTimeout = std::chrono::seconds(300);
+
+void group_break(abnn_comm_group* g, const std::string& why)
+{
+    std::lock_guard<std::mutex> lk(g->m);
+    if (!g->broken) g->why = why;
+    g->broken = true;
+    g->cv.notify_all();
+}
+
+abnn_status group_barrier(abnn_comm_group* g)
+{
+    std::unique_lock<std::mutex> lk(g->m);
+    if (g->broken) {
+        set_err("local communicator group is broken: " + g->why);
+        return ABNN_ERR_INVALID;
+    }
+    const uint64_t my = g->gen;
+    if (++g->arrived == g->world) {
+        g->arrived = 0;
+        ++g->gen;
+        g->cv.notify_all();
+        return ABNN_OK;
+    }
+    if (!g->cv.wait_for(lk, kGroupTimeout, [&] { return g->gen != my || g->broken; })) {
+        g->broken = true;
+        g->why = "a rank did not reach a collective within 300 s";
+        g->cv.notify_all();
+    }
+    if (g->broken) {
+        set_err("local communicator group is broken: " + g->why);
+        return ABNN_ERR_INVALID;
+    }
+    return ABNN_OK;
+}
+
+// Steps 1-2 of a collective: publish (buf, s), wait for every rank, check the
+// stream rule, and make s wait for every peer's inputs.
+abnn_status group_enter(abnn_comm* c, const void* buf, hipStream_t s)
+{
+    abnn_comm_group* g = c->local;
+    g->buf[c->rank] = static_cast<const char*>(buf);
+    g->streams[c->rank] = s;
+    HIP_TRY(hipEventRecord(c->ev_ready, s));
+    ST_TRY(group_barrier(g));
+    for (uint32_t j = 0; j < g->world; ++j) {
+        if (j == c->rank) continue;
+        if (g->ranks[j]->device == c->device && g->streams[j] != s) {
+            // every rank sees the same mismatch and fails the same way
+            set_err("local communicator: ranks on one device must pass the same stream (their passes must not "
+                    "run at once)");
+            return ABNN_ERR_INVALID;
+        }
+        HIP_TRY(hipStreamWaitEvent(s, g->ranks[j]->ev_ready, 0));
+    }
+    return ABNN_OK;
+}
+
+// Step 3: the peers' reads of this rank's buffer are enqueued before s goes on.
+abnn_status group_leave(abnn_comm* c, hipStream_t s)
+{
+    abnn_comm_group* g = c->local;
+    HIP_TRY(hipEventRecord(c->ev_done, s));
+    ST_TRY(group_barrier(g));
+    for (uint32_t j = 0; j < g->world; ++j)
+        if (j != c->rank) HIP_TRY(hipStreamWaitEvent(s, g->ranks[j]->ev_done, 0));
+    return ABNN_OK;
+}
+
+abnn_status local_all_gather(abnn_comm* c, char* recv, uint64_t bytes, hipStream_t s)
+{
+    abnn_comm_group* g = c->local;
+    ST_TRY(group_enter(c, recv, s));
+    for (uint32_t j = 0; j < g->world; ++j)  // slot j of every rank's buffer = rank j's record
+        if (j != c->rank)
+            HIP_TRY(hipMemcpyAsync(recv + bytes * j, g->buf[j] + bytes * j, bytes, hipMemcpyDefault, s));
+    return group_leave(c, s);
+}
+
+abnn_status local_all_reduce_u64(abnn_comm* c, uint64_t* buf, uint64_t n, bool max, hipStream_t s)
+{
+    abnn_comm_group* g = c->local;
+    if (c->red_n < n) {  // before the barrier: a failed allocation must not leave peers waiting in step 2
+        if (c->red_acc) (void)hipFree(c->red_acc);
+        if (c->red_in) (void)hipFree(c->red_in);
+        c->red_acc = c->red_in = nullptr;
+        c->red_n = 0;
+        if (dalloc(&c->red_acc, n) != ABNN_OK || dalloc(&c->red_in, n) != ABNN_OK) {
+            group_break(g, "rank " + std::to_string(c->rank) + " could not allocate the all-reduce buffers");
+            return ABNN_ERR_OOM;
+        }
+        c->red_n = n;
+    }
+    ST_TRY(group_enter(c, buf, s));
+    HIP_TRY(hipMemcpyAsync(c->red_acc, buf, n * 8, hipMemcpyDefault, s));
+    for (uint32_t j = 0; j < g->world; ++j) {
+        if (j == c->rank) continue;
+        HIP_TRY(hipMemcpyAsync(c->red_in, g->buf[j], n * 8, hipMemcpyDefault, s));
+        HIP_TRY(launch_reduce_u64(c->red_acc, c->red_in, n, max, s));
+    }
+    ST_TRY(group_leave(c, s));
+    HIP_TRY(hipMemcpyAsync(buf, c->red_acc, n * 8, hipMemcpyDefault, s));
+    return ABNN_OK;
+}
+
+}  // namespace
+
+// The collectives of the sharded pass, over RCCL or the in-process group.
+static abnn_status comm_all_gather(abnn_comm* c, char* recv, uint64_t bytes, hipStream_t s)
+{
+    if (c->local) return local_all_gather(c, recv, bytes, s);
+    RCCL_TRY(rccl_api().all_gather(recv + bytes * c->rank, recv, bytes, ncclInt8, c->comm, s));  // in place
+    return ABNN_OK;
+}
+
+static abnn_status comm_all_reduce_u64(abnn_comm* c, uint64_t* buf, uint64_t n, bool max, hipStream_t s)
+{
+    if (c->local) return local_all_reduce_u64(c, buf, n, max, s);
+    RCCL_TRY(rccl_api().all_reduce(buf, buf, n, ncclUint64, max ? ncclMax : ncclSum, c->comm, s));
+    return ABNN_OK;
+}
 
 // The lastVisited merge on the stream: every rank's deltas
 // (k_visits_delta), one all-reduce(MAX) of n_nrn words in place, the merge.
@@ -1358,7 +1525,7 @@ static abnn_status merge_visits(abnn_brain* b, abnn_comm* c, hipStream_t s)
         c->visits_n = b->n_nrn;
     }
     HIP_TRY(launch_visits_delta(b->d.last_visited, b->d.visit_mark, c->visits, b->n_nrn, s));
-    RCCL_TRY(rccl_api().all_reduce(c->visits, c->visits, b->n_nrn, ncclUint64, ncclMax, c->comm, s));
+    ST_TRY(comm_all_reduce_u64(c, c->visits, b->n_nrn, true, s));
     HIP_TRY(launch_visits_merge(b->d.last_visited, b->d.visit_mark, c->visits, b->n_nrn, s));
     b->marks_dirty = false;
     return ABNN_OK;
@@ -1416,10 +1583,74 @@ abnn_status abnn_comm_destroy(abnn_comm* c)
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     if (c->comm) rccl_api().comm_destroy(c->comm);
-    if (c->gathered) (void)hipFree(c->gathered);
-    if (c->scratch) (void)hipFree(c->scratch);
-    if (c->visits) (void)hipFree(c->visits);
+    if (c->local) {
+        std::lock_guard<std::mutex> lk(c->local->m);
+        c->local->ranks[c->rank] = nullptr;
+    }
+    for (void* p : {(void*)c->gathered, (void*)c->scratch, (void*)c->visits, (void*)c->red_acc, (void*)c->red_in})
+        if (p) (void)hipFree(p);
+    if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     delete c;
+    return ABNN_OK;
+}
+
+abnn_status abnn_comm_group_create(uint32_t world, abnn_comm_group** out)
+{
+    REQUIRE(out && world >= 1 && world <= 4096, "bad argument");
+    abnn_comm_group* g = new (std::nothrow) abnn_comm_group();
+    if (!g) return ABNN_ERR_OOM;
+    g->world = world;
+    g->ranks.assign(world, nullptr);
+    g->buf.assign(world, nullptr);
+    g->streams.assign(world, nullptr);
+    *out = g;
+    return ABNN_OK;
+}
+
+abnn_status abnn_comm_group_destroy(abnn_comm_group* g)
+{
+    if (!g) return ABNN_OK;
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        for (abnn_comm* c : g->ranks)
+            REQUIRE(c == nullptr, "abnn_comm_group_destroy: destroy every rank's communicator first");
+    }
+    delete g;
+    return ABNN_OK;
+}
+
+abnn_status abnn_comm_create_local(abnn_comm_group* g, uint32_t rank, int device, abnn_comm** out)
+{
+    REQUIRE(g && out, "null argument");
+    REQUIRE(rank < g->world, "rank out of range");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(device));
+    abnn_comm* c = new (std::nothrow) abnn_comm();
+    if (!c) return ABNN_ERR_OOM;
+    c->local = g;
+    c->world = g->world;
+    c->rank = rank;
+    c->device = device;
+    if (hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
+        dalloc(&c->scratch, 1) != ABNN_OK) {
+        c->local = nullptr;
+        abnn_comm_destroy(c);
+        set_err("abnn_comm_create_local: event or buffer allocation failed");
+        return ABNN_ERR_OOM;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        if (g->ranks[rank] != nullptr) {
+            c->local = nullptr;
+            abnn_comm_destroy(c);
+            set_err("abnn_comm_create_local: rank already has a communicator in this group");
+            return ABNN_ERR_INVALID;
+        }
+        g->ranks[rank] = c;
+    }
+    *out = c;
     return ABNN_OK;
 }
 
@@ -1430,7 +1661,6 @@ abnn_status abnn_comm_destroy(abnn_comm* c)
 // half-done pass is dropped (no walk of a gate whose exchange never came).
 static abnn_status shard_traverse_passes(abnn_brain* b, abnn_comm* c, uint32_t passes, hipStream_t s)
 {
-    const RcclApi& r = rccl_api();
     const uint64_t rec = abnn_exchange_bytes(b);
     if (rec != c->rec_bytes) {  // the records' size follows the budget: sized on first use
         if (c->gathered) HIP_TRY(hipFree(c->gathered));
@@ -1441,7 +1671,7 @@ static abnn_status shard_traverse_passes(abnn_brain* b, abnn_comm* c, uint32_t p
     char* mine = c->gathered + rec * c->rank;
     for (uint32_t i = 0; i < passes; ++i) {
         ST_TRY(abnn_shard_gate(b, mine, s));
-        RCCL_TRY(r.all_gather(mine, c->gathered, rec, ncclInt8, c->comm, s));  // in place, rank order
+        ST_TRY(comm_all_gather(c, c->gathered, rec, s));  // in place, rank order
         ST_TRY(abnn_shard_apply(b, c->gathered, c->world, c->rank, s));
         const uint64_t updates = b->structural_updates, renorms = b->renorms;
         ST_TRY(abnn_shard_commit(b, c->gathered, c->world, s));
@@ -1453,7 +1683,7 @@ static abnn_status shard_traverse_passes(abnn_brain* b, abnn_comm* c, uint32_t p
             // same pass): re-sum the visited events for the clock-tick rule
             uint64_t mine_ev = visited_events(b->dims, b->params.mode), tot = 0;
             HIP_TRY(hipMemcpyAsync(c->scratch, &mine_ev, 8, hipMemcpyHostToDevice, s));
-            RCCL_TRY(r.all_reduce(c->scratch, c->scratch, 1, ncclUint64, ncclSum, c->comm, s));
+            ST_TRY(comm_all_reduce_u64(c, c->scratch, 1, false, s));
             HIP_TRY(hipMemcpyAsync(&tot, c->scratch, 8, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
             b->dims.global_events = tot;
@@ -1462,17 +1692,26 @@ static abnn_status shard_traverse_passes(abnn_brain* b, abnn_comm* c, uint32_t p
     return ABNN_OK;
 }
 
-abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, void* stream)
+static abnn_status shard_traverse_checked(abnn_brain* b, abnn_comm* c, uint32_t passes, void* stream)
 {
-    REQUIRE(b && c, "null argument");
+    REQUIRE(b, "null argument");
     REQUIRE(c->device == b->device, "communicator and handle are on different devices");
     REQUIRE(!c->broken, "communicator unusable after an earlier error on this rank: abort / destroy it on every rank");
     HIP_TRY(hipSetDevice(b->device));
-    abnn_status st = pass_error(b);
-    if (st == ABNN_OK) st = shard_traverse_passes(b, c, passes, pick(b, stream));
+    ST_TRY(pass_error(b));
+    return shard_traverse_passes(b, c, passes, pick(b, stream));
+}
+
+abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, void* stream)
+{
+    REQUIRE(c, "null argument");
+    const abnn_status st = shard_traverse_checked(b, c, passes, stream);
     if (st != ABNN_OK) {
         c->broken = true;
-        b->pending_walk = false;
+        if (b) b->pending_walk = false;
+        // the peers are in (or about to enter) this pass's collectives: an
+        // in-process group lets them fail at once (RCCL ranks abort)
+        if (c->local) group_break(c->local, "rank " + std::to_string(c->rank) + ": " + g_err);
     }
     return st;
 }
@@ -1487,8 +1726,7 @@ abnn_status abnn_debug_comm_allgather(abnn_comm* c, void* buf, uint64_t bytes, u
     HIP_TRY(hipSetDevice(c->device));
     const hipStream_t s = static_cast<hipStream_t>(stream);
     char* base = static_cast<char*>(buf);
-    for (uint32_t i = 0; i < count; ++i)
-        RCCL_TRY(rccl_api().all_gather(base + bytes * c->rank, base, bytes, ncclInt8, c->comm, s));
+    for (uint32_t i = 0; i < count; ++i) ST_TRY(comm_all_gather(c, base, bytes, s));
     return ABNN_OK;
 }
 
@@ -1504,7 +1742,10 @@ abnn_status abnn_comm_sync_visits(abnn_brain* b, abnn_comm* c, void* stream)
         set_err("hipStreamSynchronize failed after the lastVisited merge");
         st = ABNN_ERR_HIP;
     }
-    if (st != ABNN_OK) c->broken = true;
+    if (st != ABNN_OK) {
+        c->broken = true;
+        if (c->local) group_break(c->local, "rank " + std::to_string(c->rank) + ": " + g_err);
+    }
     return st;
 }
 

@@ -48,7 +48,9 @@ struct alignas(16) PassWork {
     uint32_t epoch;        // fused passes run so far: tags this pass's look-back words (never set by the host)
     uint32_t error;        // unused (the error word is host-mapped: DeviceState::err_word)
     uint32_t spec_wgs;     // fused pass: gate workgroups predicted below the budget cut (the last pass's, less one)
-    uint32_t pad;
+    uint32_t lazy_from;    // fused pass: gate workgroups from this one on are predicted past the budget cut
+                           // (the last pass's cut + 1 + lazy_margin; 0: none): their refractory stage gathers
+                           // lastFired[dst] only where the LDS filter says dst may be recent
     unsigned long long shard_g2;  // sharded fused pass: refractory survivors of the shard (the summary's word 3)
     // sharded fused pass: the pass-start scalars as the gate launch read them
     // (written by its workgroup 0), so every k_shard_walk workgroup reads
@@ -64,6 +66,14 @@ struct alignas(16) PassWork {
 // kind 1 = the spike candidates of the workgroup's ranges (capped at the
 // budget).  max_spikes < 2^30.
 constexpr uint32_t kLbAggregate = 1u;
+// kind bit 1 (word bit 31): the workgroup holds survivors whose isi it did not
+// gather (lazy); if it lies below the budget cut its walk reads lastFired for
+// them and then publishes its second word (lb_status[kMaxGateBlocks + b] =
+// tag << 32 | 1), which the stampers wait for before they stamp
+constexpr uint32_t kLbLazy = 2u;
+// a survivor entry's dst with this bit set: isi not gathered (its updated
+// weight is computed by the walk, if the entry is below the budget)
+constexpr uint32_t kDstLazy = 0x80000000u;
 constexpr uint32_t kLbSpinLimit = 1u << 22;  // ~1 s of polls: then error, never a hang
 
 // Synapse records on the device, structure of arrays: record
@@ -178,6 +188,9 @@ struct DeviceState {
     uint32_t spec_mode;       // fused: speculative weight stores 0 off, 1 below the predicted cut (default),
                               // 2 everywhere (ABNN_SPEC; 2 exercises the restore path)
     uint32_t lean;            // fused single-GPU pass without plasticity: the lean kernel (ABNN_LEAN, default 1)
+    uint32_t lazy_isi;        // fused single-GPU pass: workgroups predicted past the cut skip lastFired[dst] for
+                              // dsts the LDS filter rules out (needs refractory <= window_pre; ABNN_LAZY, default 1)
+    uint32_t lazy_margin;     // ... workgroups past the last cut that still gather eagerly (ABNN_LAZY_MARGIN, 3)
     uint32_t shard_mode;      // fused pass = the first launch of a sharded pass (k_gate: no stamps, exchange record)
     int32_t* xchg;            // ... its exchange record (abnn.h: summary + local spike list)
     uint32_t prologue_adapt;  // the previous pass was fused over the same ranges: its costs move the next
@@ -255,20 +268,23 @@ hipError_t launch_renorm(const DeviceState& d, uint64_t base, hipStream_t s);
 hipError_t launch_pack_src(const SynArrays& a, const uint32_t* in_dev, uint64_t first, uint64_t n, hipStream_t s);
 hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t first, uint64_t n, hipStream_t s);
 // Structural update (abnn.h contract, capi.hip structural_update), all on `s`:
-// the tally's span {first block, last block + 1, tombstones, z, appended} in
-// sp, its blocks' offsets, the in-place compaction (one workgroup per CU; a
-// poll that reaches spin_limit sets *err = 1 and is never a hang), the hole
-// filled from the array's end (*err = 2: the tally and the records disagree),
-// then the grown records appended -- skipped when *err is set.
+// the tally's tombstones D and their blocks into sp, the holes' ranks (offsets,
+// part: the scan's per-slice sums), the tail's live prefix when the tail holds
+// tombstones (toff), the fill of every tombstone below m = n - D from the tail
+// [m, n) (*err = 2: the tally and the records disagree), the tally cleared, then
+// the grown records appended -- skipped when *err is set.
 hipError_t launch_structural_update(const SynArrays& syn, uint64_t n, uint64_t cap, uint32_t* dead, uint64_t nb,
-                                    uint64_t* offsets, unsigned long long* sp, uint32_t* flags, uint32_t epoch,
-                                    uint32_t* err, uint32_t spin_limit, uint32_t cus, uint4* grown, uint64_t slots,
-                                    uint32_t* grown_cnt, unsigned long long* stats_grown, hipStream_t s);
+                                    uint64_t* offsets, uint64_t* part, uint64_t* toff, unsigned long long* sp,
+                                    uint32_t* err, uint32_t cus, uint4* grown, uint64_t slots, uint32_t* grown_cnt,
+                                    unsigned long long* stats_grown, hipStream_t s);
 // The sharded lastVisited merge (kernels.hip k_visits_delta / k_visits_merge):
 // delta[i] = mark[i] ? lv[i] + 1 : 0; after the all-reduce(MAX), lv[i] =
 // reduced[i] - 1 where it is non-zero, and every mark clears.
 hipError_t launch_visits_delta(const uint64_t* lv, const uint8_t* mark, uint64_t* delta, uint64_t n, hipStream_t s);
 hipError_t launch_visits_merge(uint64_t* lv, uint8_t* mark, const uint64_t* reduced, uint64_t n, hipStream_t s);
+// acc[i] = max(acc[i], x[i]) (max) or acc[i] + x[i]: the in-process
+// communicator's all-reduce (capi.hip, abnn_comm_group), one peer at a time
+hipError_t launch_reduce_u64(uint64_t* acc, const uint64_t* x, uint64_t n, bool max, hipStream_t s);
 // dead[] (pruning tally) recounted for the blocks that hold records [first, first + count) of n
 hipError_t launch_tally_dead(const SynArrays& a, uint64_t n, uint32_t* dead, uint64_t first, uint64_t count,
                              hipStream_t s);

@@ -309,6 +309,18 @@ __device__ __forceinline__ bool f2_test(const uint32_t* s_f2, uint32_t n)
     return ((s_f2[h1 >> 5] >> (h1 & 31u)) & (s_f2[h2 >> 5] >> (h2 & 31u)) & 1u) != 0u;
 }
 
+// Whether neuron n may be recent at pass start (the blocked filter of the LDS
+// copy and the second-level filter; no false negatives): the refractory
+// stage's test of a dst.  A dst it rules out is older than window_pre, so
+// with refractory <= window_pre it passes the refractory gate without its
+// lastFired being read (the lazy isi).
+__device__ __forceinline__ bool nrn_maybe_recent(const uint2* s_fb, const uint32_t* s_f2, uint32_t n)
+{
+    const uint32_t j = n >> 5, t = filter_t(j, 13), g = (j ^ t) & (kCodeFilterWords - 1);
+    const uint2 f = s_fb[g];
+    return ((f.x >> (n & 31u)) & (f.y >> ((n + t) & 31u)) & 1u) && f2_test(s_f2, n);
+}
+
 // ---------------------------------------------------------------------------
 // k_bitmap: bit i = (now - lastFired[i]) <= window_pre; stimulus stamp fused.
 // A wave covers 256 neurons = four bitmap words; lane l owns neurons
@@ -500,14 +512,34 @@ __device__ __forceinline__ uint4 range_totals(const DeviceState& d, uint32_t r) 
 // (the workgroup is predicted to lie below the pass's budget cut) the updated
 // weight is stored here already; the walk restores w where the prediction was
 // wrong.
+// The lazy isi is an experiment compiled in only
+// with -DABNN_LAZY_ISI (tools/build_variant.sh): measured slower than the
+// eager refractory stage, so the product builds without it.
+#ifdef ABNN_LAZY_ISI
+constexpr bool kLazyBuild = true;
+#else
+constexpr bool kLazyBuild = false;
+#endif
+
+// lazy (fused sweep, a workgroup predicted past the budget cut; wave-uniform):
+// lastFired[dst] is gathered only where the filter (s_fb, s_f2) says dst may
+// be recent; the other survivors pass the refractory gate on the filter's word
+// (age > window_pre >= refractory) and are stored with kDstLazy and no updated
+// weight -- the walk computes it if such an entry falls below the budget.
+// The fourth count returned is the number of such survivors.
 template <int R, bool kRandom, bool kFused, bool kTail, class At>
 __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const KernelParams& kp, uint64_t region,
                                               uint64_t base, uint32_t n, uint64_t now, uint64_t pass, float Rw,
                                               float rbw, bool spec, uint32_t crange, uint32_t c0,
-                                              const uint32_t* s_f2, At&& at, uint4* lds_out = nullptr)
+                                              const uint32_t* s_f2, At&& at, uint4* lds_out = nullptr,
+                                              bool lazy = false, const uint2* s_fb = nullptr)
 {
     const uint32_t lane = threadIdx.x & 63, nn = (uint32_t)d.n_nrn;
-    uint32_t n_g1 = 0, n_g2 = 0, n_cand = 0;
+    uint32_t n_g1 = 0, n_g2 = 0, n_cand = 0, n_lazy = 0;
+    // (the tail only: in the steady state a sparse range's staged events all
+    // wait for its tail, and the dense ranges lie below the cut, eager; every
+    // mid-stream instance of this function would grow the stream loop's code)
+    constexpr bool kLazyOk = kLazyBuild && kFused && !kRandom && kTail;
     auto record_of = [&](uint32_t rel) -> uint64_t {
         const uint64_t t = region + rel;
         return kRandom ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : t;
@@ -574,14 +606,26 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
         }
         // the stimulus of this pass is stamped `now` (brain.cpp:82) by k_bitmap
         // or, in steady state, by the gate itself at some point of the pass
+        // lz: lazy, dst not recent (filter), so its lastFired is not read
+        bool lz[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            lz[j] = false;
+            if constexpr (kLazyOk)
+                lz[j] = lazy && dst[j] < nn && dst[j] - d.stim_first >= d.stim_count &&
+                        !nrn_maybe_recent(s_fb, s_f2, dst[j]);
+        }
         if constexpr (!kTail) {
 #pragma unroll
             for (int j = 0; j < R; ++j)
-                ld[j] = dst[j] - d.stim_first < d.stim_count ? now : (dst[j] < nn ? d.last_fired[dst[j]] : 0ull);
+                ld[j] = dst[j] - d.stim_first < d.stim_count ? now
+                                                             : (dst[j] < nn && !lz[j] ? d.last_fired[dst[j]] : 0ull);
         } else {
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                ld[j] = d.last_fired[dst[j] < nn ? dst[j] : 0u];
+                const bool need = dst[j] < nn && !lz[j];
+                // (lazy: a round none of whose lanes needs its lastFired issues no load)
+                ld[j] = (!kLazyOk || !lazy || __ballot(need) != 0) ? d.last_fired[need ? dst[j] : 0u] : 0ull;
             }
 #pragma unroll
             for (int j = 0; j < R; ++j)
@@ -591,16 +635,18 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
         for (int j = 0; j < R; ++j) {
             if (b0 + (uint32_t)j * 64 >= n) break;  // wave-uniform
             n_g1 += (uint32_t)__popcll(__ballot(bw[j] != 0u));
-            const bool g2 = dst[j] < nn && age32(now, ld[j]) > kp.refractory;  // brain.metal:79-83
+            // brain.metal:79-83 (lz: older than window_pre >= refractory)
+            const bool g2 = dst[j] < nn && (lz[j] || age32(now, ld[j]) > kp.refractory);
             const uint64_t tg = d.syn_offset + region + rel[j];
             const bool cand = g2 && spike_candidate(kp, w[j], tg, now);
             const uint64_t bg = __ballot(g2), bcd = __ballot(cand);
+            if constexpr (kLazyOk) n_lazy += (uint32_t)__popcll(__ballot(g2 && lz[j]));
             if (g2) {
                 const uint64_t o = base + n_g2 + mbcnt64(bg);
                 if constexpr (kFused) {
-                    const float wn = updated_weight(kp, w[j], cand, Rw, rbw, (float)age32(now, ld[j]));
+                    const float wn = lz[j] ? 0.0f : updated_weight(kp, w[j], cand, Rw, rbw, (float)age32(now, ld[j]));
                     const uint4 ent = make_uint4(rel[j] | (cand ? 0x80000000u : 0u), __float_as_uint(w[j]),
-                                                 __float_as_uint(wn), dst[j]);
+                                                 __float_as_uint(wn), dst[j] | (lz[j] ? kDstLazy : 0u));
                     if (kTail && lds_out) {
                         // the fused tail keeps its survivors in LDS (fused_end's
                         // walk reads them there, and stores the weights)
@@ -630,7 +676,7 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
             n_cand += (uint32_t)__popcll(bcd);
         }
     }
-    return make_uint4(n_g1, n_g2, n_cand, 0u);
+    return make_uint4(n_g1, n_g2, n_cand, n_lazy);
 }
 
 // ---------------------------------------------------------------------------
@@ -752,7 +798,8 @@ constexpr uint32_t kLbMaxWords = 8;  // look-back words per lane: gate_blocks <=
 
 // One wave sweeps the words of workgroups [0, n): their values (capped sum)
 // once all carry `tag`, or as soon as the published ones reach the budget
-// (stop_at_budget).  vals: this lane's words (q = 64 i + lane), for the caller.
+// (stop_at_budget).  vals: this lane's words (q = 64 i + lane), for the caller:
+// the value in bits 0-29, the workgroup's kLbLazy kind bit in bit 31.
 // pub != 0: this workgroup's own word, published by lane 0 right after the
 // first sweep's loads are issued (a load issued after a store waits for it:
 // vmcnt counts both, in order).
@@ -783,8 +830,9 @@ __device__ uint32_t wg_poll(const DeviceState& d, uint32_t n, uint32_t tag, uint
             vals[i] = 0u;
             if (i * 64 < n && q < n) {
                 const bool mine = (uint32_t)(raw[i] >> 32) == tag;
-                vals[i] = mine ? (uint32_t)raw[i] & 0x3FFFFFFFu : 0u;
-                sum += vals[i];
+                // the value, and the lazy kind bit (kLbLazy) in bit 31
+                vals[i] = mine ? (uint32_t)raw[i] & 0xBFFFFFFFu : 0u;
+                sum += vals[i] & 0x3FFFFFFFu;
                 ok = ok && mine;
             }
         }
@@ -854,6 +902,22 @@ __device__ void fused_next_bounds(const DeviceState& d, uint32_t* cc)
     }
     const uint32_t gain = (uint64_t)cmax * NR > 4ull * total ? 4u : 0u;
     if (mine) d.range_bounds_next[k] = adapted_bound(d, cc, d.range_bounds_prev, NR, k, total, d.range_bounds[k], gain);
+}
+
+// A lazy survivor (kDstLazy: its refractory stage did not gather isi) that
+// reached the update: lastFired[dst] read now and the updated weight computed
+// (brain.metal:101-121, the entry's w and candidate bit).  Only in a workgroup
+// predicted past the budget cut that lies below it after all: the stamps of
+// the pass wait for its second look-back word (fused_end), so this read sees
+// the pass-start value (C1).
+__device__ __forceinline__ void resolve_lazy(const DeviceState& d, const KernelParams& kp, const ApplyCtx& c, uint4& x,
+                                             bool cand)
+{
+    if (x.w & kDstLazy) {
+        x.w &= ~kDstLazy;
+        const uint64_t ld = d.last_fired[x.w];
+        x.z = __float_as_uint(updated_weight(kp, __uint_as_float(x.y), cand, c.R, c.rb, (float)age32(c.now, ld)));
+    }
 }
 
 // The walk of one range's survivors (the fused pass's g2x entries, contiguous
@@ -930,12 +994,16 @@ __device__ __forceinline__ uint32_t range_walk(const DeviceState& d, const Kerne
             if (b0 + j * 64 >= S || (!spec && P >= budget)) break;  // wave-uniform
             const uint32_t q = b0 + j * 64 + lane;
             const bool v = q < S, cand = v && (e[j].x >> 31);
-            const uint4 x = make_uint4(e[j].x & 0x7FFFFFFFu, e[j].y, e[j].z, e[j].w);
+            uint4 x = make_uint4(e[j].x & 0x7FFFFFFFu, e[j].y, e[j].z, e[j].w);
             const uint64_t bc = __ballot(cand);
             const uint64_t pre = P + mbcnt64(bc);  // spike candidates before this event
             const bool below = v && pre < budget;
             if (!spec) {
-                if (below) apply_event(d, kp, ac, region, x, cand, pre, region + q);
+                if (below) {
+                    if constexpr (kLazyBuild) resolve_lazy(d, kp, ac, x, cand);
+                    apply_event(d, kp, ac, region, x, cand, pre, region + q);
+                }
+                if constexpr (kLazyBuild) x.w &= ~kDstLazy;
             } else if (below) {
                 ++ac.upd;
                 if (cand) record_spike(d, kp, ac, x, pre, region + q);
@@ -966,12 +1034,16 @@ __device__ __forceinline__ void lds_walk(const DeviceState& d, const KernelParam
     for (uint32_t q0 = 0; q0 < S && P < budget; q0 += 64) {  // wave-uniform
         const uint32_t q = q0 + lane;
         const bool v = q < S;
-        const uint4 x = v ? e[q] : make_uint4(0u, 0u, 0u, 0u);
-        const bool cand = v && (x.x >> 31);
+        const uint4 xe = v ? e[q] : make_uint4(0u, 0u, 0u, 0u);
+        uint4 x = make_uint4(xe.x & 0x7FFFFFFFu, xe.y, xe.z, xe.w);
+        const bool cand = v && (xe.x >> 31);
         const uint64_t bc = __ballot(cand);
         const uint64_t pre = P + mbcnt64(bc);
-        if (v && pre < budget) apply_event(d, kp, ac, region, make_uint4(x.x & 0x7FFFFFFFu, x.y, x.z, x.w), cand, pre, 0);
-        if (set_next) wave_set_next_dedup(d, cand && pre < budget, x.w, setc);  // this pass's spikes
+        if (v && pre < budget) {
+            if constexpr (kLazyBuild) resolve_lazy(d, kp, ac, x, cand);
+            apply_event(d, kp, ac, region, x, cand, pre, 0);
+        }
+        if (set_next) wave_set_next_dedup(d, cand && pre < budget, kLazyBuild ? x.w & ~kDstLazy : x.w, setc);
         P += (uint64_t)__popcll(bc);
     }
 }
@@ -1064,6 +1136,8 @@ struct FusedLds {
     uint32_t done;                     // waves through their refractory stage
     uint32_t total;                    // candidates of the pass (capped; workgroup 0)
     uint32_t sg2;                      // sharded pass: the workgroup's refractory survivors
+    uint32_t lazy;                     // some range of the workgroup holds lazy survivors (kDstLazy)
+    uint32_t waitlazy;                 // stamping: some lazy workgroup below the cut must publish its walk first
 };
 
 // Fused pass: range r's wave after its refractory stage (g1 pre-gated; Sg
@@ -1088,7 +1162,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
                                           const uint4* tl, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
                                           float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L,
                                           uint64_t t_stream, uint32_t h0, uint32_t chunk_t, uint32_t nch,
-                                          uint64_t* wcb)
+                                          uint64_t* wcb, uint32_t n_lazy)
 {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
     const uint32_t tag = epoch + 1u;
@@ -1100,6 +1174,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     const uint32_t S = Sg + St, C = Cg + Ct;  // the range's survivors and spike candidates
     uint32_t order = 0;
     if (lane == 0) {
+        if (kLazyBuild && n_lazy) L.lazy = 1u;
         L.cand[wid] = C < budget ? C : budget;
         if (shard) atomicAdd(&L.sg2, S);
         order = atomicAdd(&L.done, 1u);
@@ -1127,7 +1202,8 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     if (wid == 0) {
         uint32_t c = lane < (uint32_t)NW ? L.cand[lane] : 0u;
         c = wave_sum(c);
-        const uint64_t word = (uint64_t)tag << 32 | (uint64_t)kLbAggregate << 30 | (c < budget ? c : budget);
+        const uint32_t kind = kLbAggregate | (kLazyBuild && L.lazy ? kLbLazy : 0u);
+        const uint64_t word = (uint64_t)tag << 32 | (uint64_t)kind << 30 | (c < budget ? c : budget);
         uint32_t e;
         if (shard) {
             // the pass's refractory survivors for the exchange summary: added
@@ -1165,25 +1241,46 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     // done: no lastFired read is left, the stamps may land.  Wave 0 waits for
     // that before its walk (its loads then wait for no store of the walk).
     uint32_t tot = 0, t0 = 0;
+    uint32_t lazy_wait = 0;  // wave 0 of a stamping workgroup: bit i = word 64 i + lane is a lazy workgroup
+                             // below the cut (not this one): its walk reads lastFired, the stamps wait for it
     if (wid == 0 && stamping) {
         tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
-        if (first) {
-            // the next pass's prediction (refrac_chunk's spec): the workgroups
-            // below the one where the budget ran out, less one
-            uint32_t run = 0, cut = gridDim.x;
+        // the budget's cut (the next pass's predictions, refrac_chunk's spec
+        // and lazy) and the lazy workgroups below it
+        uint32_t run = 0, cut = gridDim.x;
+        bool any_lazy = false;
+        if constexpr (kLazyBuild) {
+#pragma unroll
+            for (uint32_t i = 0; i < kLbMaxWords; ++i) any_lazy = any_lazy || (vals[i] >> 31);
+            any_lazy = __ballot(any_lazy) != 0;
+        }
+        if (first || any_lazy) {
 #pragma unroll
             for (uint32_t i = 0; i < kLbMaxWords; ++i) {
-                const uint32_t inc = wave_incl_scan(vals[i]) + run;  // prefix through word 64 i + lane
-                const uint64_t hit = __ballot(inc >= budget && inc - vals[i] < budget);
+                const uint32_t v = vals[i] & 0x3FFFFFFFu;
+                const uint32_t inc = wave_incl_scan(v) + run;  // prefix through word 64 i + lane
+                const uint64_t hit = __ballot(inc >= budget && inc - v < budget);
                 if (hit && cut == gridDim.x) cut = i * 64 + (uint32_t)__builtin_ctzll(hit);
+                const uint32_t q = i * 64 + lane;
+                if (kLazyBuild && (vals[i] >> 31) && inc - v < budget && q < gridDim.x && q != blockIdx.x)
+                    lazy_wait |= 1u << i;
                 run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
             }
+        }
+        if constexpr (kLazyBuild) {
+            const bool any_wait = __ballot(lazy_wait != 0) != 0;
+            if (lane == 0) L.waitlazy = any_wait ? 1u : 0u;
+        }
+        if (first) {
             // the event-0 flag (refrac_chunk): stored and drained before its
             // workgroup's word was published
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             t0 = __hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("" ::"v"(t0));  // consumed here, before any store of the walk (see range_walk)
-            if (lane == 0) d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
+            if (lane == 0) {
+                d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
+                d.work->lazy_from = cut >= gridDim.x ? gridDim.x : min(gridDim.x, cut + 1u + d.lazy_margin);
+            }
         }
     }
     const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
@@ -1236,6 +1333,12 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     // LDS only (the statistics, the LDS spike list): the walks' stores stay in flight
     if (shard || (stamping && !spk_lds)) __syncthreads();
     else lds_barrier();
+    // a lazy workgroup: every wave's walk is done (a walk below the cut read
+    // lastFired for its lazy survivors, values consumed): the second word
+    // lets the stampers go on (they wait for it only below the cut)
+    if (kLazyBuild && !shard && L.lazy && threadIdx.x == 0)
+        __hip_atomic_store((gu64*)(d.lb_status + kMaxGateBlocks + blockIdx.x), (uint64_t)tag << 32 | 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) {
         typedef unsigned long long ull;
         abnn_stats* st = d.wg_stats + blockIdx.x % kWalkBlocks;
@@ -1272,6 +1375,25 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         return;
     }
     uint64_t* wc0 = wcb + (uint64_t)kWaveClock * r;  // diagnostics, wave 0: exit
+    if (kLazyBuild && stamping && L.waitlazy) {  // a mispredicted lazy workgroup below the cut: its walk's reads first
+        if (wid == 0) {
+            for (uint32_t spins = 0;; ++spins) {  // wave-uniform
+                bool ok = true;
+#pragma unroll
+                for (uint32_t i = 0; i < kLbMaxWords; ++i)
+                    if ((lazy_wait >> i) & 1u)
+                        ok = ok && (uint32_t)(__hip_atomic_load((gu64*)(d.lb_status + kMaxGateBlocks + i * 64 + lane),
+                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
+                if (__ballot(!ok) == 0) break;
+                if (spins >= kLbSpinLimit) {  // never hang the GPU: report and go on
+                    if (lane == 0) __hip_atomic_store(d.err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        lds_barrier();
+    }
     if (stamping) {
         if (spk_lds) {
             for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
@@ -1486,6 +1608,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         if (tid < 5) s_fz.stat[tid] = 0u;
         if (tid == 0) s_fz.done = 0u;
         if (tid == 0) s_fz.sg2 = 0u;
+        if (tid == 0) s_fz.lazy = 0u;
+        if (tid == 0) s_fz.waitlazy = 0u;
         if (tid < kSetCache) s_fz.setc[tid] = ~0ull;
         // the filter images in LDS for every wave, the first records still in
         // flight: this wave's LDS-DMAs are older than its kDepth iterations of
@@ -1550,6 +1674,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         tot.x += c.x;
         tot.y += c.y;
         tot.z += c.z;
+        tot.w += c.w;
         nch += pend >= kChunk;
         pend = 0;
         chunk_t += (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc);
@@ -1772,8 +1897,17 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         const bool lds_ok = kShard ? false : (kLean || (!d.shard_mode && !d.g2src));
         if (lds_ok && pend <= 256u) tail_lds = reinterpret_cast<uint4*>(s_stage[wid]);
     }
+    // fused single-GPU sweep: a workgroup predicted past the budget cut (the
+    // previous pass's cut + 1 + lazy_margin on) gathers lastFired[dst] only
+    // where the LDS filter says dst may be recent (refrac_chunk lazy).  Read
+    // here, not held through the stream (workgroup 0 writes it only once
+    // every look-back word, this one's included, is published)
+    bool lazy_wg = false;
+    if constexpr (kLazyBuild && kFused && !kRandom && !kShard)
+        lazy_wg = d.lazy_isi && !d.shard_mode && !spec && blockIdx.x >= sload(&d.work->lazy_from) &&
+                  sload(&d.work->lazy_from) != 0u;
     const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, true>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
-                                                               r, tot.z, s_f2, stage_at, tail_lds);
+                                                               r, tot.z, s_f2, stage_at, tail_lds, lazy_wg, s_fb);
     const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
     const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
     if constexpr (kFused) {
@@ -1783,7 +1917,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         const bool tl = tail_lds != nullptr;
         fused_end<BLOCK, NW, kLean, kShard>(d, kp, r, region, tot.x + c.x, tl ? tot.y : tot.y + c.y, tl ? tot.z : tot.z + c.z,
                              tl ? c.y : 0u, tl ? c.z : 0u, tail_lds, (uint32_t)gf, len == 0, spec, now, Rw, rbw, pass_f,
-                             epoch, s_fz, t_stream, hw0, chunk_t, nch, wcb);
+                             epoch, s_fz, t_stream, hw0, chunk_t, nch, wcb, tot.w + c.w);
         return;
     }
     if (lane == 0) {
@@ -2410,180 +2544,233 @@ __global__ __launch_bounds__(256) void k_visits_merge(uint64_t* lv, uint8_t* mar
     }
 }
 
-// The structural update's compaction of the span's blocks [b0, b0 + nblk), IN
-// PLACE, in one pass over the records (round 4: the span went to the spare
-// buffer and was copied back, two passes).  A live record only ever moves
-// down, and by less than the records before its block hold tombstones: block
-// c writes into blocks c_lo..c (c_lo from its offset), so it may write only
-// once each of those has READ its records (registers).  Block c publishes
-// rd[c] = epoch once its loads have landed, then polls the flags of
-// c_lo..c-1.  A persistent grid (one workgroup per CU, all resident) takes
-// blocks in increasing order, strided: the lowest unfinished block waits for
-// none, so no cycle; every poll is bounded (err, never a hang).
-__global__ __launch_bounds__(kCompactThreads) void k_compact_inplace(SynArrays syn, uint64_t n, const uint64_t* offsets,
-                                                                     const unsigned long long* sp, uint32_t* rd,
-                                                                     uint32_t epoch, uint32_t* err, uint32_t spin_limit)
+// ---------------------------------------------------------------------------
+// The structural update's removal (abnn.h, round 6): with D tombstones and
+// m = n - D, the k-th tombstone below m (index order) takes the k-th live
+// record of the tail [m, n) (index order) and the array ends at m.  Holes lie
+// below m and their fill above it, so no record is both read and written:
+// every hole block moves its records at once, no inter-workgroup waits.
+// Only the filled holes' records move (O(D)); the update reads the codes of
+// the blocks holding tombstones (in a sweep: the visited window) to find the
+// holes.  Round 4-5 closed the tombstones' span up in order (O(span) moves,
+// 1.65 GB at config 5, in rounds that waited on lower blocks: ~0.8 ms).
+// The update's words sp: [0] first block with a tombstone bf, [1] last such
+// block + 1 bl, [2] tombstones D, [3] tombstones of block m / C below m,
+// [4] records appended, [5] tombstones in the tail [m, n).
+constexpr uint32_t kSwapThreads = 256;
+constexpr uint32_t kSwapPer = kCompactChunk / kSwapThreads;  // records per thread (contiguous)
+static_assert(kSwapPer == 16, "a thread loads its codes as 2 x 16 B (lo) + 16 B (hi)");
+
+// the 24-bit code of the tombstone src (engine.h src_code(kSrcNone)), split
+__device__ __forceinline__ uint32_t tomb_code() { return src_code(kSrcNone); }
+
+// Records [base + 16 t, +16) of thread t: bit k of the result = record
+// base + 16 t + k is a tombstone (tomb) or live, within [lo, hi).
+__device__ __forceinline__ uint32_t swap_mask(const SynArrays& a, uint64_t base, uint64_t lo, uint64_t hi, bool tomb)
 {
-    // KB blocks per workgroup and round, all their loads in flight at once:
-    // round i takes blocks [i KB G, (i + 1) KB G), workgroup w the blocks
-    // (i KB + k) G + w.  Every workgroup flags its round's blocks before it
-    // waits, and a block waits only for lower ones (this round's or earlier),
-    // so the rounds cannot deadlock.
-    constexpr int KB = 2;
-    __shared__ uint64_t s_wave[kCompactThreads / 64];
-    __shared__ uint32_t s_bad;
-    const uint32_t lane = threadIdx.x & 63;
-    // the span's blocks (k_dead_bounds); the records from z on (after the
-    // last tombstone, in its block) stay where they are: the hole's fill
-    // takes the array's end (k_span_fill)
-    const uint64_t b0 = sp[0], D = sp[2], z = sp[3], lb = D ? (sp[1] - 1) * kCompactChunk : 0u;
-    // (a tally that disagrees with the records moves nothing: k_span_fill reports it)
-    const uint64_t nblk = D && z > lb && z <= n && z >= D ? sp[1] - sp[0] : 0u;
-    const uint64_t G = gridDim.x;
-    for (uint64_t r0 = 0; r0 < nblk; r0 += KB * G) {  // workgroup-uniform
-        uint32_t rs[KB][4];
-        uint64_t rdw[KB][4], o0[KB];
+    const uint64_t i0 = base + (uint64_t)kSwapPer * threadIdx.x;
+    if (i0 >= hi || i0 + kSwapPer <= lo) return 0u;
+    const u32x4* pl = reinterpret_cast<const u32x4*>(a.lo + i0);
+    const u32x4 l0 = __builtin_nontemporal_load(pl), l1 = __builtin_nontemporal_load(pl + 1);
+    const u32x4 h = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.hi + hi_pos(i0)));
+    const uint32_t lw[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w}, hw[4] = {h.x, h.y, h.z, h.w};
+    const uint32_t tc = tomb_code();
+    uint32_t m = 0;
 #pragma unroll
-        for (int k = 0; k < KB; ++k) {
-            const uint64_t c = r0 + k * G + blockIdx.x;
-            const uint64_t base = (b0 + c) * kCompactChunk;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint64_t i = base + (uint64_t)j * kCompactThreads + threadIdx.x;
-                const bool in = c < nblk && i < z;  // z <= n
-                rs[k][j] = in ? src_of(syn, i) : kSrcNone;
-                rdw[k][j] = in ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(syn.dw + i)) : 0ull;
-            }
-            o0[k] = c < nblk ? offsets[c] : 0u;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's records are in registers
-        __syncthreads();
-        if (threadIdx.x < KB) {
-            const uint64_t c = r0 + threadIdx.x * G + blockIdx.x;
-            if (c < nblk) __hip_atomic_store(rd + c, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (threadIdx.x == 0) s_bad = 0u;
-        // the blocks each one writes into, below it, must have read theirs
-        if (threadIdx.x < 64) {
-#pragma unroll
-            for (int k = 0; k < KB; ++k) {
-                const uint64_t c = r0 + k * G + blockIdx.x;
-                if (c >= nblk) break;
-                const uint64_t c_lo = o0[k] / kCompactChunk - b0;  // o0 >= b0 * kCompactChunk
-                for (uint64_t j0 = c_lo; j0 < c; j0 += 64) {       // wave-uniform
-                    const uint64_t jj = j0 + lane;
-                    for (uint32_t spins = 0;; ++spins) {
-                        const bool ok =
-                            jj >= c || __hip_atomic_load(rd + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-                        // (spin_limit 0: every wait gives up -- the debug knob
-                        // abnn_debug_set_compact_spin_limit tests the error path)
-                        if (__ballot(!ok) == 0 && spins < spin_limit) break;
-                        if (spins >= spin_limit) {
-                            if (lane == 0) {
-                                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                s_bad = 1u;
-                            }
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        if (s_bad) continue;  // (reported: the records are then not trusted)
-#pragma unroll
-        for (int k = 0; k < KB; ++k) {
-            if (r0 + k * G + blockIdx.x >= nblk) break;  // workgroup-uniform
-            uint64_t o = o0[k];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool live = rs[k][j] != kSrcNone;
-                uint64_t tot;
-                // (LDS-only barriers: the stores stay in flight)
-                const uint64_t pre = block_exclusive_scan<kCompactThreads, true>(live ? 1u : 0u, &tot, s_wave);
-                if (live) {
-                    set_src(syn, o + pre, rs[k][j]);
-                    __builtin_nontemporal_store(rdw[k][j], reinterpret_cast<uint64_t*>(syn.dw + o + pre));
-                }
-                o += tot;
-            }
-        }
+    for (uint32_t k = 0; k < kSwapPer; ++k) {
+        const uint32_t code = ((lw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu) | ((hw[k >> 2] >> (8 * (k & 3))) & 0xFFu) << 16;
+        const uint64_t i = i0 + k;
+        if (i >= lo && i < hi && (code == tc) == tomb) m |= 1u << k;
     }
+    return m;
 }
 
-// The structural update driven from the device (round 4: one host
-// synchronisation per update instead of six, no host copy of the grown
-// slots).  sp = the update's words: [0] first block with a tombstone, [1] last
-// such block + 1, [2] tombstones D, [3] z = 1 + the last tombstone, [4]
-// records appended; offsets[i] = where block bf + i's first live record goes.
+__device__ __forceinline__ void move_record(const SynArrays& a, uint64_t from, uint64_t to)
+{
+    set_src(a, to, src_of(a, from));
+    __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(a.dw + from)),
+                                reinterpret_cast<uint64_t*>(a.dw + to));
+}
+
 __global__ void k_span_init(unsigned long long* sp)
 {
+    if (threadIdx.x < 8) sp[threadIdx.x] = threadIdx.x == 0 ? ~0ull : 0ull;
+}
+
+// Block mb = m / C (the one m falls in): its tombstones below m (sp[3]), the
+// tally checked against it, and the tail's tombstones (sp[5]) from the tally
+// of the blocks above it.
+__global__ __launch_bounds__(kSwapThreads) void k_swap_mb(SynArrays a, uint64_t n, const uint32_t* dead, uint64_t nb,
+                                                          unsigned long long* sp, uint32_t* err)
+{
+    __shared__ uint64_t s_wave[kSwapThreads / 64];
+    const uint64_t D = sp[2];
+    if (D == 0) return;
+    if (D > n) {  // the tally disagrees with the records
+        if (threadIdx.x == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    const uint64_t m = n - D, mb = m / kCompactChunk, base = mb * kCompactChunk;
+    const uint64_t end = n < base + kCompactChunk ? n : base + kCompactChunk;
+    const uint64_t below = __popc(swap_mask(a, base, base, m, true));
+    const uint64_t above = __popc(swap_mask(a, base, m, end, true));
+    const uint64_t tm = block_sum<kSwapThreads>(below, s_wave), ta = block_sum<kSwapThreads>(above, s_wave);
+    uint64_t up = 0;  // tallied tombstones of the blocks above mb
+    for (uint64_t b = mb + 1 + threadIdx.x; b < nb; b += kSwapThreads) up += dead[b];
+    up = block_sum<kSwapThreads>(up, s_wave);
     if (threadIdx.x == 0) {
-        sp[0] = ~0ull;
-        sp[1] = sp[2] = sp[3] = sp[4] = 0ull;
+        sp[3] = tm;
+        sp[5] = ta + up;
+        if (tm + ta != (mb < nb ? dead[mb] : 0u)) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
-// offsets over the span's blocks [bf, bl): the records before the first
-// tombstone keep their places, every block's live records follow the lower
-// blocks' (one workgroup; the span lies in the sweep's window: ~E / 4096
-// blocks)
-__global__ __launch_bounds__(kScanThreads) void k_span_offsets(const uint32_t* dead, uint64_t n,
-                                                               const unsigned long long* sp, uint64_t* offsets)
+// The holes' ranks: off[b] = tallied tombstones of blocks [bf, b), for the
+// hole blocks [bf, min(bl, mb + 1)) -- a two-launch scan over slices of 1024
+// blocks (part[] = each slice's sum; the second launch adds the lower slices').
+__device__ __forceinline__ void swap_hole_range(const unsigned long long* sp, uint64_t n, uint64_t& b0, uint64_t& b1)
+{
+    const uint64_t D = sp[2];
+    b0 = b1 = 0;
+    if (D == 0 || D >= n) return;  // (D = n: no record stays, nothing to fill)
+    const uint64_t mb = (n - D) / kCompactChunk;
+    b0 = sp[0];
+    b1 = sp[1] < mb + 1 ? sp[1] : mb + 1;
+    if (b1 < b0) b1 = b0;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_swap_scan1(const uint32_t* dead, uint64_t n,
+                                                             const unsigned long long* sp, uint64_t* part)
 {
     __shared__ uint64_t s_wave[kScanThreads / 64];
-    if (sp[2] == 0) return;
-    const uint64_t bf = sp[0], bl = sp[1];
-    uint64_t run = bf * kCompactChunk;
-    for (uint64_t i0 = 0; i0 < bl - bf; i0 += kScanThreads) {  // workgroup-uniform
-        const uint64_t i = i0 + threadIdx.x, b = bf + i;
+    uint64_t b0, b1;
+    swap_hole_range(sp, n, b0, b1);
+    const uint64_t b = b0 + (uint64_t)blockIdx.x * kScanThreads + threadIdx.x;
+    if (b0 + (uint64_t)blockIdx.x * kScanThreads >= b1) return;  // workgroup-uniform
+    const uint64_t t = block_sum<kScanThreads>(b < b1 ? dead[b] : 0u, s_wave);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_swap_scan2(const uint32_t* dead, uint64_t n,
+                                                             const unsigned long long* sp, const uint64_t* part,
+                                                             uint64_t* off)
+{
+    __shared__ uint64_t s_wave[kScanThreads / 64];
+    uint64_t b0, b1;
+    swap_hole_range(sp, n, b0, b1);
+    if (b0 + (uint64_t)blockIdx.x * kScanThreads >= b1) return;  // workgroup-uniform
+    uint64_t lower = 0;
+    for (uint32_t s = threadIdx.x; s < blockIdx.x; s += kScanThreads) lower += part[s];
+    lower = block_sum<kScanThreads>(lower, s_wave);
+    const uint64_t b = b0 + (uint64_t)blockIdx.x * kScanThreads + threadIdx.x;
+    uint64_t tot;
+    const uint64_t pre = block_exclusive_scan<kScanThreads>(b < b1 ? dead[b] : 0u, &tot, s_wave);
+    if (b < b1) off[b] = lower + pre;
+}
+
+// Tail blocks' live prefix (only when the tail holds tombstones: else the k-th
+// live tail record is m + k): toff[b - mb] = live records of [m, b C) for the
+// tail blocks b of [mb, ceil(n / C)) and one past them.  One workgroup.
+__global__ __launch_bounds__(kScanThreads) void k_swap_tail(const uint32_t* dead, uint64_t n,
+                                                            const unsigned long long* sp, uint64_t* toff)
+{
+    __shared__ uint64_t s_wave[kScanThreads / 64];
+    const uint64_t D = sp[2];
+    if (D == 0 || D >= n || sp[5] == 0) return;
+    const uint64_t m = n - D, mb = m / kCompactChunk, nbn = (n + kCompactChunk - 1) / kCompactChunk;
+    uint64_t run = 0;
+    for (uint64_t j0 = 0; j0 <= nbn - mb; j0 += kScanThreads) {  // workgroup-uniform
+        const uint64_t j = j0 + threadIdx.x, b = mb + j;
         uint64_t live = 0;
-        if (i < bl - bf) {
-            const uint64_t len = n - b * kCompactChunk < kCompactChunk ? n - b * kCompactChunk : kCompactChunk;
-            live = len - dead[b];
+        if (b < nbn) {
+            const uint64_t lo = b == mb ? m : b * kCompactChunk;
+            const uint64_t hi = n < (b + 1) * kCompactChunk ? n : (b + 1) * kCompactChunk;
+            const uint64_t tombs = b == mb ? dead[b] - sp[3] : dead[b];
+            live = (hi - lo) - tombs;
         }
         uint64_t tot;
         const uint64_t pre = block_exclusive_scan<kScanThreads>(live, &tot, s_wave);
-        if (i < bl - bf) offsets[i] = run + pre;
+        if (j <= nbn - mb) toff[j] = run + pre;
         run += tot;
     }
 }
 
-// z over the last block with a tombstone
-__global__ __launch_bounds__(256) void k_span_last(SynArrays a, uint64_t n, unsigned long long* sp)
+// The fill: hole blocks [bf, min(bl, mb + 1)) over a persistent grid, one
+// workgroup per block at a time.  A block's holes get the consecutive ranks
+// off[b] + (their order in the block); its tombstones must match the tally
+// (err = 2: the tally and the records disagree).
+__global__ __launch_bounds__(kSwapThreads) void k_swap_fill(SynArrays a, uint64_t n, const uint32_t* dead,
+                                                            const unsigned long long* sp, const uint64_t* off,
+                                                            const uint64_t* toff, uint32_t* err)
 {
-    if (sp[2] == 0) return;
-    const uint64_t lb = (sp[1] - 1) * kCompactChunk, count = n - lb < kCompactChunk ? n - lb : kCompactChunk;
-    unsigned long long m = 0;
-    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < count; k += (uint64_t)gridDim.x * 256)
-        if (src_of(a, lb + k) == kSrcNone) m = lb + k + 1;
-    if (m) atomicMax(sp + 3, m);
+    __shared__ uint64_t s_wave[kSwapThreads / 64];
+    __shared__ uint16_t s_hole[kCompactChunk];  // the block's holes by rank (slow path)
+    uint64_t b0, b1;
+    swap_hole_range(sp, n, b0, b1);
+    const uint64_t D = sp[2], m = n - D, mb = m / kCompactChunk, tail_tombs = sp[5];
+    for (uint64_t b = b0 + blockIdx.x; b < b1; b += gridDim.x) {  // workgroup-uniform
+        const uint32_t tally = dead[b];
+        if (tally == 0) continue;
+        const uint64_t base = b * kCompactChunk, hi = m < base + kCompactChunk ? m : base + kCompactChunk;
+        const uint32_t hm = swap_mask(a, base, base, hi, true);
+        uint64_t h;
+        const uint64_t pre = block_exclusive_scan<kSwapThreads, true>((uint64_t)__popc(hm), &h, s_wave);
+        // block mb: its tombstones below m (checked against the tally by k_swap_mb)
+        if (h != (b == mb ? sp[3] : tally)) {
+            if (threadIdx.x == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            continue;
+        }
+        const uint64_t k0 = off[b];
+        const uint64_t i0 = base + (uint64_t)kSwapPer * threadIdx.x;
+        if (tail_tombs == 0) {  // the tail is all live: the k-th live tail record is m + k
+            uint32_t x = hm;
+            for (uint64_t r = k0 + pre; x; x &= x - 1u, ++r) move_record(a, m + r, i0 + (uint32_t)__builtin_ctz(x));
+            continue;
+        }
+        // the tail holds tombstones: the holes' offsets in LDS by rank, then
+        // the tail blocks covering ranks [k0, k0 + h), each scanned for its
+        // live records' ranks
+        {
+            uint32_t x = hm;
+            for (uint64_t q = pre; x; x &= x - 1u, ++q)
+                s_hole[q] = (uint16_t)(kSwapPer * threadIdx.x + (uint32_t)__builtin_ctz(x));
+        }
+        __syncthreads();
+        const uint64_t nt = (n + kCompactChunk - 1) / kCompactChunk - mb;  // tail blocks
+        uint64_t lo_j = 0, hi_j = nt;  // the last j with toff[j] <= k0
+        while (hi_j - lo_j > 1) {
+            const uint64_t mid = (lo_j + hi_j) >> 1;
+            if (toff[mid] <= k0) lo_j = mid;
+            else hi_j = mid;
+        }
+        for (uint64_t j = lo_j; j < nt && toff[j] < k0 + h; ++j) {  // workgroup-uniform
+            const uint64_t tb = (mb + j) * kCompactChunk;
+            const uint64_t tlo = j == 0 ? m : tb, thi = n < tb + kCompactChunk ? n : tb + kCompactChunk;
+            const uint32_t lm = swap_mask(a, tb, tlo, thi, false);
+            uint64_t lt;
+            const uint64_t lp = block_exclusive_scan<kSwapThreads, true>((uint64_t)__popc(lm), &lt, s_wave);
+            if (lt != toff[j + 1] - toff[j]) {
+                if (threadIdx.x == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            const uint64_t t0 = tb + (uint64_t)kSwapPer * threadIdx.x;
+            uint32_t x = lm;
+            for (uint64_t r = toff[j] + lp; x; x &= x - 1u, ++r)
+                if (r >= k0 && r < k0 + h) move_record(a, t0 + (uint32_t)__builtin_ctz(x), base + s_hole[r - k0]);
+        }
+        __syncthreads();  // s_hole is reused by the next block
+    }
 }
 
-// After the compaction: the hole [z - D, z) takes the last D records, or the
-// tail [z, n) shifts down when it is shorter (abnn.h); the tally of the
-// span's blocks is cleared.  A tally that disagrees with the records (z not
-// in the last block, or fewer records than tombstones) is reported (err = 2)
-// and nothing moves.
-__global__ __launch_bounds__(256) void k_span_fill(SynArrays a, uint64_t n, const unsigned long long* sp, uint32_t* dead,
-                                                   uint32_t* err)
+// After the fill: no tombstone is left below m, and the blocks from m on hold
+// the appended (live) records next: their tally is cleared.
+__global__ __launch_bounds__(256) void k_dead_clear(uint32_t* dead, uint64_t n, const unsigned long long* sp)
 {
     const uint64_t D = sp[2];
     if (D == 0) return;
-    const uint64_t bf = sp[0], bl = sp[1], z = sp[3], lb = (bl - 1) * kCompactChunk;
-    if (z <= lb || z > n || z < D) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
-    }
-    const uint64_t f0 = n - z >= D ? n - D : z, count = n - z >= D ? D : n - z, t0 = z - D;
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < count; k += stride) {
-        set_src(a, t0 + k, src_of(a, f0 + k));
-        __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(a.dw + f0 + k)),
-                                    reinterpret_cast<uint64_t*>(a.dw + t0 + k));
-    }
-    for (uint64_t b = bf + (uint64_t)blockIdx.x * 256 + threadIdx.x; b < bl; b += stride) dead[b] = 0u;
+    const uint64_t mb = (D <= n ? n - D : 0) / kCompactChunk, bf = sp[0] < mb ? sp[0] : mb;
+    const uint64_t nbn = (n + kCompactChunk - 1) / kCompactChunk;
+    for (uint64_t b = bf + (uint64_t)blockIdx.x * 256 + threadIdx.x; b < nbn; b += (uint64_t)gridDim.x * 256) dead[b] = 0u;
 }
 
 // The grown records (slots in (pass, slot) order, w = 1: used) appended after
@@ -2972,19 +3159,23 @@ hipError_t launch_unpack_src(const SynArrays& a, uint32_t* out_dev, uint64_t fir
 // see k_span_init): span bounds, offsets, z, the in-place compaction (one
 // workgroup per CU), the hole, the grown records.
 hipError_t launch_structural_update(const SynArrays& syn, uint64_t n, uint64_t cap, uint32_t* dead, uint64_t nb,
-                                    uint64_t* offsets, unsigned long long* sp, uint32_t* flags, uint32_t epoch,
-                                    uint32_t* err, uint32_t spin_limit, uint32_t cus, uint4* grown, uint64_t slots,
-                                    uint32_t* grown_cnt, unsigned long long* stats_grown, hipStream_t s)
+                                    uint64_t* offsets, uint64_t* part, uint64_t* toff, unsigned long long* sp,
+                                    uint32_t* err, uint32_t cus, uint4* grown, uint64_t slots, uint32_t* grown_cnt,
+                                    unsigned long long* stats_grown, hipStream_t s)
 {
     hipLaunchKernelGGL(k_span_init, dim3(1), dim3(64), 0, s, sp);
     if (dead && nb && n) {
         hipLaunchKernelGGL(k_dead_bounds, dim3((uint32_t)std::min<uint64_t>((nb + 255) / 256, 1024)), dim3(256), 0, s,
                            dead, nb, sp);
-        hipLaunchKernelGGL(k_span_offsets, dim3(1), dim3(kScanThreads), 0, s, dead, n, sp, offsets);
-        hipLaunchKernelGGL(k_span_last, dim3(16), dim3(256), 0, s, syn, n, sp);
-        hipLaunchKernelGGL(k_compact_inplace, dim3(cus), dim3(kCompactThreads), 0, s, syn, n, offsets, sp, flags, epoch,
-                           err, spin_limit);
-        hipLaunchKernelGGL(k_span_fill, dim3(1024), dim3(256), 0, s, syn, n, sp, dead, err);
+        hipLaunchKernelGGL(k_swap_mb, dim3(1), dim3(kSwapThreads), 0, s, syn, n, dead, nb, sp, err);
+        const uint32_t slices = (uint32_t)((nb + kScanThreads - 1) / kScanThreads);  // covers any hole range
+        hipLaunchKernelGGL(k_swap_scan1, dim3(slices), dim3(kScanThreads), 0, s, dead, n, sp, part);
+        hipLaunchKernelGGL(k_swap_scan2, dim3(slices), dim3(kScanThreads), 0, s, dead, n, sp, part, offsets);
+        hipLaunchKernelGGL(k_swap_tail, dim3(1), dim3(kScanThreads), 0, s, dead, n, sp, toff);
+        hipLaunchKernelGGL(k_swap_fill, dim3(std::max(1u, cus) * 8u), dim3(kSwapThreads), 0, s, syn, n, dead, sp, offsets,
+                           toff, err);
+        hipLaunchKernelGGL(k_dead_clear, dim3((uint32_t)std::min<uint64_t>((nb + 255) / 256, 1024)), dim3(256), 0, s,
+                           dead, n, sp);
     }
     if (grown && slots) {
         const uint32_t gb = (uint32_t)((slots + kScanThreads - 1) / kScanThreads);
@@ -3000,6 +3191,23 @@ hipError_t launch_visits_delta(const uint64_t* lv, const uint8_t* mark, uint64_t
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_visits_delta, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, lv,
                        mark, delta, n);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_reduce_u64(uint64_t* acc, const uint64_t* x, uint64_t n, uint32_t max)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const uint64_t a = acc[i], b = x[i];
+        acc[i] = max ? (a > b ? a : b) : a + b;
+    }
+}
+
+hipError_t launch_reduce_u64(uint64_t* acc, const uint64_t* x, uint64_t n, bool max, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_reduce_u64, dim3(blocks), dim3(256), 0, s, acc, x, n, max ? 1u : 0u);
     return hipGetLastError();
 }
 

@@ -57,6 +57,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <utility>
+#include <atomic>
 #include <vector>
 
 #include "engine.h"
@@ -105,7 +106,7 @@ constexpr uint32_t kRawRedo = 0xFFFFFFFDu;  // ginfo: not all stored (the pool r
 constexpr uint32_t kRawInit = 0x52415731u;  // RawHdr::init of a workspace whose err word is live
 
 // Workspace (16-B aligned pieces):
-//   hdr | filter (FB uint2) | gcand[NG] | gpre[NG] | btot[NG / 4096] | ginfo[NG] {S, seq, chunks} |
+//   hdr | filter (FB uint2) | lb | bounds | cost | clk (E-independent: raw_state_bytes) | gcand[NG] | gpre[NG] | btot[NG / 4096] | ginfo[NG] {S, seq, chunks} |
 //   wlim[W] | wstat[W] | ctab[W][maxc] | spikes[L] | pool[cap][kRawChunk] uint4
 struct RawHdr {
     uint32_t now, budget0, t0, ncand;  // pass-start clock and budget; event 0 survived; spikes (capped)
@@ -153,16 +154,27 @@ __host__ __device__ inline uint32_t raw_maxc(uint64_t ng)
     const uint64_t per_wave = (ng + kRawWaves - 1) / kRawWaves;  // groups of one wave
     return (uint32_t)(per_wave * (kRawGroup / kRawChunk) + 1);
 }
-inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
+inline constexpr uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
+
+// The part of the workspace whose offsets do not depend on E: the header, the
+// filter and the fused pass's state kept across passes (look-back words,
+// bounds, costs, wave clocks).  A workspace reused with another n_syn or
+// events keeps its look-back words where they were, so an epoch tag is never
+// compared against a spike list or a bound of a differently sized pass
+// (ADVICE r5).
+inline constexpr uint64_t raw_state_bytes()
+{
+    return 128 + kRawFB * 8 + 8ull * kRawGateWGs + al16(4ull * 3 * (kRfNR + 1)) + 4ull * 2 * kRfNR +
+           8ull * kRfClk * kRawWaves;
+}
 
 inline uint64_t raw_fixed_bytes(uint64_t E)
 {
     const uint64_t ng = raw_groups(E);
     const uint64_t L = std::min<uint64_t>(E, kRawSpikeCap);
-    return 128 + kRawFB * 8 + al16(4 * ng) * 2 + al16(4 * ((ng + kRawScanBlock - 1) / kRawScanBlock)) + al16(16 * ng) +
-           al16(4ull * kRawWaves) + al16(8ull * kRawWaves) +
-           al16(4ull * kRawWaves * raw_maxc(ng)) + al16(4 * L) +
-           8ull * kRawGateWGs + al16(4ull * 3 * (kRfNR + 1)) + 4ull * 2 * kRfNR + 8ull * kRfClk * kRawWaves;
+    return raw_state_bytes() + al16(4 * ng) * 2 + al16(4 * ((ng + kRawScanBlock - 1) / kRawScanBlock)) +
+           al16(16 * ng) + al16(4ull * kRawWaves) + al16(8ull * kRawWaves) + al16(4ull * kRawWaves * raw_maxc(ng)) +
+           al16(4 * L);
 }
 
 // Recommended pool: a partial chunk per wave plus 1/64 of the events (config
@@ -189,6 +201,14 @@ inline RawWs raw_ws(void* base, uint64_t E, uint64_t bytes)
     p += 128;
     w.filter = reinterpret_cast<uint2*>(p);
     p += kRawFB * 8;
+    w.lb = reinterpret_cast<unsigned long long*>(p);
+    p += 8ull * kRawGateWGs;
+    w.bounds = reinterpret_cast<uint32_t*>(p);
+    p += al16(4ull * 3 * (kRfNR + 1));
+    w.cost = reinterpret_cast<uint32_t*>(p);
+    p += 4ull * 2 * kRfNR;
+    w.clk = reinterpret_cast<uint64_t*>(p);
+    p += 8ull * kRfClk * kRawWaves;
     w.gcand = reinterpret_cast<uint32_t*>(p);
     p += al16(4 * ng);
     w.gpre = reinterpret_cast<uint32_t*>(p);
@@ -205,14 +225,6 @@ inline RawWs raw_ws(void* base, uint64_t E, uint64_t bytes)
     p += al16(4ull * kRawWaves * w.maxc);
     w.spikes = reinterpret_cast<uint32_t*>(p);
     p += al16(4ull * w.spike_cap);
-    w.lb = reinterpret_cast<unsigned long long*>(p);
-    p += 8ull * kRawGateWGs;
-    w.bounds = reinterpret_cast<uint32_t*>(p);
-    p += al16(4ull * 3 * (kRfNR + 1));
-    w.cost = reinterpret_cast<uint32_t*>(p);
-    p += 4ull * 2 * kRfNR;
-    w.clk = reinterpret_cast<uint64_t*>(p);
-    p += 8ull * kRfClk * kRawWaves;
     w.pool = reinterpret_cast<uint4*>(p);
     const uint64_t fixed = (uint64_t)(p - static_cast<char*>(base));
     w.pool_chunks = (uint32_t)std::min<uint64_t>((bytes - fixed) / (kRawChunk * 16), 0xFFFFFFFEu);
@@ -429,7 +441,7 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_gate(const uint4* __restrict_
                     id = wave_uniform(id);
                     if (id >= ws.pool_chunks) {  // the pool is spent: the rest of the sequence is not stored
                         lim = have * kRawChunk;
-                        if (lane == 0) ws.hdr->ovf = 1u;  // k_raw_apply will recompute: stamps deferred
+                        if (lane == 0) __hip_atomic_store(&ws.hdr->ovf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // k_raw_apply will recompute: stamps deferred
                         break;
                     }
                     if (lane == 0) ws.ctab[(uint64_t)v * ws.maxc + have] = id;
@@ -903,7 +915,8 @@ __device__ uint32_t rf_poll(const RawWs& ws, uint32_t n, uint32_t tag, uint32_t 
         for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
         if (__ballot(!ok) == 0 || (stop_at_budget && tot >= budget)) return (uint32_t)(tot < budget ? tot : budget);
         if (spins >= kRfSpinLimit) {  // never hang the GPU: report (abnn_traversal_workspace_error) and go on
-            if (lane == 0) ws.hdr->err = 2u;  // (every workgroup is resident: never expected)
+            if (lane == 0)  // (every workgroup is resident: never expected)
+                __hip_atomic_store(&ws.hdr->err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return budget;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -1163,7 +1176,7 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn,
             cur_id = ids[c1 - c0] != kRawNone ? ids[c1 - c0] : cur_id;
             if (stored < n) {
                 lim = S + stored;
-                if (lane == 0) ws.hdr->ovf = 1u;  // the walk recomputes the rest: the stamps wait for every walk
+                if (lane == 0) __hip_atomic_store(&ws.hdr->ovf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the walk recomputes the rest: the stamps wait for every walk
             }
         }
         S += n;
@@ -1250,6 +1263,11 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn,
     }
     __syncthreads();  // every wave of the workgroup through its tail: the tallies complete
     if (wid == 0) {
+        // the workgroup's flag stores (hdr->ovf, hdr->err) released at agent
+        // scope before its look-back word publishes them (the stampers acquire
+        // after their poll); the barrier above drained every wave's stores, so
+        // this waits for nothing in practice
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         // the groups' candidates -> their exclusive prefix in the workgroup
         // (each lane a run of consecutive groups)
         const uint32_t per = (ngrp + 63) / 64, g0 = lane * per;
@@ -1287,7 +1305,7 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn,
         else {  // beyond the list (a budget above 65536 and more spikes than that): stamped now,
                 // which may race with another workgroup's refractory reads -- reported
             lastF[dst] = now;
-            ws.hdr->err = 1u;
+            __hip_atomic_store(&ws.hdr->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
     // budget position of the survivor of group gl with K wave candidates
@@ -1416,10 +1434,16 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn,
         const uint32_t tot = rf_poll(ws, gridDim.x, tag, b0, false, 0ull);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (__hip_atomic_load(&ws.hdr->ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            for (uint32_t spins = 0; spins < kRfSpinLimit; ++spins) {
-                if (__hip_atomic_load(&ws.hdr->wdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gridDim.x) break;
-                __builtin_amdgcn_s_sleep(1);
+            bool all_walked = false;
+            for (uint32_t spins = 0; spins < kRfSpinLimit && !all_walked; ++spins) {
+                all_walked = __hip_atomic_load(&ws.hdr->wdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gridDim.x;
+                if (!all_walked) __builtin_amdgcn_s_sleep(1);
             }
+            // gave up (never expected: every workgroup is resident): the stamps
+            // may race with a recompute's lastF reads -- reported, as a look-back
+            // timeout is (abnn_traversal_workspace_error = 2)
+            if (!all_walked && lane == 0)
+                __hip_atomic_store(&ws.hdr->err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         if (lane == 0) L.tot = tot;
@@ -1475,15 +1499,21 @@ int g_raw_fused = -1;  // abnn_debug_raw_fused: -1 the environment, 0 off, 1 on
 bool raw_fused_ok()
 {
     if (g_raw_fused == 0) return false;
-    static const bool fits = [] {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return false;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_raw_pass, kRawBlock, 0) != hipSuccess) return false;
-        return (uint64_t)cus * (uint64_t)per >= kRawGateWGs;
-    }();
-    if (!fits) return false;
+    // per device (a process may drive several): 0 unknown, 1 fits, 2 does not
+    constexpr int kMaxDev = 64;
+    static std::atomic<int8_t> fits_by_dev[kMaxDev];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return false;
+    int8_t f = dev < kMaxDev ? fits_by_dev[dev].load(std::memory_order_relaxed) : 0;
+    if (f == 0) {
+        int cus = 0, per = 0;
+        const bool ok = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_raw_pass, kRawBlock, 0) == hipSuccess &&
+                        (uint64_t)cus * (uint64_t)per >= kRawGateWGs;
+        f = ok ? 1 : 2;
+        if (dev < kMaxDev) fits_by_dev[dev].store(f, std::memory_order_relaxed);
+    }
+    if (f != 1) return false;
     if (g_raw_fused == 1) return true;
     static const bool env_on = [] {
         const char* env = std::getenv("ABNN_RAW_FUSED");

@@ -200,13 +200,79 @@ class NativeComm:
             pass
 
 
+class LocalGroup:
+    """In-process communicator group (abnn_comm_group, include/abnn/abnn.h):
+    ``world`` ranks in ONE process, one host thread per rank, each driving its
+    shard handle through the C-ABI (abnn_shard_traverse) with the communicator
+    :meth:`comm` returns.  The collectives are device copies and a reduction
+    kernel between host barriers -- no RCCL: the sharded pass at world > 1 on
+    one GPU (SURVEY §4 item 4's fake communicator behind the same interface).
+    Ranks on one device must use one stream (torch's default stream in every
+    thread does)."""
+
+    def __init__(self, world: int):
+        import ctypes as C
+
+        from . import _lib
+
+        self.world = int(world)
+        h = C.c_void_p()
+        _lib.call("abnn_comm_group_create", self.world, C.byref(h))
+        self.handle = h
+        self._comms: list = []
+
+    def comm(self, rank: int, device: int = 0) -> "LocalComm":
+        c = LocalComm(self, rank, device)
+        self._comms.append(c)
+        return c
+
+    def close(self) -> None:
+        from . import _lib
+
+        for c in self._comms:
+            c.close()
+        self._comms = []
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            _lib.call("abnn_comm_group_destroy", self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class LocalComm:
+    """Rank ``rank`` of a :class:`LocalGroup`: the ``world`` / ``rank`` of the
+    shard layout and the abnn_comm handle ShardedBrain drives (native)."""
+
+    def __init__(self, group: LocalGroup, rank: int, device: int):
+        import ctypes as C
+
+        from . import _lib
+
+        self.world, self.rank = group.world, int(rank)
+        h = C.c_void_p()
+        _lib.call("abnn_comm_create_local", group.handle, self.rank, int(device), C.byref(h))
+        self.handle = h
+
+    def close(self) -> None:
+        from . import _lib
+
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            _lib.call("abnn_comm_destroy", self.handle)
+        self.handle = None
+
+
 class ShardedBrain:
     """The rank-local shard of a graph of ``n_syn_global`` synapses on GPU ``device``.
 
     native=True (one GPU per rank, RCCL): passes are driven by the C-ABI over
     the library's RCCL communicator (NativeComm, abnn_shard_traverse); False:
     phase by phase from Python around ``comm.all_gather`` (any backend; the
-    gloo rehearsal of ranks that share a GPU)."""
+    gloo rehearsal of ranks that share a GPU).  ``comm`` a :class:`LocalComm`:
+    the C-driven passes over the in-process group (one thread per rank)."""
 
     def __init__(self, comm, n_input: int, n_output: int, n_hidden: int, n_syn_global: int,
                  events_per_pass: int, *, device: int = 0, capacity_factor: float = 1.0,
@@ -233,7 +299,9 @@ class ShardedBrain:
         self.compact_every = int(self.brain.params.compact_every)
         self._updates = self.brain.structural_updates()
         self.native = None
-        if native:
+        if isinstance(comm, LocalComm):
+            self.native = comm  # C-driven passes over the in-process group
+        elif native:
             # the RCCL communicator spans the same process group as `comm`:
             # rank_offset and the gathered records' order follow its ranks
             self.native = NativeComm(device, group=getattr(comm, "group", None))

@@ -186,7 +186,15 @@ def cpu_baseline(wl, events: int, mode: int, threads: int, timed_passes: int, ex
         sweep[n] = timed_passes * E / (time.perf_counter() - t0)
     best = max(sweep, key=sweep.get)
     hc = host_cpus()
-    return {"value": sweep[best], "unit": "events/s", "cores": hc["available"], "threads": best,
+    # cores: the CPU time the run could get -- the cgroup quota when one caps
+    # the affinity set (16 of 256 on the GPU box), else the affinity set;
+    # threads: the pool that ran the best pass (more threads than the quota
+    # still overlap memory stalls); the machine's count beside them
+    quota = hc["cgroup_quota_cpus"]
+    eff = min(hc["available"], int(-(-quota // 1))) if quota else hc["available"]
+    return {"value": sweep[best], "unit": "events/s", "cores": eff, "cores_source":
+            "cgroup CPU quota" if quota and eff < hc["available"] else "affinity set",
+            "cores_visible": hc["available"], "threads": best,
             "thread_sweep": {str(k): round(v) for k, v in sweep.items()},
             "host_cpus": hc["machine"], "cgroup_quota_cpus": hc["cgroup_quota_cpus"], "kind": "port",
             "n_syn": n_syn, "graph": ("reduced: %d of %d synapses, picks hit a smaller working set than "
@@ -550,7 +558,8 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (build_random_graph recipe, portable RNG, generated on GPU)",
             "config": {
-                "workload": f"{wl.name}: {wl.note}", "n_neuron": wl.n_neuron, "n_syn": wl.n_syn,
+                "workload": f"{wl.name}: {wl.note}; " + (f"sharded {world} ways, one GPU per shard" if world > 1
+                                                         else "one GPU holds the whole graph"), "n_neuron": wl.n_neuron, "n_syn": wl.n_syn,
                 "events_per_pass_per_gpu": events, "visited_events_per_pass_per_gpu": local_events,
                 "mode": args.mode,
                 "plasticity": (dict(PLASTICITY, syn_capacity_factor=1.01, reward=0.25,

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define ABNN_ABI_VERSION 9
+#define ABNN_ABI_VERSION 10
 
 typedef enum abnn_status {
     ABNN_OK = 0,
@@ -140,14 +140,13 @@ typedef struct abnn_params {
  *     record {src of the firing synapse, n_input + ((x & 0xFFFFFFFF) *
  *     (N_NRN - n_input) >> 32), w_init, 0};
  *   structural update, after every pass whose ticked pass_index is a multiple
- *     of compact_every: the tombstones are removed -- their span [a, z)
- *     (first tombstone to last, D of them) closes up in order, and the D-
- *     record hole left at its end, [z - D, z), takes the array's last D
- *     records in order if the tail [z, n_syn) holds at least D records, else
- *     the tail shifts down by D (O(z - a + D) records move; a sweep prunes
- *     only inside its visited window, so the update costs O(events), not
- *     O(n_syn)); then the synapses grown since the previous update are
- *     appended in (pass, slot) order while n_syn < syn_capacity.  n_syn and
+ *     of compact_every: the D tombstones are removed -- the array ends at
+ *     m = n_syn - D, and the tombstones below m, in index order, take the
+ *     live records of the tail [m, n_syn), in index order (only the filled
+ *     holes' records move: O(D); ABI 10 -- until ABI 9 the tombstones' span
+ *     closed up in order, O(span)); then the synapses grown since the
+ *     previous update are appended in (pass, slot) order while n_syn <
+ *     syn_capacity.  n_syn and
  *     the visited events change here; the records are compacted in place (no
  *     second buffer), so the borrowed synapse pointer (abnn_state_ptrs) stays
  *     valid.  Sweep-mode event ids stay syn_offset + local index (syn_offset
@@ -282,6 +281,10 @@ abnn_status abnn_get_last_fired(abnn_brain* b, uint64_t first, uint64_t* out, ui
 abnn_status abnn_set_last_fired(abnn_brain* b, uint64_t first, const uint64_t* src, uint64_t n);
 abnn_status abnn_get_last_visited(abnn_brain* b, uint64_t first, uint64_t* out, uint64_t n);
 abnn_status abnn_set_last_visited(abnn_brain* b, uint64_t first, const uint64_t* src, uint64_t n);
+/* (A shard's abnn_set_last_visited clears the visit marks of what it writes,
+ * and a write of [0, N_NRN) leaves none unmerged.  Writes through the
+ * abnn_state_ptrs pointers bypass the marks and the host's bookkeeping: use
+ * the setters on sharded brains.) */
 /* lastFired[idx[i]] = value for i < n (teacher / input spikes written by the
  * host, brain.cpp:82, brain-engine.cpp:131). */
 abnn_status abnn_set_timestamps(abnn_brain* b, const uint32_t* idx, uint64_t n, uint64_t value);
@@ -404,6 +407,12 @@ uint64_t abnn_structural_updates(const abnn_brain* b);
  * answered from an LDS filter of lastF, which is gathered only for the ~1 %
  * of events the filter passes (the handle API's layout moves
  * 3 B per event).
+ * The single-launch pass after the filter keeps one workgroup per CU resident
+ * for the whole pass (its look-back waits on every other workgroup): run it
+ * with the device to itself -- not beside another stream's persistent kernels
+ * (a second handle's pass, RCCL) -- or select the five-launch pass
+ * (ABNN_RAW_FUSED=0), and check abnn_traversal_workspace_error now and then:
+ * a starved pass is not hung but reported there (2).
  * renormalise_clock_and_times (brain.metal:135-145) on the same buffers:
  * lastF[i] -= *clock for i < n_nrn, then *clock = 0 (the host decides when,
  * brain.cpp:127-128).                                                         */
@@ -465,6 +474,23 @@ abnn_status abnn_comm_create(const void* id, uint32_t world, uint32_t rank, int 
 abnn_status abnn_comm_destroy(abnn_comm* c);
 abnn_status abnn_shard_traverse(abnn_brain* b, abnn_comm* c, uint32_t passes, void* stream);
 abnn_status abnn_comm_sync_visits(abnn_brain* b, abnn_comm* c, void* stream);
+
+/* In-process communicator group: `world` ranks in ONE process, one host
+ * thread per rank, each calling abnn_shard_traverse / abnn_comm_sync_visits
+ * on its own shard handle with the communicator of abnn_comm_create_local
+ * (the same calls, in the same order, on every rank -- as with RCCL).  The
+ * collectives are device copies and a reduction kernel on each rank's stream
+ * between host barriers (no RCCL): the sharded pass at world > 1 on ONE GPU
+ * (k handles share the device), or over several GPUs of one process.  Ranks
+ * on one device must pass the same stream (a pass keeps one workgroup per CU
+ * resident: two must not run at once); a rank that fails, or one that does
+ * not reach a collective within 300 s, breaks the group and every rank's
+ * next collective fails (ABNN_ERR_INVALID).  Destroy every rank's
+ * communicator before the group.                                             */
+typedef struct abnn_comm_group abnn_comm_group;
+abnn_status abnn_comm_group_create(uint32_t world, abnn_comm_group** out);
+abnn_status abnn_comm_group_destroy(abnn_comm_group* g);
+abnn_status abnn_comm_create_local(abnn_comm_group* g, uint32_t rank, int device, abnn_comm** out);
 
 /* ---- statistics / timing ---------------------------------------------------- */
 abnn_status abnn_get_stats(abnn_brain* b, abnn_stats* out);   /* synchronises */

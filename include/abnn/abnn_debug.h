@@ -54,13 +54,6 @@ abnn_status abnn_debug_raw_wave_clock(const void* workspace, uint64_t workspace_
  * buf holds world x bytes, this rank's record at rank x bytes). */
 abnn_status abnn_debug_comm_allgather(abnn_comm* c, void* buf, uint64_t bytes, uint32_t count, void* stream);
 
-/* The structural update's in-place compaction gives up a wait after `limit`
- * polls (default 2^22, ~1 s) and reports it: the update returns an error and
- * the handle refuses passes until its records are reloaded.  limit = 0 makes
- * every wait give up at once (tests/test_gpu_plasticity.py exercises that
- * error path with it). */
-abnn_status abnn_debug_set_compact_spin_limit(abnn_brain* b, uint32_t limit);
-
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -283,34 +283,29 @@ static void genesis(oracle_state* s, uint64_t k, uint32_t src)
     memcpy(&g->pad, &one, 4);
 }
 
-/* After every compact_every-th pass: stable compaction of the tombstones,
- * then the grown synapses in (pass, slot) order while capacity lasts. */
+/* After every compact_every-th pass: the tombstones removed (their holes filled
+ * from the array's end), then the grown synapses in (pass, slot) order while
+ * capacity lasts. */
 static void structural_update(oracle_state* s)
 {
     const abnn_params* p = &s->p;
     if (p->compact_every == 0 || s->pass_index % p->compact_every != 0) return;
-    /* Removal (abnn.h contract): the tombstones' span [a, z) closes up in
-     * order; the D-record hole left at its end [z - D, z) takes the array's
-     * last D records in order when the tail [z, n) holds at least D of them,
-     * else the tail shifts down by D.  Records outside the span and the moved
-     * ones keep their order; the work is O(z - a + D), not O(n) -- in a sweep
-     * the span lies in the visited window. */
-    uint64_t n = s->dims.n_syn, a = n, z = 0, D = 0;
-    for (uint64_t i = 0; i < n; ++i)
-        if (s->syn[i].src == kTomb) {
-            if (a == n) a = i;
-            z = i + 1;
-            D++;
-        }
+    /* Removal (abnn.h contract, round 6): with D tombstones and m = n - D,
+     * the k-th tombstone below m (in index order) takes the k-th live record
+     * of the tail [m, n) (in index order), and the array ends at m.  Only the
+     * filled holes' records move: O(D) -- a sweep prunes inside its visited
+     * window, and the tail's live records (D of them at most) fill its holes. */
+    uint64_t n = s->dims.n_syn, D = 0;
+    for (uint64_t i = 0; i < n; ++i) D += s->syn[i].src == kTomb;
     if (D) {
-        uint64_t o = a;
-        for (uint64_t i = a; i < z; ++i)
-            if (s->syn[i].src != kTomb) s->syn[o++] = s->syn[i];  /* o ends at z - D */
-        if (n - z >= D)
-            memcpy(s->syn + (z - D), s->syn + (n - D), D * sizeof(abnn_synapse));  /* disjoint: n - D >= z */
-        else
-            memmove(s->syn + (z - D), s->syn + z, (n - z) * sizeof(abnn_synapse));
-        n -= D;
+        const uint64_t m = n - D;
+        uint64_t from = m;  /* the next tail record to consider */
+        for (uint64_t i = 0; i < m; ++i) {
+            if (s->syn[i].src != kTomb) continue;
+            while (s->syn[from].src == kTomb) ++from;  /* tail live records = holes below m */
+            s->syn[i] = s->syn[from++];
+        }
+        n = m;
     }
     const uint64_t slots = (uint64_t)p->compact_every * p->max_spikes;
     for (uint64_t j = 0; s->grown && j < slots; ++j) {

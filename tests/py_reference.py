@@ -198,18 +198,14 @@ class MetalEmu:
         self.pass_index += 1
         ce = p.get("compact_every", 0)
         if ce and self.pass_index % ce == 0:          # structural update (abnn.h contract)
-            # the tombstones' span [a, z): its live records close up in order,
-            # the D-record hole left at its end takes the array's last D
-            # records (or the whole tail shifts down when it is shorter)
-            tombs = [i for i in range(len(self.src)) if self.src[i] == TOMB]
-            if tombs:
-                a, z, n, D = tombs[0], tombs[-1] + 1, len(self.src), len(tombs)
+            # the array shrinks to m = n - D: the tombstones below m, in
+            # order, take the live records of the tail [m, n), in order
+            D = sum(1 for x in self.src if x == TOMB)
+            if D:
+                m = len(self.src) - D
                 recs = list(zip(self.src, self.dst, self.w))
-                mid = [r for r in recs[a:z] if r[0] != TOMB]
-                if n - z >= D:
-                    recs = recs[:a] + mid + recs[n - D:] + recs[z:n - D]
-                else:
-                    recs = recs[:a] + mid + recs[z:]
+                fill = iter([r for r in recs[m:] if r[0] != TOMB])
+                recs = [next(fill) if r[0] == TOMB else r for r in recs[:m]]
                 self.src = [r[0] for r in recs]
                 self.dst = [r[1] for r in recs]
                 self.w = [r[2] for r in recs]

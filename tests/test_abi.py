@@ -79,7 +79,7 @@ def test_abi_version_and_status_strings():
     from abnn_amd import _lib
 
     lib = _lib.load()
-    assert lib.abnn_abi_version() == _lib.ABI_VERSION == 9
+    assert lib.abnn_abi_version() == _lib.ABI_VERSION == 10
     assert lib.abnn_status_string(0) == b"ok"
     assert lib.abnn_status_string(4) == b"size mismatch"
 

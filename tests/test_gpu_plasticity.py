@@ -143,13 +143,14 @@ def test_plasticity_virtual_shards_vs_oracle_shards(gpu):
 @pytest.mark.parametrize("pattern", ["spread", "dense_block", "tail_short", "almost_all"])
 def test_structural_update_in_place_patterns(gpu, pattern):
     """The device-driven structural update (kernels.hip launch_structural_update:
-    span offsets, the in-place compaction with per-block read flags, the
-    hole's fill) on uploaded tombstone patterns the passes' pruning does not
-    produce -- tombstones everywhere incl. the first and last record, a dense
-    run of 50k (live records move 12 blocks down: a block waits on many
-    lower ones), tombstones near the end (the tail shorter than D shifts
-    down), and all but every 1000th record -- against the oracle's restatement
-    of the contract (abnn.h), records and count after each update."""
+    the holes' ranks, the tail's live prefix, the holes filled from the tail)
+    on uploaded tombstone patterns the passes' pruning does not produce --
+    tombstones everywhere incl. the first and last record (the tail holds
+    tombstones: the tail-scan path), a dense run of 50k (12 whole blocks of
+    holes) plus a spread (the tail is live: the direct path), a run at the
+    end that reaches below m, and all but every 1000th record -- against the
+    oracle's restatement of the contract (abnn.h), records and count after
+    each update."""
     kw = dict(w_prune=1e-30, p_new=0.0, compact_every=1)  # the passes prune nothing; the update removes the uploads'
     g, o = _pair(0, **kw)
     syn = g.download_synapses()
@@ -184,14 +185,14 @@ def _hip_copy_d2d(dst: int, src: int, nbytes: int) -> None:
 
 
 def test_failed_structural_update_refuses_passes(gpu, tmp_path):
-    """The in-place compaction cannot be rolled back, so a structural update
-    that fails part-way leaves the records invalid: the handle then refuses
-    every pass (ABNN_ERR_INVALID) until they are reloaded.  Both failures:
-    (1) a compaction wait that gives up (the debug knob's spin limit 0 makes
-    every wait give up: a 50k tombstone run makes blocks wait on lower ones);
-    (2) a tombstone tally that disagrees with the records (the last block's
-    tombstones revived behind the handle's back through the device layout).
-    After a reload the passes equal the oracle again."""
+    """A structural update that fails part-way leaves the records invalid (the
+    holes' fill moves records in place), so the handle then refuses every
+    pass (ABNN_ERR_INVALID) until they are reloaded.  The failure the fill
+    detects: a tombstone tally that disagrees with the records (the last
+    tallied block's tombstones revived behind the handle's back through the
+    device layout).  (Round 5's second case, a compaction wait that gave up,
+    has no counterpart: the round-6 fill waits on no other workgroup.)  After
+    a reload the passes equal the oracle again."""
     from abnn_amd import _lib
 
     kw = dict(w_prune=1e-30, p_new=0.0, compact_every=1)
@@ -214,15 +215,6 @@ def test_failed_structural_update_refuses_passes(gpu, tmp_path):
     def reload():
         g.load_flat(flat)
         g.set_scalars(sc["clock"], sc["reward"], sc["rbar"], sc["pass_index"])
-
-    # (1) the compaction's waits give up
-    _lib.call("abnn_debug_set_compact_spin_limit", g._h, 0)
-    with pytest.raises(_lib.AbnnError, match="wait timed out; the records are not valid"):
-        g.encode_traversal(1)
-    refused()
-    refused()
-    _lib.call("abnn_debug_set_compact_spin_limit", g._h, 1 << 22)
-    reload()
 
     # (2) records [57344, 60160) (the last tallied block's tombstones, whole
     # 256-record groups) revived with the codes and {dst, w} of records [0, 2816)

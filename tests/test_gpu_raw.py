@@ -31,7 +31,7 @@ class RawBrain:
     """Caller-owned buffers, as Brain::build_buffers allocates them (brain.cpp:52-69)."""
 
     def __init__(self, syn: np.ndarray, n_nrn: int, events: int, max_spikes: int = 2560, knobs=None,
-                 pool_chunks=None):
+                 pool_chunks=None, ws=None):
         import torch
 
         from abnn_amd import _lib
@@ -48,7 +48,10 @@ class RawBrain:
         # that many 4-KiB survivor chunks (0: every survivor recomputed)
         nb = int(self.lib.abnn_traversal_workspace_bytes(self.n_syn, events)) if pool_chunks is None else \
             int(self.lib.abnn_traversal_workspace_min_bytes(self.n_syn, events)) + 4096 * pool_chunks
-        self.ws = torch.zeros(max(16, nb), dtype=torch.uint8, device=dev)
+        if ws is not None:  # another brain's workspace (at least as large)
+            assert ws.numel() >= nb
+            nb = ws.numel()
+        self.ws = torch.zeros(max(16, nb), dtype=torch.uint8, device=dev) if ws is None else ws
         self.knobs = knobs
         a = _lib.TraversalArgs()
         p = self.scal.data_ptr()
@@ -233,3 +236,34 @@ def test_raw_config3_bit_exact_vs_threaded_oracle(gpu):
     o = _run(5_000_000, 150_000_128, 150_000_000, 16, reward_at=9, threads=32)
     st = o.stats()
     assert st["fired"] >= 2560 * 8 and st["updated"] > st["fired"]
+
+
+def test_raw_workspace_reused_across_sizes(gpu):
+    """One workspace for passes of different n_syn / events, interleaved
+    (ADVICE r5): the state the fused pass keeps across passes (epoch-tagged
+    look-back words, bounds, costs) lives at offsets that do not depend on E,
+    so a pass of another size never reads a spike list or a bound of the
+    other as a published look-back word.  Every pass bit-exact against its
+    oracle."""
+    from oracle import oracle as O
+
+    sizes = [(99_488, 1_000_000, 1_000_000), (9_488, 200_000, 150_000), (9_488, 3_000, 4_097)]
+    pairs, ws = [], None
+    for n_hidden, n_syn, events in sizes:
+        o = O.OracleBrain(256, 256, n_hidden, n_syn, events, renorm_thresh=2**64 - 1)
+        o.build_random_graph(3, nthreads=8)
+        o.set_scalars(0, 0.0, 0.0)
+        r = RawBrain(o.syn.copy(), 512 + n_hidden, events, ws=ws)
+        ws = r.ws if ws is None else ws  # the first (largest) workspace serves all three
+        pairs.append((o, r))
+    for k in range(18):
+        o, r = pairs[(k // 2) % 3]  # two passes each, round robin: every switch changes E
+        o.set_timestamps(range(256), o.clock)
+        o.pass_serial()
+        r.one_pass()
+        clock, _, rbar = r.scalars()
+        assert clock == o.clock & 0xFFFFFFFF, k
+        assert np.float32(rbar) == np.float32(o.s.rbar), k
+        assert np.array_equal(r.last_fired(), (o.last_fired & np.uint64(0xFFFFFFFF)).astype(np.uint32)), k
+        assert np.array_equal(r.records(), o.syn.view(np.uint32)), k
+        assert r.workspace_error() == 0, k

@@ -231,14 +231,14 @@ def test_c4_random_mode_eight_virtual_shards(gpu):
 
 def test_c5_4b_records_plasticity(gpu):
     """Config 5's size on one GPU: 4e9 records (44 GB of packed records; the
-    structural update compacts in place), sweep mode, reward 0.25, pruning
+    structural update works in place), sweep mode, reward 0.25, pruning
     and synaptogenesis with a structural update every 10 passes (two inside
     the test).  Every pass: at most max_spikes spikes, one clock tick, n_syn =
     n_syn(before) - pruned + grown across updates, no tombstone left in the
     swept window after an update.  The threaded oracle holds the graph's
-    first E + 4M records and its LAST 6M (the update's removal moves only
-    the tombstones' span, inside the window, and the array's last D records:
-    abnn.h), so at the end the GPU's whole array is pinned: the head and the
+    first E + 4M records and its LAST 6M (the update's removal fills the
+    window's tombstones with the array's last live records and ends the array
+    before them: abnn.h), so at the end the GPU's whole array is pinned: the head and the
     tail (grown records included) bit-exact, the untouched middle by the
     whole-array checksum (the fresh graph's, less the head's and tail's)."""
     import abnn_amd

@@ -336,22 +336,25 @@ def test_structural_plasticity_matches_python_restatement(mode, events):
 
 
 @pytest.mark.parametrize("tombs,expect", [
-    # span [2, 5), D = 2: live 3 closes up; the hole [3, 5) takes 18, 19
-    ([2, 4], [0, 1, 3, 18, 19] + list(range(5, 18))),
-    # span [0, 1): the hole is the first record
+    # D = 2, m = 18: the holes 2 and 4 take the tail's 18 and 19
+    ([2, 4], [0, 1, 18, 3, 19] + list(range(5, 18))),
+    # the first record: its hole takes the last one
     ([0], [19] + list(range(1, 19))),
-    # span [15, 19), D = 3, tail [19, 20) shorter than D: it shifts down
-    ([15, 17, 18], list(range(15)) + [16, 19]),
-    # the last record: span [19, 20), tail empty
+    # D = 3, m = 17, tombstones in the tail too: the hole 15 takes the tail's
+    # only live record, 19; 17 and 18 lie in the tail and just go
+    ([15, 17, 18], list(range(15)) + [19, 16]),
+    # the last record: nothing below m to fill
     ([19], list(range(19))),
     # every record
     (list(range(20)), []),
+    # D = 4, m = 16: holes 0, 7 take 16, 19 (17 is in the tail, 18 too)
+    ([0, 7, 17, 18], [16] + list(range(1, 7)) + [19] + list(range(8, 16))),
 ])
 def test_structural_update_removal_contract(tombs, expect):
     """The removal of abnn.h's structural update on a hand-made array (no
-    pass work: 0 events, an update after every pass): the tombstones' span
-    closes up, its hole takes the array's last D records, or the tail shifts
-    down when it holds fewer than D."""
+    pass work: 0 events, an update after every pass): with D tombstones the
+    array ends at m = n - D, and the tombstones below m take, in order, the
+    live records of the tail [m, n) in order."""
     ob = O.OracleBrain(256, 256, 100, 20, 0, compact_every=1, w_prune=0.1, syn_capacity=20)
     syn = np.zeros(20, dtype=O.SYN_DTYPE)
     syn["src"] = 256 + np.arange(20)
@@ -369,7 +372,7 @@ def test_structural_update_is_not_the_stable_compaction():
     """Deliberate change from round 4 (structural update): the
     stable compaction of the whole array is a non-goal.  Where the two orders
     differ, the records a sweep's visited window [0, events) holds after the
-    update differ too: here the window of 5 takes records 18, 19 (the hole's
+    update differ too: here the window of 5 takes records 18, 19 (the holes'
     fill), where the stable order would have given 5, 6."""
     ob = O.OracleBrain(256, 256, 100, 20, 5, compact_every=1, w_prune=0.1, syn_capacity=20)
     syn = np.zeros(20, dtype=O.SYN_DTYPE)
@@ -383,7 +386,7 @@ def test_structural_update_is_not_the_stable_compaction():
     got = ob.syn["dst"].tolist()
     stable = [i for i in range(20) if i not in (2, 4)]
     assert sorted(got) == stable and got != stable
-    assert got[:5] == [0, 1, 3, 18, 19] and stable[:5] == [0, 1, 3, 5, 6]
+    assert got[:5] == [0, 1, 18, 3, 19] and stable[:5] == [0, 1, 3, 5, 6]
 
 
 def test_structural_update_semantics():

@@ -6,6 +6,7 @@
 #   ROUNDS=2 bash tools/ab_cfg.sh head=tools/exp/r03c.so new=. new_d0=.,ABNN_DEFER_STAMPS=0
 set -o pipefail
 export TMPDIR=/tmp
+export ABNN_LIB_ANY_ABI=1  # variants of an older ABI (timing entry points only)
 mkdir -p gpurun_out
 for r in $(seq 1 "${ROUNDS:-2}"); do
   for cfg in "$@"; do

@@ -3,6 +3,7 @@
 # ROUNDS rounds of tools/pass_times.py (300 back-to-back passes, every launch
 # timed) per library.  usage: tools/ab_times.sh [ROUNDS]
 set -o pipefail
+export ABNN_LIB_ANY_ABI=1  # variants of an older ABI (timing entry points only)
 ROUNDS=${1:-3}
 libs=("abnn_amd/libabnn_hip.so" tools/exp/*.so)
 for r in $(seq 1 "$ROUNDS"); do

@@ -8,10 +8,10 @@ name=${1:?usage: tools/build_variant.sh NAME}
 cd "$(dirname "$0")/.."
 mkdir -p tools/exp
 python3 - "$name" <<'PY'
-import os, subprocess, sys
+import os, sys
 from abnn_amd import build as b
 out = os.path.join("tools", "exp", sys.argv[1] + ".so")
 extra = os.environ.get("VARIANT_FLAGS", "").split()
-subprocess.check_call([b.HIPCC, *b.HIP_FLAGS, *extra, "-o", out, *b.HIP_SOURCES])
+b.build_hip(out=out, defines=extra)
 print(out)
 PY

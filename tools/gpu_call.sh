@@ -14,10 +14,13 @@
 #   prof=<tag> / profraw=<tag>  rocprofv3 kernel trace + FETCH/WRITE passes (tools/profile.sh, profile_raw.sh)
 #   shardvar=<rounds>         sharded-path bench at world 1 per library (in-tree, tools/exp/*.so), interleaved
 #   rawclk=<file>             per-range timeline of the fused buffer-index pass (tools/raw_clock.py)
+#   benchv=<variant>:<name>[:args]  bench.py with tools/exp/<variant>.so -> gpurun_out/<name>.json
+#   pt=<file>:<lib>[,VAR=VALUE...]    tools/pass_times.py (300 passes) with a library ("." in-tree) and knobs
 #   smoke
 # usage: tools/gpu_call.sh step [step ...]
 set -o pipefail
 export TMPDIR=/tmp
+export ABNN_LIB_ANY_ABI=1  # A/B variants of an older ABI (timing entry points only)
 mkdir -p gpurun_out
 (while sleep 50; do date +%s >> gpurun_out/heartbeat.txt; done) &
 HB=$!
@@ -38,6 +41,13 @@ for st in "$@"; do
     benchbase) name=${val%%:*}; args=""; [ "$name" != "$val" ] && args=${val#*:}
            ABNN_LIB=$PWD/tools/exp/base.so timeout -k 10 400 python -u bench.py $args > "gpurun_out/$name.json" 2> "gpurun_out/$name.err" || { echo "bench $name failed"; tail -5 "gpurun_out/$name.err"; exit 1; }
            python3 tools/bench_line.py "gpurun_out/$name.json" "$name(base)" ;;
+    benchv) var=${val%%:*}; rest=${val#*:}; name=${rest%%:*}; args=""; [ "$name" != "$rest" ] && args=${rest#*:}
+           ABNN_LIB=$PWD/tools/exp/$var.so timeout -k 10 400 python -u bench.py $args > "gpurun_out/$name.json" 2> "gpurun_out/$name.err" || { echo "bench $name failed"; tail -5 "gpurun_out/$name.err"; exit 1; }
+           python3 tools/bench_line.py "gpurun_out/$name.json" "$name($var)" ;;
+    pt) name=${val%%:*}; cfg=${val#*:}; lib=${cfg%%,*}; envs=""; [ "$cfg" != "$lib" ] && envs=$(echo "${cfg#*,}" | tr ',' ' ')
+        [ "$lib" = "." ] && lib=abnn_amd/libabnn_hip.so
+        env ABNN_LIB=$PWD/$lib $envs timeout -k 10 120 python -u tools/pass_times.py 300 1 > "gpurun_out/$name" 2>&1 || { tail -5 "gpurun_out/$name"; exit 1; }
+        cat "gpurun_out/$name" ;;
     cal) bash tools/gpu_step.sh 300 fetch_cal.log timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -T --kernel-trace --output-format csv -d gpurun_out/fcal -o run -- ./tools/ubench_fetch_cal || exit 1
          python3 tools/fetch_cal.py gpurun_out/fcal | tee "gpurun_out/$val" ;;
     absweep) for r in $(seq 1 "$val"); do for lib in abnn_amd/libabnn_hip.so tools/exp/*.so; do
