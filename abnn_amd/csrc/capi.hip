@@ -878,8 +878,7 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     }
     for (int i = 0; i < 2; ++i)
         if ((s = dalloc(&b->cost_buf[i], max_ranges)) != ABNN_OK) return fail(s);
-    // look-back words, then the lazy workgroups' second words (kLbLazy)
-    if ((s = dalloc(&d.lb_status, 2 * kMaxGateBlocks)) != ABNN_OK) return fail(s);
+    if ((s = dalloc(&d.lb_status, kMaxGateBlocks)) != ABNN_OK) return fail(s);
     if ((s = dalloc(&d.cand_list, (uint64_t)kFusedMaxRanges * kCandCap)) != ABNN_OK) return fail(s);
     if (const char* env = std::getenv("ABNN_FUSED")) b->use_fused = std::atoi(env) != 0;
     d.spec_mode = 1;
@@ -891,13 +890,6 @@ abnn_status abnn_brain_create(const abnn_dims* dims, const abnn_params* params, 
     d.lean = 1;
     if (const char* env = std::getenv("ABNN_LEAN")) d.lean = std::atoi(env) != 0;
     if (const char* env = std::getenv("ABNN_SPEC")) d.spec_mode = (uint32_t)std::min(2, std::max(0, std::atoi(env)));
-    // the lazy isi (kernels.hip refrac_chunk): a dst the filter rules out is
-    // older than window_pre, so it passes the refractory gate unread only if
-    // refractory <= window_pre
-    d.lazy_isi = p.refractory <= p.window_pre ? 1u : 0u;
-    if (const char* env = std::getenv("ABNN_LAZY")) d.lazy_isi = d.lazy_isi && std::atoi(env) != 0 ? 1u : 0u;
-    d.lazy_margin = 3;
-    if (const char* env = std::getenv("ABNN_LAZY_MARGIN")) d.lazy_margin = (uint32_t)std::max(0, std::atoi(env));
     d.bitmap = b->bitmap_buf[0];
     d.filter = b->filter_buf[0];
     if ((s = dalloc(&d.range_info, max_ranges)) != ABNN_OK) return fail(s);

@@ -48,9 +48,7 @@ struct alignas(16) PassWork {
     uint32_t epoch;        // fused passes run so far: tags this pass's look-back words (never set by the host)
     uint32_t error;        // unused (the error word is host-mapped: DeviceState::err_word)
     uint32_t spec_wgs;     // fused pass: gate workgroups predicted below the budget cut (the last pass's, less one)
-    uint32_t lazy_from;    // fused pass: gate workgroups from this one on are predicted past the budget cut
-                           // (the last pass's cut + 1 + lazy_margin; 0: none): their refractory stage gathers
-                           // lastFired[dst] only where the LDS filter says dst may be recent
+    uint32_t pad;
     unsigned long long shard_g2;  // sharded fused pass: refractory survivors of the shard (the summary's word 3)
     // sharded fused pass: the pass-start scalars as the gate launch read them
     // (written by its workgroup 0), so every k_shard_walk workgroup reads
@@ -66,14 +64,6 @@ struct alignas(16) PassWork {
 // kind 1 = the spike candidates of the workgroup's ranges (capped at the
 // budget).  max_spikes < 2^30.
 constexpr uint32_t kLbAggregate = 1u;
-// kind bit 1 (word bit 31): the workgroup holds survivors whose isi it did not
-// gather (lazy); if it lies below the budget cut its walk reads lastFired for
-// them and then publishes its second word (lb_status[kMaxGateBlocks + b] =
-// tag << 32 | 1), which the stampers wait for before they stamp
-constexpr uint32_t kLbLazy = 2u;
-// a survivor entry's dst with this bit set: isi not gathered (its updated
-// weight is computed by the walk, if the entry is below the budget)
-constexpr uint32_t kDstLazy = 0x80000000u;
 constexpr uint32_t kLbSpinLimit = 1u << 22;  // ~1 s of polls: then error, never a hang
 
 // Synapse records on the device, structure of arrays: record
@@ -188,9 +178,6 @@ struct DeviceState {
     uint32_t spec_mode;       // fused: speculative weight stores 0 off, 1 below the predicted cut (default),
                               // 2 everywhere (ABNN_SPEC; 2 exercises the restore path)
     uint32_t lean;            // fused single-GPU pass without plasticity: the lean kernel (ABNN_LEAN, default 1)
-    uint32_t lazy_isi;        // fused single-GPU pass: workgroups predicted past the cut skip lastFired[dst] for
-                              // dsts the LDS filter rules out (needs refractory <= window_pre; ABNN_LAZY, default 1)
-    uint32_t lazy_margin;     // ... workgroups past the last cut that still gather eagerly (ABNN_LAZY_MARGIN, 3)
     uint32_t shard_mode;      // fused pass = the first launch of a sharded pass (k_gate: no stamps, exchange record)
     int32_t* xchg;            // ... its exchange record (abnn.h: summary + local spike list)
     uint32_t prologue_adapt;  // the previous pass was fused over the same ranges: its costs move the next

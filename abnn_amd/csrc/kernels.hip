@@ -309,18 +309,6 @@ __device__ __forceinline__ bool f2_test(const uint32_t* s_f2, uint32_t n)
     return ((s_f2[h1 >> 5] >> (h1 & 31u)) & (s_f2[h2 >> 5] >> (h2 & 31u)) & 1u) != 0u;
 }
 
-// Whether neuron n may be recent at pass start (the blocked filter of the LDS
-// copy and the second-level filter; no false negatives): the refractory
-// stage's test of a dst.  A dst it rules out is older than window_pre, so
-// with refractory <= window_pre it passes the refractory gate without its
-// lastFired being read (the lazy isi).
-__device__ __forceinline__ bool nrn_maybe_recent(const uint2* s_fb, const uint32_t* s_f2, uint32_t n)
-{
-    const uint32_t j = n >> 5, t = filter_t(j, 13), g = (j ^ t) & (kCodeFilterWords - 1);
-    const uint2 f = s_fb[g];
-    return ((f.x >> (n & 31u)) & (f.y >> ((n + t) & 31u)) & 1u) && f2_test(s_f2, n);
-}
-
 // ---------------------------------------------------------------------------
 // k_bitmap: bit i = (now - lastFired[i]) <= window_pre; stimulus stamp fused.
 // A wave covers 256 neurons = four bitmap words; lane l owns neurons
@@ -512,34 +500,14 @@ __device__ __forceinline__ uint4 range_totals(const DeviceState& d, uint32_t r) 
 // (the workgroup is predicted to lie below the pass's budget cut) the updated
 // weight is stored here already; the walk restores w where the prediction was
 // wrong.
-// The lazy isi is an experiment compiled in only
-// with -DABNN_LAZY_ISI (tools/build_variant.sh): measured slower than the
-// eager refractory stage, so the product builds without it.
-#ifdef ABNN_LAZY_ISI
-constexpr bool kLazyBuild = true;
-#else
-constexpr bool kLazyBuild = false;
-#endif
-
-// lazy (fused sweep, a workgroup predicted past the budget cut; wave-uniform):
-// lastFired[dst] is gathered only where the filter (s_fb, s_f2) says dst may
-// be recent; the other survivors pass the refractory gate on the filter's word
-// (age > window_pre >= refractory) and are stored with kDstLazy and no updated
-// weight -- the walk computes it if such an entry falls below the budget.
-// The fourth count returned is the number of such survivors.
 template <int R, bool kRandom, bool kFused, bool kTail, class At>
 __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const KernelParams& kp, uint64_t region,
                                               uint64_t base, uint32_t n, uint64_t now, uint64_t pass, float Rw,
                                               float rbw, bool spec, uint32_t crange, uint32_t c0,
-                                              const uint32_t* s_f2, At&& at, uint4* lds_out = nullptr,
-                                              bool lazy = false, const uint2* s_fb = nullptr)
+                                              const uint32_t* s_f2, At&& at, uint4* lds_out = nullptr)
 {
     const uint32_t lane = threadIdx.x & 63, nn = (uint32_t)d.n_nrn;
-    uint32_t n_g1 = 0, n_g2 = 0, n_cand = 0, n_lazy = 0;
-    // (the tail only: in the steady state a sparse range's staged events all
-    // wait for its tail, and the dense ranges lie below the cut, eager; every
-    // mid-stream instance of this function would grow the stream loop's code)
-    constexpr bool kLazyOk = kLazyBuild && kFused && !kRandom && kTail;
+    uint32_t n_g1 = 0, n_g2 = 0, n_cand = 0;
     auto record_of = [&](uint32_t rel) -> uint64_t {
         const uint64_t t = region + rel;
         return kRandom ? pick_record(d.seed, d.syn_offset, pass, t, d.n_syn) : t;
@@ -606,26 +574,14 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
         }
         // the stimulus of this pass is stamped `now` (brain.cpp:82) by k_bitmap
         // or, in steady state, by the gate itself at some point of the pass
-        // lz: lazy, dst not recent (filter), so its lastFired is not read
-        bool lz[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            lz[j] = false;
-            if constexpr (kLazyOk)
-                lz[j] = lazy && dst[j] < nn && dst[j] - d.stim_first >= d.stim_count &&
-                        !nrn_maybe_recent(s_fb, s_f2, dst[j]);
-        }
         if constexpr (!kTail) {
 #pragma unroll
             for (int j = 0; j < R; ++j)
-                ld[j] = dst[j] - d.stim_first < d.stim_count ? now
-                                                             : (dst[j] < nn && !lz[j] ? d.last_fired[dst[j]] : 0ull);
+                ld[j] = dst[j] - d.stim_first < d.stim_count ? now : (dst[j] < nn ? d.last_fired[dst[j]] : 0ull);
         } else {
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                const bool need = dst[j] < nn && !lz[j];
-                // (lazy: a round none of whose lanes needs its lastFired issues no load)
-                ld[j] = (!kLazyOk || !lazy || __ballot(need) != 0) ? d.last_fired[need ? dst[j] : 0u] : 0ull;
+                ld[j] = d.last_fired[dst[j] < nn ? dst[j] : 0u];
             }
 #pragma unroll
             for (int j = 0; j < R; ++j)
@@ -635,18 +591,16 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
         for (int j = 0; j < R; ++j) {
             if (b0 + (uint32_t)j * 64 >= n) break;  // wave-uniform
             n_g1 += (uint32_t)__popcll(__ballot(bw[j] != 0u));
-            // brain.metal:79-83 (lz: older than window_pre >= refractory)
-            const bool g2 = dst[j] < nn && (lz[j] || age32(now, ld[j]) > kp.refractory);
+            const bool g2 = dst[j] < nn && age32(now, ld[j]) > kp.refractory;  // brain.metal:79-83
             const uint64_t tg = d.syn_offset + region + rel[j];
             const bool cand = g2 && spike_candidate(kp, w[j], tg, now);
             const uint64_t bg = __ballot(g2), bcd = __ballot(cand);
-            if constexpr (kLazyOk) n_lazy += (uint32_t)__popcll(__ballot(g2 && lz[j]));
             if (g2) {
                 const uint64_t o = base + n_g2 + mbcnt64(bg);
                 if constexpr (kFused) {
-                    const float wn = lz[j] ? 0.0f : updated_weight(kp, w[j], cand, Rw, rbw, (float)age32(now, ld[j]));
+                    const float wn = updated_weight(kp, w[j], cand, Rw, rbw, (float)age32(now, ld[j]));
                     const uint4 ent = make_uint4(rel[j] | (cand ? 0x80000000u : 0u), __float_as_uint(w[j]),
-                                                 __float_as_uint(wn), dst[j] | (lz[j] ? kDstLazy : 0u));
+                                                 __float_as_uint(wn), dst[j]);
                     if (kTail && lds_out) {
                         // the fused tail keeps its survivors in LDS (fused_end's
                         // walk reads them there, and stores the weights)
@@ -676,7 +630,7 @@ __device__ __forceinline__ uint4 refrac_chunk(const DeviceState& d, const Kernel
             n_cand += (uint32_t)__popcll(bcd);
         }
     }
-    return make_uint4(n_g1, n_g2, n_cand, n_lazy);
+    return make_uint4(n_g1, n_g2, n_cand, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -798,8 +752,7 @@ constexpr uint32_t kLbMaxWords = 8;  // look-back words per lane: gate_blocks <=
 
 // One wave sweeps the words of workgroups [0, n): their values (capped sum)
 // once all carry `tag`, or as soon as the published ones reach the budget
-// (stop_at_budget).  vals: this lane's words (q = 64 i + lane), for the caller:
-// the value in bits 0-29, the workgroup's kLbLazy kind bit in bit 31.
+// (stop_at_budget).  vals: this lane's words (q = 64 i + lane), for the caller.
 // pub != 0: this workgroup's own word, published by lane 0 right after the
 // first sweep's loads are issued (a load issued after a store waits for it:
 // vmcnt counts both, in order).
@@ -830,9 +783,8 @@ __device__ uint32_t wg_poll(const DeviceState& d, uint32_t n, uint32_t tag, uint
             vals[i] = 0u;
             if (i * 64 < n && q < n) {
                 const bool mine = (uint32_t)(raw[i] >> 32) == tag;
-                // the value, and the lazy kind bit (kLbLazy) in bit 31
-                vals[i] = mine ? (uint32_t)raw[i] & 0xBFFFFFFFu : 0u;
-                sum += vals[i] & 0x3FFFFFFFu;
+                vals[i] = mine ? (uint32_t)raw[i] & 0x3FFFFFFFu : 0u;
+                sum += vals[i];
                 ok = ok && mine;
             }
         }
@@ -902,22 +854,6 @@ __device__ void fused_next_bounds(const DeviceState& d, uint32_t* cc)
     }
     const uint32_t gain = (uint64_t)cmax * NR > 4ull * total ? 4u : 0u;
     if (mine) d.range_bounds_next[k] = adapted_bound(d, cc, d.range_bounds_prev, NR, k, total, d.range_bounds[k], gain);
-}
-
-// A lazy survivor (kDstLazy: its refractory stage did not gather isi) that
-// reached the update: lastFired[dst] read now and the updated weight computed
-// (brain.metal:101-121, the entry's w and candidate bit).  Only in a workgroup
-// predicted past the budget cut that lies below it after all: the stamps of
-// the pass wait for its second look-back word (fused_end), so this read sees
-// the pass-start value (C1).
-__device__ __forceinline__ void resolve_lazy(const DeviceState& d, const KernelParams& kp, const ApplyCtx& c, uint4& x,
-                                             bool cand)
-{
-    if (x.w & kDstLazy) {
-        x.w &= ~kDstLazy;
-        const uint64_t ld = d.last_fired[x.w];
-        x.z = __float_as_uint(updated_weight(kp, __uint_as_float(x.y), cand, c.R, c.rb, (float)age32(c.now, ld)));
-    }
 }
 
 // The walk of one range's survivors (the fused pass's g2x entries, contiguous
@@ -994,16 +930,12 @@ __device__ __forceinline__ uint32_t range_walk(const DeviceState& d, const Kerne
             if (b0 + j * 64 >= S || (!spec && P >= budget)) break;  // wave-uniform
             const uint32_t q = b0 + j * 64 + lane;
             const bool v = q < S, cand = v && (e[j].x >> 31);
-            uint4 x = make_uint4(e[j].x & 0x7FFFFFFFu, e[j].y, e[j].z, e[j].w);
+            const uint4 x = make_uint4(e[j].x & 0x7FFFFFFFu, e[j].y, e[j].z, e[j].w);
             const uint64_t bc = __ballot(cand);
             const uint64_t pre = P + mbcnt64(bc);  // spike candidates before this event
             const bool below = v && pre < budget;
             if (!spec) {
-                if (below) {
-                    if constexpr (kLazyBuild) resolve_lazy(d, kp, ac, x, cand);
-                    apply_event(d, kp, ac, region, x, cand, pre, region + q);
-                }
-                if constexpr (kLazyBuild) x.w &= ~kDstLazy;
+                if (below) apply_event(d, kp, ac, region, x, cand, pre, region + q);
             } else if (below) {
                 ++ac.upd;
                 if (cand) record_spike(d, kp, ac, x, pre, region + q);
@@ -1034,16 +966,12 @@ __device__ __forceinline__ void lds_walk(const DeviceState& d, const KernelParam
     for (uint32_t q0 = 0; q0 < S && P < budget; q0 += 64) {  // wave-uniform
         const uint32_t q = q0 + lane;
         const bool v = q < S;
-        const uint4 xe = v ? e[q] : make_uint4(0u, 0u, 0u, 0u);
-        uint4 x = make_uint4(xe.x & 0x7FFFFFFFu, xe.y, xe.z, xe.w);
-        const bool cand = v && (xe.x >> 31);
+        const uint4 x = v ? e[q] : make_uint4(0u, 0u, 0u, 0u);
+        const bool cand = v && (x.x >> 31);
         const uint64_t bc = __ballot(cand);
         const uint64_t pre = P + mbcnt64(bc);
-        if (v && pre < budget) {
-            if constexpr (kLazyBuild) resolve_lazy(d, kp, ac, x, cand);
-            apply_event(d, kp, ac, region, x, cand, pre, 0);
-        }
-        if (set_next) wave_set_next_dedup(d, cand && pre < budget, kLazyBuild ? x.w & ~kDstLazy : x.w, setc);
+        if (v && pre < budget) apply_event(d, kp, ac, region, make_uint4(x.x & 0x7FFFFFFFu, x.y, x.z, x.w), cand, pre, 0);
+        if (set_next) wave_set_next_dedup(d, cand && pre < budget, x.w, setc);  // this pass's spikes
         P += (uint64_t)__popcll(bc);
     }
 }
@@ -1136,8 +1064,6 @@ struct FusedLds {
     uint32_t done;                     // waves through their refractory stage
     uint32_t total;                    // candidates of the pass (capped; workgroup 0)
     uint32_t sg2;                      // sharded pass: the workgroup's refractory survivors
-    uint32_t lazy;                     // some range of the workgroup holds lazy survivors (kDstLazy)
-    uint32_t waitlazy;                 // stamping: some lazy workgroup below the cut must publish its walk first
 };
 
 // Fused pass: range r's wave after its refractory stage (g1 pre-gated; Sg
@@ -1162,7 +1088,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
                                           const uint4* tl, uint32_t stream_cost, bool empty, bool spec, uint64_t now,
                                           float R, float rb, uint64_t pass, uint32_t epoch, FusedLds<NW>& L,
                                           uint64_t t_stream, uint32_t h0, uint32_t chunk_t, uint32_t nch,
-                                          uint64_t* wcb, uint32_t n_lazy)
+                                          uint64_t* wcb)
 {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, budget = kp.max_spikes;
     const uint32_t tag = epoch + 1u;
@@ -1174,7 +1100,6 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     const uint32_t S = Sg + St, C = Cg + Ct;  // the range's survivors and spike candidates
     uint32_t order = 0;
     if (lane == 0) {
-        if (kLazyBuild && n_lazy) L.lazy = 1u;
         L.cand[wid] = C < budget ? C : budget;
         if (shard) atomicAdd(&L.sg2, S);
         order = atomicAdd(&L.done, 1u);
@@ -1202,8 +1127,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     if (wid == 0) {
         uint32_t c = lane < (uint32_t)NW ? L.cand[lane] : 0u;
         c = wave_sum(c);
-        const uint32_t kind = kLbAggregate | (kLazyBuild && L.lazy ? kLbLazy : 0u);
-        const uint64_t word = (uint64_t)tag << 32 | (uint64_t)kind << 30 | (c < budget ? c : budget);
+        const uint64_t word = (uint64_t)tag << 32 | (uint64_t)kLbAggregate << 30 | (c < budget ? c : budget);
         uint32_t e;
         if (shard) {
             // the pass's refractory survivors for the exchange summary: added
@@ -1241,46 +1165,25 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     // done: no lastFired read is left, the stamps may land.  Wave 0 waits for
     // that before its walk (its loads then wait for no store of the walk).
     uint32_t tot = 0, t0 = 0;
-    uint32_t lazy_wait = 0;  // wave 0 of a stamping workgroup: bit i = word 64 i + lane is a lazy workgroup
-                             // below the cut (not this one): its walk reads lastFired, the stamps wait for it
     if (wid == 0 && stamping) {
         tot = wg_poll(d, gridDim.x, tag, budget, false, vals);
-        // the budget's cut (the next pass's predictions, refrac_chunk's spec
-        // and lazy) and the lazy workgroups below it
-        uint32_t run = 0, cut = gridDim.x;
-        bool any_lazy = false;
-        if constexpr (kLazyBuild) {
-#pragma unroll
-            for (uint32_t i = 0; i < kLbMaxWords; ++i) any_lazy = any_lazy || (vals[i] >> 31);
-            any_lazy = __ballot(any_lazy) != 0;
-        }
-        if (first || any_lazy) {
+        if (first) {
+            // the next pass's prediction (refrac_chunk's spec): the workgroups
+            // below the one where the budget ran out, less one
+            uint32_t run = 0, cut = gridDim.x;
 #pragma unroll
             for (uint32_t i = 0; i < kLbMaxWords; ++i) {
-                const uint32_t v = vals[i] & 0x3FFFFFFFu;
-                const uint32_t inc = wave_incl_scan(v) + run;  // prefix through word 64 i + lane
-                const uint64_t hit = __ballot(inc >= budget && inc - v < budget);
+                const uint32_t inc = wave_incl_scan(vals[i]) + run;  // prefix through word 64 i + lane
+                const uint64_t hit = __ballot(inc >= budget && inc - vals[i] < budget);
                 if (hit && cut == gridDim.x) cut = i * 64 + (uint32_t)__builtin_ctzll(hit);
-                const uint32_t q = i * 64 + lane;
-                if (kLazyBuild && (vals[i] >> 31) && inc - v < budget && q < gridDim.x && q != blockIdx.x)
-                    lazy_wait |= 1u << i;
                 run = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
             }
-        }
-        if constexpr (kLazyBuild) {
-            const bool any_wait = __ballot(lazy_wait != 0) != 0;
-            if (lane == 0) L.waitlazy = any_wait ? 1u : 0u;
-        }
-        if (first) {
             // the event-0 flag (refrac_chunk): stored and drained before its
             // workgroup's word was published
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             t0 = __hip_atomic_load((gu32*)&d.work->t0_g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("" ::"v"(t0));  // consumed here, before any store of the walk (see range_walk)
-            if (lane == 0) {
-                d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
-                d.work->lazy_from = cut >= gridDim.x ? gridDim.x : min(gridDim.x, cut + 1u + d.lazy_margin);
-            }
+            if (lane == 0) d.work->spec_wgs = spec_prediction(d, cut, gridDim.x);
         }
     }
     const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
@@ -1333,12 +1236,6 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     // LDS only (the statistics, the LDS spike list): the walks' stores stay in flight
     if (shard || (stamping && !spk_lds)) __syncthreads();
     else lds_barrier();
-    // a lazy workgroup: every wave's walk is done (a walk below the cut read
-    // lastFired for its lazy survivors, values consumed): the second word
-    // lets the stampers go on (they wait for it only below the cut)
-    if (kLazyBuild && !shard && L.lazy && threadIdx.x == 0)
-        __hip_atomic_store((gu64*)(d.lb_status + kMaxGateBlocks + blockIdx.x), (uint64_t)tag << 32 | 1u,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) {
         typedef unsigned long long ull;
         abnn_stats* st = d.wg_stats + blockIdx.x % kWalkBlocks;
@@ -1375,25 +1272,6 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         return;
     }
     uint64_t* wc0 = wcb + (uint64_t)kWaveClock * r;  // diagnostics, wave 0: exit
-    if (kLazyBuild && stamping && L.waitlazy) {  // a mispredicted lazy workgroup below the cut: its walk's reads first
-        if (wid == 0) {
-            for (uint32_t spins = 0;; ++spins) {  // wave-uniform
-                bool ok = true;
-#pragma unroll
-                for (uint32_t i = 0; i < kLbMaxWords; ++i)
-                    if ((lazy_wait >> i) & 1u)
-                        ok = ok && (uint32_t)(__hip_atomic_load((gu64*)(d.lb_status + kMaxGateBlocks + i * 64 + lane),
-                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
-                if (__ballot(!ok) == 0) break;
-                if (spins >= kLbSpinLimit) {  // never hang the GPU: report and go on
-                    if (lane == 0) __hip_atomic_store(d.err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        lds_barrier();
-    }
     if (stamping) {
         if (spk_lds) {
             for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
@@ -1608,8 +1486,6 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         if (tid < 5) s_fz.stat[tid] = 0u;
         if (tid == 0) s_fz.done = 0u;
         if (tid == 0) s_fz.sg2 = 0u;
-        if (tid == 0) s_fz.lazy = 0u;
-        if (tid == 0) s_fz.waitlazy = 0u;
         if (tid < kSetCache) s_fz.setc[tid] = ~0ull;
         // the filter images in LDS for every wave, the first records still in
         // flight: this wave's LDS-DMAs are older than its kDepth iterations of
@@ -1674,7 +1550,6 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         tot.x += c.x;
         tot.y += c.y;
         tot.z += c.z;
-        tot.w += c.w;
         nch += pend >= kChunk;
         pend = 0;
         chunk_t += (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc);
@@ -1897,17 +1772,8 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         const bool lds_ok = kShard ? false : (kLean || (!d.shard_mode && !d.g2src));
         if (lds_ok && pend <= 256u) tail_lds = reinterpret_cast<uint4*>(s_stage[wid]);
     }
-    // fused single-GPU sweep: a workgroup predicted past the budget cut (the
-    // previous pass's cut + 1 + lazy_margin on) gathers lastFired[dst] only
-    // where the LDS filter says dst may be recent (refrac_chunk lazy).  Read
-    // here, not held through the stream (workgroup 0 writes it only once
-    // every look-back word, this one's included, is published)
-    bool lazy_wg = false;
-    if constexpr (kLazyBuild && kFused && !kRandom && !kShard)
-        lazy_wg = d.lazy_isi && !d.shard_mode && !spec && blockIdx.x >= sload(&d.work->lazy_from) &&
-                  sload(&d.work->lazy_from) != 0u;
     const uint4 c = refrac_chunk<kChunk / 64, kRandom, kFused, true>(d, kp, region, tb, pend, now, pass, Rw, rbw, spec,
-                                                               r, tot.z, s_f2, stage_at, tail_lds, lazy_wg, s_fb);
+                                                               r, tot.z, s_f2, stage_at, tail_lds);
     const uint64_t gt = ((t_stream - t_start) >> 2) + (uint64_t)nch * d.chunk_penalty;
     const uint32_t cost = len ? (uint32_t)(gt < 1 ? 1 : (gt > 0xFFFFu ? 0xFFFFu : gt)) : 0u;
     if constexpr (kFused) {
@@ -1917,7 +1783,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         const bool tl = tail_lds != nullptr;
         fused_end<BLOCK, NW, kLean, kShard>(d, kp, r, region, tot.x + c.x, tl ? tot.y : tot.y + c.y, tl ? tot.z : tot.z + c.z,
                              tl ? c.y : 0u, tl ? c.z : 0u, tail_lds, (uint32_t)gf, len == 0, spec, now, Rw, rbw, pass_f,
-                             epoch, s_fz, t_stream, hw0, chunk_t, nch, wcb, tot.w + c.w);
+                             epoch, s_fz, t_stream, hw0, chunk_t, nch, wcb);
         return;
     }
     if (lane == 0) {
