@@ -17,6 +17,7 @@
 #   benchv=<variant>:<name>[:args]  bench.py with tools/exp/<variant>.so -> gpurun_out/<name>.json
 #   pt=<file>:<lib>[,VAR=VALUE...]    tools/pass_times.py (300 passes) with a library ("." in-tree) and knobs
 #   trace=<tag>[:bench args]        rocprofv3 kernel trace + stats of bench.py (tools/prof_trace.sh)
+#   pmcrandom=<tag>                 TA / TCC counters of random mode's gate (tools/pmc_random.sh)
 #   smoke
 # usage: tools/gpu_call.sh step [step ...]
 set -o pipefail
@@ -51,6 +52,7 @@ for st in "$@"; do
         cat "gpurun_out/$name" ;;
     trace) tag=${val%%:*}; args=""; [ "$tag" != "$val" ] && args=${val#*:}
            bash tools/gpu_step.sh 600 "trace_$tag.log" bash tools/prof_trace.sh "$tag" $args || exit 1; cat "gpurun_out/trace_$tag.log" ;;
+    pmcrandom) bash tools/gpu_step.sh 400 "pmcrandom_$val.log" bash tools/pmc_random.sh "$val" || exit 1; cat "gpurun_out/pmcrandom_$val.log" ;;
     cal) bash tools/gpu_step.sh 300 fetch_cal.log timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -T --kernel-trace --output-format csv -d gpurun_out/fcal -o run -- ./tools/ubench_fetch_cal || exit 1
          python3 tools/fetch_cal.py gpurun_out/fcal | tee "gpurun_out/$val" ;;
     absweep) for r in $(seq 1 "$val"); do for lib in abnn_amd/libabnn_hip.so tools/exp/*.so; do
