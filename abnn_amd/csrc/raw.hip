@@ -1263,11 +1263,14 @@ __global__ __launch_bounds__(kRawBlock) void k_raw_pass(uint4* __restrict__ syn,
     }
     __syncthreads();  // every wave of the workgroup through its tail: the tallies complete
     if (wid == 0) {
-        // the workgroup's flag stores (hdr->ovf, hdr->err) released at agent
-        // scope before its look-back word publishes them (the stampers acquire
-        // after their poll); the barrier above drained every wave's stores, so
-        // this waits for nothing in practice
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // the workgroup's flag stores (hdr->ovf, hdr->err) are agent-scope
+        // atomics, performed at the coherence point, and the barrier above
+        // drained them (s_waitcnt vmcnt(0)) before this wave publishes the
+        // look-back word below: the stampers' acquire after their poll reads
+        // them with agent-scope loads.  Not an agent-scope release
+        // fence: on gfx950 that is an L2 write-back (buffer_wbl2) on every
+        // workgroup's critical path, +7 us per pass measured
+        // (profiles/r06g_raw_release_fence_ab.txt)
         // the groups' candidates -> their exclusive prefix in the workgroup
         // (each lane a run of consecutive groups)
         const uint32_t per = (ngrp + 63) / 64, g0 = lane * per;
