@@ -225,6 +225,7 @@ def _share_hip_runtime_with_torch() -> None:
 
 # diagnostics (include/abnn/abnn_debug.h, outside the stable boundary)
 DEBUG_SIGNATURES = [
+    ("abnn_debug_set_wave_clock", C.c_int, [_VP, C.c_int]),
     ("abnn_debug_raw_stats", C.c_int, [_VP, C.POINTER(C.c_uint64), _VP]),
     ("abnn_debug_raw_gate_timing", C.c_int, [C.c_int]),
     ("abnn_debug_raw_gate_time", C.c_int, [C.POINTER(C.c_double), _PU32]),

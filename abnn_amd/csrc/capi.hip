@@ -1741,6 +1741,15 @@ abnn_status abnn_comm_sync_visits(abnn_brain* b, abnn_comm* c, void* stream)
     return st;
 }
 
+// Diagnostics (not part of abnn.h): record the per-wave gate times of the
+// following passes (on) or not (off, the default).
+abnn_status abnn_debug_set_wave_clock(abnn_brain* b, int on)
+{
+    REQUIRE(b, "null argument");
+    b->d.wave_clock_on = on ? 1u : 0u;
+    return ABNN_OK;
+}
+
 // Diagnostics (not part of abnn.h): the last pass's per-wave gate times,
 // kWaveClock u64 per range (engine.h, DeviceState::wave_clock), 100 MHz ticks.
 abnn_status abnn_debug_wave_clock_slot(abnn_brain* b, uint32_t slot, uint64_t* out, uint64_t n)

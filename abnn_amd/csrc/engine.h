@@ -153,6 +153,8 @@ struct DeviceState {
     uint32_t* err_word;       // host-mapped: a fused pass's look-back wait gave up (capi.hip pass_error)
     uint64_t* wave_clock;     // [kWaveClockPasses][kWaveClock * kMaxRanges] per-wave gate times {start, stream done, refractory
                               // tail done, entry, (fused) look-back done, walk done} (100 MHz, diagnostics)
+    uint32_t wave_clock_on;   // record them (abnn_debug_set_wave_clock; off by default: their stores cost
+                              // ~1.2 us per fused pass, profiles/r06l_ab_wave_clock_stores.txt)
     uint32_t* fired_ring;     // [kFiredRing * max_spikes] spike list of pass q at (q % kFiredRing), budget order
     uint32_t* n_fired_ring;   // [kFiredRing] their lengths (k_apply workgroup 0)
     uint64_t* apply_clock;    // [8 * kWalkBlocks] per-workgroup k_apply timeline (diagnostics, 100 MHz)

@@ -1219,6 +1219,8 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
         atomicAdd(&L.stat[3], wf);
         atomicAdd(&L.stat[4], wp);
         d.cost_out[r] = empty ? 0u : (stream_cost < 1 ? 1u : (stream_cost > 0xFFFFu ? 0xFFFFu : stream_cost));
+    }
+    if (lane == 0 && d.wave_clock_on) {
         uint64_t* wc = wcb + (uint64_t)kWaveClock * r;  // diagnostics (tools/wave_clock.py)
         wc[1] = t_stream;  // wc[0], wc[3]: stored by k_gate at the stream's start
         wc[2] = t_tail;
@@ -1296,7 +1298,7 @@ __device__ __forceinline__ void fused_end(const DeviceState& d, const KernelPara
     }
     // last: no load of this pass follows these stores
     zero_next_images(d, kCodeFilterWords, BLOCK, now);
-    if (threadIdx.x == 0) wc0[13] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && d.wave_clock_on) wc0[13] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------------------
@@ -1503,7 +1505,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
     // diagnostics (tools/wave_clock.py): the fused pass keeps the last
     // kWaveClockPasses passes' clocks (slot pass % kWaveClockPasses)
     uint64_t* wcb = d.wave_clock + (kFused ? (pass_f % kWaveClockPasses) * (uint64_t)kWaveClock * kMaxRanges : 0);
-    if (lane == 0) {  // stored now, not held through the stream
+    if (lane == 0 && d.wave_clock_on) {  // stored now, not held through the stream
         wcb[kWaveClock * r] = t_start;
         wcb[kWaveClock * r + 3] = t_entry;
     }
@@ -1747,7 +1749,7 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
             if (j == 0 || it + j < it_end) step(bufs[j], it + j);
     }
     const uint64_t t_stream = __builtin_amdgcn_s_memrealtime();
-    if (!kFused && lane == 0) {  // diagnostics (tools/wave_clock.py; the fused pass stores them in fused_end)
+    if (!kFused && lane == 0 && d.wave_clock_on) {  // diagnostics (tools/wave_clock.py; the fused pass stores them in fused_end)
         d.wave_clock[kWaveClock * r + 6] = chunk_t;
         d.wave_clock[kWaveClock * r + 7] = nch;
     }
@@ -1797,9 +1799,10 @@ __global__ __launch_bounds__(BLOCK) void k_gate(DeviceState d, KernelParams kp)
         // made shorter than the average, leaving room for that variation.
         d.range_info[r] = make_uint4(cost, tot.y + c.y, tot.z + c.z, nch);
         d.range_g1[r] = tot.x + c.x;
-        // diagnostics (tools/wave_clock.py): 100 MHz wall clock
-        d.wave_clock[kWaveClock * r + 1] = t_stream;
-        d.wave_clock[kWaveClock * r + 2] = __builtin_amdgcn_s_memrealtime();
+        if (d.wave_clock_on) {  // diagnostics (tools/wave_clock.py): 100 MHz wall clock
+            d.wave_clock[kWaveClock * r + 1] = t_stream;
+            d.wave_clock[kWaveClock * r + 2] = __builtin_amdgcn_s_memrealtime();
+        }
     }
 }
 

@@ -14,8 +14,12 @@
 extern "C" {
 #endif
 
+/* Record the per-wave gate timeline of the following passes (on != 0) or not
+ * (the default: the timeline's stores cost ~1.2 us per fused pass). */
+abnn_status abnn_debug_set_wave_clock(abnn_brain* b, int on);
 /* The last pass's per-wave gate timeline: 12 u64 per range (100-MHz ticks:
- * start, stream done, tail done, entry, look-back done, walk done, ...). */
+ * start, stream done, tail done, entry, look-back done, walk done, ...),
+ * recorded while abnn_debug_set_wave_clock is on. */
 abnn_status abnn_debug_wave_clock(abnn_brain* b, uint64_t* out, uint64_t n);
 /* The same for pass p of the fused single-GPU pass, slot = p % 8 (the last
  * eight fused passes are kept). */

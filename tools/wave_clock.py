@@ -18,6 +18,8 @@ from abnn_amd import CONFIGS, Brain  # noqa: E402
 wl = CONFIGS[os.environ.get("CFG", "c3")]
 b = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, wl.events, device=0)
 b.build_random_graph(1)
+if hasattr(b._lib, "abnn_debug_set_wave_clock"):  # the timeline is recorded on request only
+    b._lib.abnn_debug_set_wave_clock(b._h, 1)
 b.set_auto_stimulus(0, wl.n_input)
 passes = int(sys.argv[1]) if len(sys.argv) > 1 else 12
 first = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # print passes >= first

@@ -18,6 +18,8 @@ passes = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 events = int(os.environ.get("EVENTS", wl.events))  # EVENTS=1000000000: the full sweep
 b = Brain(wl.n_input, wl.n_output, wl.n_hidden, wl.n_syn, events, device=0)
 b.build_random_graph(1)
+if hasattr(b._lib, "abnn_debug_set_wave_clock"):  # the timeline is recorded on request only
+    b._lib.abnn_debug_set_wave_clock(b._h, 1)
 b.set_auto_stimulus(0, wl.n_input)
 b.encode_traversal(74)
 b.synchronize()
