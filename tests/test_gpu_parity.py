@@ -58,6 +58,33 @@ def test_config1_every_pass(gpu):
     assert g.stats() == o.stats()
 
 
+def test_wave_clock_only_on_request(gpu):
+    """The per-wave diagnostic timeline (abnn_debug.h) is recorded only after
+    abnn_debug_set_wave_clock(b, 1) -- its stores cost 1.6 us per fused pass
+    (profiles/r06l_ab_wave_clock_stores.txt) -- and recording it changes no
+    result: the pass with it on is still bit-exact against the oracle."""
+    import ctypes
+
+    g, o = _pair(99_488, 1_000_000, 1_000_000)
+    f = g._lib.abnn_debug_wave_clock
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    buf = np.zeros(16 * 4096, dtype=np.uint64)
+    for k in range(4):
+        g.encode_traversal(1)
+        o.pass_threaded(nthreads=16)
+    assert f(g._h, buf.ctypes.data, buf.size) == 0
+    assert not buf.any(), "wave clocks recorded while off"
+    assert g._lib.abnn_debug_set_wave_clock(g._h, 1) == 0
+    for k in range(4):
+        g.encode_traversal(1)
+        o.pass_threaded(nthreads=16)
+        _assert_same(g, o, f"clocks on, pass {k}")
+    assert f(g._h, buf.ctypes.data, buf.size) == 0
+    w = buf.reshape(-1, 16)
+    assert (w[:, 0] > 0).any() and (w[:, 1] >= w[:, 0]).all(), "stream start / end not recorded"
+    assert g.stats() == o.stats()
+
+
 def test_c2_lite_every_pass(gpu):
     # 100k neurons, 1M synapses: all-gated passes 3-5, then the budget-saturated steady state
     g, o = _pair(99_488, 1_000_000, 1_000_000)
