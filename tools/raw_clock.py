@@ -49,3 +49,21 @@ if P > 1:
     print("mean lateness over passes: std %.1f (persistent part)  max %.1f" % (late.mean(0).std(), late.mean(0).max()))
 os.makedirs("gpurun_out", exist_ok=True)
 np.save("gpurun_out/raw_clock.npy", W)
+# the pass's end: per pass, the last tail (stream end), look-back, walk and
+# wave end, and the workgroups that end last (stampers are the workgroups
+# below the budget cut: their waves end after the look-back poll of every
+# workgroup's word and the stamps)
+print("per pass, us from entry: last stream end / look-back / walk / end;  latest-ending workgroups (wg: end, its last stream end, walk)")
+for p in range(P):
+    w = W[p].astype(np.int64)
+    t0 = w[:, 0].min()
+    u = (w - t0) / 100.0
+    wg_end = u[:, 5].reshape(256, 16).max(1)
+    wg_se = u[:, 2].reshape(256, 16).max(1)
+    wg_walk = u[:, 4].reshape(256, 16).max(1)
+    top = np.argsort(-wg_end)[:4]
+    print("  %.1f / %.1f / %.1f / %.1f  " % (u[:, 2].max(), u[:, 3].max(), u[:, 4].max(), u[:, 5].max()) +
+          "  ".join("wg%d: %.1f (%.1f, %.1f)" % (g, wg_end[g], wg_se[g], wg_walk[g]) for g in top))
+stampers = W[-1][:, 5].reshape(256, 16).max(1) - W[-1][:, 4].reshape(256, 16).max(1) > 0
+print("last pass: workgroups whose end follows their walk (stampers): %d; the latest stream end's workgroup: %d"
+      % (int(stampers.sum()), int(np.argmax(((W[-1][:, 2] - W[-1][:, 0].min()) / 100.0).reshape(256, 16).max(1)))))
